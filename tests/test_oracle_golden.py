@@ -1,0 +1,82 @@
+"""Pin the CPU oracle (oracle/kge_oracle.py) to the reference's own outputs.
+
+The fixtures in tests/golden/ were produced by running the reference LibKGE
+(tests/golden/make_golden.py).  The oracle must reproduce them: bit-exactly for the
+dyadic regime (where every fp32 sum is exact) and within 1e-6 of the row max otherwise;
+eval ranks must be identical in both regimes, chunked and unchunked.
+"""
+import glob
+import json
+import os
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN
+from oracle import kge_oracle as K
+
+SCORER_FILES = sorted(glob.glob(os.path.join(GOLDEN, "scorer_*.npz")))
+
+
+def _rel_err(x, ref):
+    scale = np.abs(ref).max(axis=-1, keepdims=True) if ref.ndim == 2 else np.abs(ref).max()
+    return float((np.abs(x - ref) / np.maximum(scale, 1e-30)).max())
+
+
+@pytest.mark.parametrize("fn", SCORER_FILES, ids=lambda f: os.path.basename(f)[7:-4])
+def test_scorer_outputs(fn):
+    f = np.load(fn)
+    meta = json.loads(str(f["meta"]))
+    out = K.model_scores(meta["model"], f["ent"], f["rel"], f["s"], f["p"], f["o"],
+                         f["subset"], meta["l_norm"] or 1.0)
+    exact = meta["regime"] == "dyadic" and meta["model"] in K.BILINEAR
+    for k, v in out.items():
+        ref = f[k]
+        assert v.shape == ref.shape, k
+        if exact:
+            np.testing.assert_array_equal(v.astype(np.float32), ref, err_msg=k)
+        else:
+            assert _rel_err(v, ref) < 1e-6, k
+
+
+@pytest.mark.parametrize("fn", SCORER_FILES, ids=lambda f: os.path.basename(f)[7:-4])
+def test_scorer_gradients(fn):
+    f = np.load(fn)
+    meta = json.loads(str(f["meta"]))
+    ge, gr = K.model_grads(meta["model"], f["ent"], f["rel"], f["s"], f["p"], f["o"],
+                           f["w_sp"].astype(np.float64), f["w_po"].astype(np.float64),
+                           f["w_spo"].astype(np.float64), meta["l_norm"] or 1.0)
+    assert np.abs(ge - f["g_ent"]).max() <= 1e-6 * np.abs(f["g_ent"]).max()
+    assert np.abs(gr - f["g_rel"]).max() <= 1e-6 * np.abs(f["g_rel"]).max()
+
+
+@pytest.mark.parametrize("regime", ["dyadic", "normal"])
+@pytest.mark.parametrize("tag", ["full", "chunk8"])
+def test_entity_ranking(regime, tag):
+    f = np.load(os.path.join(GOLDEN, f"eval_{regime}.npz"))
+    meta = json.loads(str(f["meta"]))
+    ref_metrics = json.loads(str(f["metrics"]))[tag]
+    splits = {k: f["tri_" + k] for k in ("train", "valid", "test")}
+    chunk = -1 if tag == "full" else meta["chunk8"]
+    ranks, metrics = K.entity_ranking("complex", f["ent"], f["rel"], splits,
+                                      batch_size=meta["batch_size"], chunk_size=chunk)
+    for k, v in ranks.items():
+        np.testing.assert_array_equal(v, f[f"{tag}_{k}"], err_msg=k)
+    assert set(metrics) == set(ref_metrics)
+    for k, v in metrics.items():
+        assert v == pytest.approx(ref_metrics[k], rel=1e-6, abs=1e-9), k
+
+
+def test_train_1vsall():
+    f = np.load(os.path.join(GOLDEN, "train1vsall_complex.npz"))
+    losses, e1, r1 = K.train_1vsall("complex", f["ent0"], f["rel0"], f["batches"], lr=0.2)
+    np.testing.assert_allclose(losses, f["losses"], rtol=1e-6)
+    np.testing.assert_allclose(e1, f["ent1"], atol=2e-5)
+    np.testing.assert_allclose(r1, f["rel1"], atol=2e-5)
+
+
+def test_relation_dims():
+    rows = json.loads(str(np.load(os.path.join(GOLDEN, "shapes.npz"))["table"]))
+    for model, d, d_e, d_r in rows:
+        assert K.relation_dim(model, d) == d_r
+        assert d_e == d
