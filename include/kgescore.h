@@ -1,0 +1,163 @@
+/*
+ * kgescore.h -- C ABI of libkgescore.so, the MI355X (gfx950) scoring engine behind the
+ * LibKGE KgeModel / RelationalScorer plugin API.
+ *
+ * Conventions (all entry points):
+ *   - every pointer is a DEVICE pointer owned by the caller (no allocation inside,
+ *     except the entry points that say otherwise); tables are fp32 row-major with an
+ *     explicit leading dimension in elements; indexes are int64;
+ *   - `stream` is a hipStream_t passed as void* (PyTorch-ROCm's current stream);
+ *     launches are asynchronous, no host synchronisation happens inside;
+ *   - the return value is 0 on success, otherwise a hipError_t or one of the
+ *     KGE_ERR_* codes below; kge_error_string() turns it into text.  The Python layer
+ *     raises RuntimeError / ValueError on a non-zero status (reference error
+ *     conventions: kge_model.py:155-180 asserts / ValueError).
+ *
+ * Which reference interface each entry point replaces is cited per function
+ * (file:line into the reference checkout, kge/...).
+ */
+#ifndef KGESCORE_H
+#define KGESCORE_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- enums ------------------------------------------------------------------- */
+#define KGE_COMPLEX 0  /* kge/model/complex.py            */
+#define KGE_DISTMULT 1 /* kge/model/distmult.py           */
+#define KGE_RESCAL 2   /* kge/model/rescal.py             */
+#define KGE_TRANSE 3   /* kge/model/transe.py             */
+#define KGE_ROTATE 4   /* kge/model/rotate.py             */
+
+#define KGE_DIR_SP 0 /* (s, p, ?): combine="sp_" */
+#define KGE_DIR_PO 1 /* (?, p, o): combine="_po" */
+
+#define KGE_PREC_FP32 0   /* fp32-input MFMA (v_mfma_f32_32x32x2_f32): exact f32 FMA chain */
+#define KGE_PREC_BF16X3 1 /* split-bf16 MFMA, hi*hi + hi*lo + lo*hi: ~2^-16 rel. per product */
+
+#define KGE_DIST_L1 0     /* sum_k |q_k - e_k|                                   */
+#define KGE_DIST_L2 1     /* sqrt(sum_k (q_k - e_k)^2)                           */
+#define KGE_DIST_ROT_L1 2 /* sum_k |q_k - e_k|_C  over complex pairs [re|im]       */
+#define KGE_DIST_ROT_L2 3 /* sqrt(sum_k |q_k - e_k|_C^2)                           */
+
+#define KGE_TIE_ROUNDED_MEAN 0 /* entity_ranking.tie_handling (entity_ranking.py:531-551) */
+#define KGE_TIE_BEST 1
+#define KGE_TIE_WORST 2
+
+#define KGE_ERR_ARG 1001     /* invalid argument (shape, enum, null pointer) */
+#define KGE_ERR_ALIGN 1002   /* pointer / leading dimension alignment        */
+#define KGE_ERR_NOGPU 1003   /* no gfx950 device visible                      */
+
+int kge_version(void);
+const char* kge_error_string(int status);
+
+/* ---- query preparation (fused LookupEmbedder gather) --------------------------
+ * Q[i, :] = prep(model, dir, ent[eidx[i]], rel[ridx[i]])      i in [0, n)
+ * eidx / ridx may be NULL (row i is then taken as row i: score_emb on embeddings).
+ *   dir = SP: complex cmul(s, r)            complex.py:31-38
+ *             distmult s*r                  distmult.py:83
+ *             rescal   s^T M_r              rescal.py:145-151
+ *             transe   s + r                transe.py:223
+ *             rotate   s * rot(r)           rotate.py:288-297
+ *   dir = PO: complex conj(r)*o             complex.py:40
+ *             distmult o*r                  distmult.py:85
+ *             rescal   M_r o                rescal.py:152-157
+ *             transe   o - r                transe.py:225
+ *             rotate   o * conj(rot(r))     rotate.py:298-307 (|e*rot - o| = |e - o*conj(rot)|)
+ * Replaces LookupEmbedder.embed (lookup_embedder.py:91-92) + the per-scorer prologue.
+ */
+int kge_prep_query(int model, int dir, const float* ent, int64_t ld_ent,
+                   const int64_t* eidx, const float* rel, int64_t ld_rel,
+                   const int64_t* ridx, int64_t n, int d_e, int d_r, float* q,
+                   int64_t ldq, void* stream);
+
+/* backward of kge_prep_query: scatter-adds dL/d(ent row) and dL/d(rel row) into
+ * d_ent / d_rel (atomic fp32 adds; either may be NULL to skip). */
+int kge_prep_query_bwd(int model, int dir, const float* ent, int64_t ld_ent,
+                       const int64_t* eidx, const float* rel, int64_t ld_rel,
+                       const int64_t* ridx, int64_t n, int d_e, int d_r,
+                       const float* dq, int64_t lddq, float* d_ent, int64_t ld_dent,
+                       float* d_rel, int64_t ld_drel, void* stream);
+
+/* ---- all-entities contraction (bilinear models) --------------------------------
+ * S[i, j] = sum_k Q[i, k] * T[row(j), k],  row(j) = tidx ? tidx[j] : j
+ * i in [0, n), j in [0, m), k in [0, d).  Output leading dim lds.
+ * Replaces the mm in complex.py:38,40 / distmult.py:83,85 / rescal.py:150,156.
+ */
+int kge_score_dot(const float* q, int64_t ldq, const float* t, int64_t ldt,
+                  const int64_t* tidx, int64_t n, int64_t m, int d, float* s,
+                  int64_t lds, int precision, void* stream);
+
+/* dQ[i, k] (+)= sum_j G[i, j] * T[row(j), k]   (accumulate != 0: add into dQ) */
+int kge_score_dot_bwd_q(const float* g, int64_t ldg, const float* t, int64_t ldt,
+                        const int64_t* tidx, int64_t n, int64_t m, int d, float* dq,
+                        int64_t lddq, int accumulate, int precision, void* stream);
+
+/* dT[row(j), k] += sum_i G[i, j] * Q[i, k]   (always accumulates; rows scattered
+ * atomically when tidx != NULL) */
+int kge_score_dot_bwd_t(const float* g, int64_t ldg, const float* q, int64_t ldq,
+                        const int64_t* tidx, int64_t n, int64_t m, int d, float* dt,
+                        int64_t lddt, int precision, void* stream);
+
+/* ---- all-entities distance scoring (TransE, RotatE; VALU, no MFMA) -------------
+ * S[i, j] = sign * dist_kind(Q[i, :], T[row(j), :])
+ * Replaces torch.cdist in transe.py:223,225 and the pairwise tensors of rotate.py:288-307.
+ */
+int kge_score_dist(int kind, float sign, const float* q, int64_t ldq, const float* t,
+                   int64_t ldt, const int64_t* tidx, int64_t n, int64_t m, int d,
+                   float* s, int64_t lds, void* stream);
+
+/* dQ[i,:] (+)= sum_j G[i,j] * d dist/dq ;  dT[row(j),:] += sum_i G[i,j] * d dist/de */
+int kge_score_dist_bwd(int kind, float sign, const float* g, int64_t ldg,
+                       const float* q, int64_t ldq, const float* t, int64_t ldt,
+                       const int64_t* tidx, int64_t n, int64_t m, int d, float* dq,
+                       int64_t lddq, float* dt, int64_t lddt, void* stream);
+
+/* ---- row-wise triple scores ------------------------------------------------------
+ * out[i] = score(ent[sidx[i]], rel[pidx[i]], ent[oidx[i]])      (combine="spo")
+ * Replaces KgeModel.score_spo (kge_model.py:620-637) for the five scorers.  TransE uses
+ * F.pairwise_distance semantics (|s+p-o+1e-6|, transe.py:221).
+ */
+int kge_score_spo(int model, float l_norm, const float* ent, int64_t ld_ent,
+                  const int64_t* sidx, const float* rel, int64_t ld_rel,
+                  const int64_t* pidx, const int64_t* oidx, int64_t n, int d_e, int d_r,
+                  float* out, void* stream);
+
+/* backward of kge_score_spo: scatter-adds g[i] * d score / d rows into d_ent, d_rel */
+int kge_score_spo_bwd(int model, float l_norm, const float* ent, int64_t ld_ent,
+                      const int64_t* sidx, const float* rel, int64_t ld_rel,
+                      const int64_t* pidx, const int64_t* oidx, int64_t n, int d_e,
+                      int d_r, const float* g, float* d_ent, int64_t ld_dent,
+                      float* d_rel, int64_t ld_drel, void* stream);
+
+/* ---- entity-ranking counts (eval) --------------------------------------------------
+ * For row i of a score chunk S[n, m] covering entities [c0, c0 + m):
+ *   v_j = S[i, j], with v_{true_i - c0} := true_score[i] when true_i is in the chunk;
+ *   NaN -> -inf, filtered entries -> -inf (entity_ranking.py:172-177, 497-502, 519-523).
+ *   greater[r, i] += #{j : v_j > t_i},  ties[r, i] += #{j : v_j == t_i}
+ * for ranking r in {0: raw, 1: filtered by F, 2: filtered by F u T}.
+ * F and T are CSR lists of GLOBAL entity ids per row (f_ptr[n+1], f_col[...]); each
+ * list must hold unique ids; T entries that are also in F are ignored; the true entity
+ * itself is never filtered.  t_ptr may be NULL (only rankings 0 and 1 are produced).
+ * Counts accumulate (+=) so chunks / shards sum exactly (entity_ranking.py:153-216).
+ * Replaces _filter_and_rank / _get_ranks_and_num_ties (entity_ranking.py:469-529).
+ */
+int kge_rank_counts(const float* s, int64_t lds, int64_t n, int64_t m, int64_t c0,
+                    const int64_t* true_idx, const float* true_score,
+                    const int64_t* f_ptr, const int64_t* f_col, const int64_t* t_ptr,
+                    const int64_t* t_col, int64_t* greater, int64_t* ties,
+                    void* stream);
+
+/* ranks[i] = tie rule(greater[i], ties[i]) and hist[ranks[i]] += 1 (float histogram
+ * of length hist_len, eval.py:148-171); ranks may be NULL. */
+int kge_rank_hist(const int64_t* greater, const int64_t* ties, int64_t n,
+                  int tie_handling, int64_t* ranks, float* hist, int64_t hist_len,
+                  void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* KGESCORE_H */

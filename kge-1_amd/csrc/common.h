@@ -1,0 +1,71 @@
+// Shared device helpers for libkgescore (gfx950 / CDNA4 only).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <algorithm>
+
+#include "../../include/kgescore.h"
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+#define KGE_WAVE 64
+
+#define KGE_CHECK_LAUNCH()                                   \
+  do {                                                       \
+    hipError_t _e = hipGetLastError();                       \
+    if (_e != hipSuccess) return (int)_e;                    \
+  } while (0)
+
+#define KGE_REQUIRE(cond) \
+  do {                    \
+    if (!(cond)) return KGE_ERR_ARG; \
+  } while (0)
+
+static inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
+
+static inline bool aligned16(const void* p) {
+  return (reinterpret_cast<uintptr_t>(p) & 15u) == 0;
+}
+
+// Split an fp32 value into bf16 hi + bf16 lo with x ~= hi + lo (|x - hi - lo| <= 2^-16 |x|).
+__device__ __forceinline__ void split_bf16(float x, __bf16& hi, __bf16& lo) {
+  hi = (__bf16)x;
+  lo = (__bf16)(x - (float)hi);
+}
+
+// Split four fp32 values into bf16x4 hi / lo planes.
+__device__ __forceinline__ void split_bf16x4(const float4& v, bf16x4& hi, bf16x4& lo) {
+  const float x[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    const __bf16 h = (__bf16)x[c];
+    hi[c] = h;
+    lo[c] = (__bf16)(x[c] - (float)h);
+  }
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+  return v;
+}
+
+template <typename T>
+__device__ __forceinline__ T ceil_div(T a, T b) {
+  return (a + b - 1) / b;
+}
+
+// Bijective XCD-aware remap of a 1-D block id (cdna_hip_programming.md §5 "XCD swizzle
+// must be bijective"): consecutive logical ids land on the same XCD, so tiles that share
+// an operand panel share that XCD's L2.  Placement is a speed hint only.
+__device__ __forceinline__ int xcd_remap(int bid, int nblocks) {
+  const int nx = 8;
+  int q = nblocks / nx, r = nblocks % nx;
+  int xcd = bid % nx, local = bid / nx;
+  int base = (xcd < r) ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q;
+  return base + local;
+}

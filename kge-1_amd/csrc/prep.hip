@@ -1,0 +1,298 @@
+// Query preparation (fused LookupEmbedder gather + per-model prologue) and its backward.
+//
+// Every in-scope scorer reduces to "per-query prep + one contraction (dot or distance)
+// against the entity table" (SURVEY.md §8a A6-A10).  These kernels produce the query
+// rows Q[n, d_e]; they are small (n * d work) next to the contraction.
+#include "common.h"
+
+namespace {
+
+struct Rows {
+  const float* e;
+  const float* r;
+};
+
+__device__ __forceinline__ Rows fetch_rows(const float* ent, int64_t ld_ent, const int64_t* eidx,
+                                           const float* rel, int64_t ld_rel, const int64_t* ridx,
+                                           int64_t i) {
+  const int64_t ei = eidx ? eidx[i] : i;
+  const int64_t ri = ridx ? ridx[i] : i;
+  return Rows{ent + ei * ld_ent, rel + ri * ld_rel};
+}
+
+// Elementwise models: complex / distmult / transe / rotate.  One block per query row.
+template <int MODEL, int DIR>
+__global__ void __launch_bounds__(256) prep_elementwise(const float* __restrict__ ent, int64_t ld_ent,
+                                                         const int64_t* __restrict__ eidx,
+                                                         const float* __restrict__ rel, int64_t ld_rel,
+                                                         const int64_t* __restrict__ ridx, int d_e,
+                                                         float* __restrict__ q, int64_t ldq) {
+  const int64_t i = blockIdx.x;
+  Rows rw = fetch_rows(ent, ld_ent, eidx, rel, ld_rel, ridx, i);
+  float* qi = q + i * ldq;
+  if (MODEL == KGE_COMPLEX || MODEL == KGE_ROTATE) {
+    const int h = d_e / 2;
+    for (int k = threadIdx.x; k < h; k += blockDim.x) {
+      const float a_re = rw.e[k], a_im = rw.e[k + h];
+      float c, s;
+      if (MODEL == KGE_COMPLEX) {
+        c = rw.r[k];
+        s = rw.r[k + h];
+      } else {
+        sincosf(rw.r[k], &s, &c);  // rotate.py:273 (radians -> unit complex)
+      }
+      if (DIR == KGE_DIR_SP) {  // a * (c + i s)
+        qi[k] = a_re * c - a_im * s;
+        qi[k + h] = a_re * s + a_im * c;
+      } else {  // conj(c + i s) * a
+        qi[k] = c * a_re + s * a_im;
+        qi[k + h] = c * a_im - s * a_re;
+      }
+    }
+  } else {
+    for (int k = threadIdx.x; k < d_e; k += blockDim.x) {
+      const float a = rw.e[k], b = rw.r[k];
+      if (MODEL == KGE_DISTMULT)
+        qi[k] = a * b;
+      else  // TRANSE
+        qi[k] = (DIR == KGE_DIR_SP) ? a + b : a - b;
+    }
+  }
+}
+
+// RESCAL: Q = s^T M (sp) or M o (po), M = rel row viewed as [d, d] row-major.
+template <int DIR>
+__global__ void __launch_bounds__(256) prep_rescal(const float* __restrict__ ent, int64_t ld_ent,
+                                                    const int64_t* __restrict__ eidx,
+                                                    const float* __restrict__ rel, int64_t ld_rel,
+                                                    const int64_t* __restrict__ ridx, int d,
+                                                    float* __restrict__ q, int64_t ldq) {
+  extern __shared__ float xs[];
+  const int64_t i = blockIdx.x;
+  Rows rw = fetch_rows(ent, ld_ent, eidx, rel, ld_rel, ridx, i);
+  for (int k = threadIdx.x; k < d; k += blockDim.x) xs[k] = rw.e[k];
+  __syncthreads();
+  float* qi = q + i * ldq;
+  if (DIR == KGE_DIR_SP) {  // q_j = sum_a x_a M[a][j]  (coalesced over j)
+    for (int j = threadIdx.x; j < d; j += blockDim.x) {
+      float acc = 0.f;
+      for (int a = 0; a < d; ++a) acc = fmaf(xs[a], rw.r[(int64_t)a * d + j], acc);
+      qi[j] = acc;
+    }
+  } else {  // q_a = sum_j M[a][j] x_j : one wave per output row
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    for (int a = wave; a < d; a += nw) {
+      float acc = 0.f;
+      for (int j = lane; j < d; j += 64) acc = fmaf(rw.r[(int64_t)a * d + j], xs[j], acc);
+      acc = wave_sum(acc);
+      if (lane == 0) qi[a] = acc;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------- backward
+__device__ __forceinline__ void atomic_add_row(float* base, int k, float v) {
+  if (base) atomicAdd(base + k, v);
+}
+
+template <int MODEL, int DIR>
+__global__ void __launch_bounds__(256) prep_elementwise_bwd(
+    const float* __restrict__ ent, int64_t ld_ent, const int64_t* __restrict__ eidx,
+    const float* __restrict__ rel, int64_t ld_rel, const int64_t* __restrict__ ridx, int d_e,
+    const float* __restrict__ dq, int64_t lddq, float* d_ent, int64_t ld_dent, float* d_rel,
+    int64_t ld_drel) {
+  const int64_t i = blockIdx.x;
+  Rows rw = fetch_rows(ent, ld_ent, eidx, rel, ld_rel, ridx, i);
+  const float* g = dq + i * lddq;
+  float* ge = d_ent ? d_ent + (eidx ? eidx[i] : i) * ld_dent : nullptr;
+  float* gr = d_rel ? d_rel + (ridx ? ridx[i] : i) * ld_drel : nullptr;
+  if (MODEL == KGE_COMPLEX) {
+    const int h = d_e / 2;
+    for (int k = threadIdx.x; k < h; k += blockDim.x) {
+      const float a_re = rw.e[k], a_im = rw.e[k + h], r_re = rw.r[k], r_im = rw.r[k + h];
+      const float g_re = g[k], g_im = g[k + h];
+      if (DIR == KGE_DIR_SP) {  // q = a*r: da = g*conj(r), dr = g*conj(a)
+        atomic_add_row(ge, k, g_re * r_re + g_im * r_im);
+        atomic_add_row(ge, k + h, g_im * r_re - g_re * r_im);
+        atomic_add_row(gr, k, g_re * a_re + g_im * a_im);
+        atomic_add_row(gr, k + h, g_im * a_re - g_re * a_im);
+      } else {  // q = conj(r)*a: da = g*r, dr = conj(g)*a
+        atomic_add_row(ge, k, g_re * r_re - g_im * r_im);
+        atomic_add_row(ge, k + h, g_re * r_im + g_im * r_re);
+        atomic_add_row(gr, k, g_re * a_re + g_im * a_im);
+        atomic_add_row(gr, k + h, g_re * a_im - g_im * a_re);
+      }
+    }
+  } else if (MODEL == KGE_ROTATE) {
+    const int h = d_e / 2;
+    for (int k = threadIdx.x; k < h; k += blockDim.x) {
+      const float a_re = rw.e[k], a_im = rw.e[k + h];
+      float c, s;
+      sincosf(rw.r[k], &s, &c);
+      const float g_re = g[k], g_im = g[k + h];
+      if (DIR == KGE_DIR_SP) {  // q = a*rot: da = g*conj(rot), dtheta = g_re(-q_im) + g_im q_re
+        const float q_re = a_re * c - a_im * s, q_im = a_re * s + a_im * c;
+        atomic_add_row(ge, k, g_re * c + g_im * s);
+        atomic_add_row(ge, k + h, g_im * c - g_re * s);
+        atomic_add_row(gr, k, g_im * q_re - g_re * q_im);
+      } else {  // q = a*conj(rot): da = g*rot, dtheta = g_re q_im - g_im q_re
+        const float q_re = c * a_re + s * a_im, q_im = c * a_im - s * a_re;
+        atomic_add_row(ge, k, g_re * c - g_im * s);
+        atomic_add_row(ge, k + h, g_re * s + g_im * c);
+        atomic_add_row(gr, k, g_re * q_im - g_im * q_re);
+      }
+    }
+  } else {
+    for (int k = threadIdx.x; k < d_e; k += blockDim.x) {
+      const float a = rw.e[k], b = rw.r[k], gk = g[k];
+      if (MODEL == KGE_DISTMULT) {
+        atomic_add_row(ge, k, gk * b);
+        atomic_add_row(gr, k, gk * a);
+      } else {  // TRANSE: q = a + b (sp) / a - b (po)
+        atomic_add_row(ge, k, gk);
+        atomic_add_row(gr, k, DIR == KGE_DIR_SP ? gk : -gk);
+      }
+    }
+  }
+}
+
+template <int DIR>
+__global__ void __launch_bounds__(256) prep_rescal_bwd(
+    const float* __restrict__ ent, int64_t ld_ent, const int64_t* __restrict__ eidx,
+    const float* __restrict__ rel, int64_t ld_rel, const int64_t* __restrict__ ridx, int d,
+    const float* __restrict__ dq, int64_t lddq, float* d_ent, int64_t ld_dent, float* d_rel,
+    int64_t ld_drel) {
+  extern __shared__ float sm[];
+  float* xs = sm;      // entity row
+  float* gs = sm + d;  // dq row
+  const int64_t i = blockIdx.x;
+  Rows rw = fetch_rows(ent, ld_ent, eidx, rel, ld_rel, ridx, i);
+  for (int k = threadIdx.x; k < d; k += blockDim.x) {
+    xs[k] = rw.e[k];
+    gs[k] = dq[i * lddq + k];
+  }
+  __syncthreads();
+  float* ge = d_ent ? d_ent + (eidx ? eidx[i] : i) * ld_dent : nullptr;
+  float* gr = d_rel ? d_rel + (ridx ? ridx[i] : i) * ld_drel : nullptr;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  // dM[a][b] = x_a g_b (sp) or g_a x_b (po)
+  if (gr) {
+    for (int64_t t = threadIdx.x; t < (int64_t)d * d; t += blockDim.x) {
+      const int a = (int)(t / d), b = (int)(t % d);
+      atomicAdd(gr + t, DIR == KGE_DIR_SP ? xs[a] * gs[b] : gs[a] * xs[b]);
+    }
+  }
+  if (ge) {
+    if (DIR == KGE_DIR_SP) {  // dx_a = sum_b M[a][b] g_b
+      for (int a = wave; a < d; a += nw) {
+        float acc = 0.f;
+        for (int b = lane; b < d; b += 64) acc = fmaf(rw.r[(int64_t)a * d + b], gs[b], acc);
+        acc = wave_sum(acc);
+        if (lane == 0) atomicAdd(ge + a, acc);
+      }
+    } else {  // dx_b = sum_a M[a][b] g_a
+      for (int b = threadIdx.x; b < d; b += blockDim.x) {
+        float acc = 0.f;
+        for (int a = 0; a < d; ++a) acc = fmaf(rw.r[(int64_t)a * d + b], gs[a], acc);
+        atomicAdd(ge + b, acc);
+      }
+    }
+  }
+}
+
+template <int DIR>
+int launch_prep(int model, const float* ent, int64_t ld_ent, const int64_t* eidx, const float* rel,
+                int64_t ld_rel, const int64_t* ridx, int64_t n, int d_e, float* q, int64_t ldq,
+                hipStream_t st) {
+  dim3 grid((unsigned)n), block(256);
+  switch (model) {
+    case KGE_COMPLEX:
+      prep_elementwise<KGE_COMPLEX, DIR><<<grid, block, 0, st>>>(ent, ld_ent, eidx, rel, ld_rel, ridx, d_e, q, ldq);
+      break;
+    case KGE_DISTMULT:
+      prep_elementwise<KGE_DISTMULT, DIR><<<grid, block, 0, st>>>(ent, ld_ent, eidx, rel, ld_rel, ridx, d_e, q, ldq);
+      break;
+    case KGE_TRANSE:
+      prep_elementwise<KGE_TRANSE, DIR><<<grid, block, 0, st>>>(ent, ld_ent, eidx, rel, ld_rel, ridx, d_e, q, ldq);
+      break;
+    case KGE_ROTATE:
+      prep_elementwise<KGE_ROTATE, DIR><<<grid, block, 0, st>>>(ent, ld_ent, eidx, rel, ld_rel, ridx, d_e, q, ldq);
+      break;
+    case KGE_RESCAL:
+      prep_rescal<DIR><<<grid, block, d_e * sizeof(float), st>>>(ent, ld_ent, eidx, rel, ld_rel, ridx, d_e, q, ldq);
+      break;
+    default:
+      return KGE_ERR_ARG;
+  }
+  KGE_CHECK_LAUNCH();
+  return 0;
+}
+
+template <int DIR>
+int launch_prep_bwd(int model, const float* ent, int64_t ld_ent, const int64_t* eidx, const float* rel,
+                    int64_t ld_rel, const int64_t* ridx, int64_t n, int d_e, const float* dq,
+                    int64_t lddq, float* d_ent, int64_t ld_dent, float* d_rel, int64_t ld_drel,
+                    hipStream_t st) {
+  dim3 grid((unsigned)n), block(256);
+#define KGE_PB(M)                                                                          \
+  prep_elementwise_bwd<M, DIR><<<grid, block, 0, st>>>(ent, ld_ent, eidx, rel, ld_rel, ridx, \
+                                                       d_e, dq, lddq, d_ent, ld_dent, d_rel, ld_drel)
+  switch (model) {
+    case KGE_COMPLEX: KGE_PB(KGE_COMPLEX); break;
+    case KGE_DISTMULT: KGE_PB(KGE_DISTMULT); break;
+    case KGE_TRANSE: KGE_PB(KGE_TRANSE); break;
+    case KGE_ROTATE: KGE_PB(KGE_ROTATE); break;
+    case KGE_RESCAL:
+      prep_rescal_bwd<DIR><<<grid, block, 2 * d_e * sizeof(float), st>>>(
+          ent, ld_ent, eidx, rel, ld_rel, ridx, d_e, dq, lddq, d_ent, ld_dent, d_rel, ld_drel);
+      break;
+    default:
+      return KGE_ERR_ARG;
+  }
+#undef KGE_PB
+  KGE_CHECK_LAUNCH();
+  return 0;
+}
+
+int check_dims(int model, int d_e, int d_r) {
+  if (d_e <= 0) return KGE_ERR_ARG;
+  switch (model) {
+    case KGE_COMPLEX: return (d_e % 2 == 0 && d_r == d_e) ? 0 : KGE_ERR_ARG;
+    case KGE_DISTMULT:
+    case KGE_TRANSE: return d_r == d_e ? 0 : KGE_ERR_ARG;
+    case KGE_ROTATE: return (d_e % 2 == 0 && d_r == d_e / 2) ? 0 : KGE_ERR_ARG;
+    case KGE_RESCAL: return (d_r == d_e * d_e && d_e <= 8192) ? 0 : KGE_ERR_ARG;
+    default: return KGE_ERR_ARG;
+  }
+}
+
+}  // namespace
+
+extern "C" int kge_prep_query(int model, int dir, const float* ent, int64_t ld_ent, const int64_t* eidx,
+                              const float* rel, int64_t ld_rel, const int64_t* ridx, int64_t n, int d_e,
+                              int d_r, float* q, int64_t ldq, void* stream) {
+  if (int e = check_dims(model, d_e, d_r)) return e;
+  KGE_REQUIRE(n >= 0 && ent && rel && q && ldq >= d_e);
+  if (n == 0) return 0;
+  hipStream_t st = as_stream(stream);
+  if (dir == KGE_DIR_SP) return launch_prep<KGE_DIR_SP>(model, ent, ld_ent, eidx, rel, ld_rel, ridx, n, d_e, q, ldq, st);
+  if (dir == KGE_DIR_PO) return launch_prep<KGE_DIR_PO>(model, ent, ld_ent, eidx, rel, ld_rel, ridx, n, d_e, q, ldq, st);
+  return KGE_ERR_ARG;
+}
+
+extern "C" int kge_prep_query_bwd(int model, int dir, const float* ent, int64_t ld_ent, const int64_t* eidx,
+                                  const float* rel, int64_t ld_rel, const int64_t* ridx, int64_t n, int d_e,
+                                  int d_r, const float* dq, int64_t lddq, float* d_ent, int64_t ld_dent,
+                                  float* d_rel, int64_t ld_drel, void* stream) {
+  if (int e = check_dims(model, d_e, d_r)) return e;
+  KGE_REQUIRE(n >= 0 && ent && rel && dq);
+  if (n == 0 || (!d_ent && !d_rel)) return 0;
+  hipStream_t st = as_stream(stream);
+  if (dir == KGE_DIR_SP)
+    return launch_prep_bwd<KGE_DIR_SP>(model, ent, ld_ent, eidx, rel, ld_rel, ridx, n, d_e, dq, lddq, d_ent,
+                                       ld_dent, d_rel, ld_drel, st);
+  if (dir == KGE_DIR_PO)
+    return launch_prep_bwd<KGE_DIR_PO>(model, ent, ld_ent, eidx, rel, ld_rel, ridx, n, d_e, dq, lddq, d_ent,
+                                       ld_dent, d_rel, ld_drel, st);
+  return KGE_ERR_ARG;
+}

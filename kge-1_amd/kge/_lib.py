@@ -1,0 +1,211 @@
+"""ctypes binding of libkgescore.so (the gfx950 HIP engine, C ABI in include/kgescore.h).
+
+There is deliberately no fallback: if the library is missing, or a tensor is not on a
+ROCm device, the call raises.  Tensors are passed as raw device pointers with explicit
+leading dimensions; launches go on PyTorch's current HIP stream.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from typing import Optional
+
+import torch
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libkgescore.so")
+
+# enums (kgescore.h)
+COMPLEX, DISTMULT, RESCAL, TRANSE, ROTATE = range(5)
+DIR_SP, DIR_PO = 0, 1
+PREC_FP32, PREC_BF16X3 = 0, 1
+DIST_L1, DIST_L2, DIST_ROT_L1, DIST_ROT_L2 = range(4)
+TIE = {"rounded_mean_rank": 0, "best_rank": 1, "worst_rank": 2}
+PRECISIONS = {"fp32": PREC_FP32, "bf16x3": PREC_BF16X3}
+
+_P = ctypes.c_void_p
+_I64 = ctypes.c_int64
+_I = ctypes.c_int
+_F = ctypes.c_float
+
+SIGNATURES = {
+    "kge_version": ([], _I),
+    "kge_error_string": ([_I], ctypes.c_char_p),
+    "kge_prep_query": ([_I, _I, _P, _I64, _P, _P, _I64, _P, _I64, _I, _I, _P, _I64, _P], _I),
+    "kge_prep_query_bwd": ([_I, _I, _P, _I64, _P, _P, _I64, _P, _I64, _I, _I, _P, _I64, _P, _I64,
+                            _P, _I64, _P], _I),
+    "kge_score_dot": ([_P, _I64, _P, _I64, _P, _I64, _I64, _I, _P, _I64, _I, _P], _I),
+    "kge_score_dot_bwd_q": ([_P, _I64, _P, _I64, _P, _I64, _I64, _I, _P, _I64, _I, _I, _P], _I),
+    "kge_score_dot_bwd_t": ([_P, _I64, _P, _I64, _P, _I64, _I64, _I, _P, _I64, _I, _P], _I),
+    "kge_score_dist": ([_I, _F, _P, _I64, _P, _I64, _P, _I64, _I64, _I, _P, _I64, _P], _I),
+    "kge_score_dist_bwd": ([_I, _F, _P, _I64, _P, _I64, _P, _I64, _P, _I64, _I64, _I, _P, _I64, _P,
+                            _I64, _P], _I),
+    "kge_score_spo": ([_I, _F, _P, _I64, _P, _P, _I64, _P, _P, _I64, _I, _I, _P, _P], _I),
+    "kge_score_spo_bwd": ([_I, _F, _P, _I64, _P, _P, _I64, _P, _P, _I64, _I, _I, _P, _P, _I64, _P,
+                           _I64, _P], _I),
+    "kge_rank_counts": ([_P, _I64, _I64, _I64, _I64, _P, _P, _P, _P, _P, _P, _P, _P, _P], _I),
+    "kge_rank_hist": ([_P, _P, _I64, _I, _P, _P, _I64, _P], _I),
+}
+
+_lib: Optional[ctypes.CDLL] = None
+
+
+class EngineError(RuntimeError):
+    pass
+
+
+def lib() -> ctypes.CDLL:
+    """Load libkgescore.so once; raise loudly if it is missing (no fallback path)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise EngineError(
+                f"libkgescore.so not found at {LIB_PATH}; build it with "
+                "`make -C kge-1_amd/csrc` (or __graft_entry__.build()). The MI355X "
+                "scoring engine has no CPU fallback.")
+        handle = ctypes.CDLL(LIB_PATH)
+        for name, (args, res) in SIGNATURES.items():
+            fn = getattr(handle, name)
+            fn.argtypes = args
+            fn.restype = res
+        _lib = handle
+    return _lib
+
+
+def _check(status: int, what: str):
+    if status != 0:
+        msg = lib().kge_error_string(status).decode()
+        if status == 1001:
+            raise ValueError(f"{what}: {msg}")
+        raise EngineError(f"{what} failed ({status}): {msg}")
+
+
+def ptr(t: Optional[torch.Tensor]) -> Optional[int]:
+    return None if t is None else t.data_ptr()
+
+
+def stream() -> int:
+    return torch.cuda.current_stream().cuda_stream
+
+
+def require_device(*tensors):
+    for t in tensors:
+        if t is None:
+            continue
+        if not t.is_cuda:
+            raise EngineError(
+                "kge-1_amd scores on the MI355X (gfx950) HIP engine only; got a tensor on "
+                f"{t.device}. Set job.device to a ROCm device ('cuda' / 'cuda:N').")
+
+
+def rows(t: torch.Tensor) -> int:
+    """Leading dimension (elements) of a row-major 2-D fp32 tensor with unit col stride."""
+    if t.dtype != torch.float32:
+        raise ValueError(f"expected float32, got {t.dtype}")
+    if t.dim() != 2 or t.stride(1) != 1:
+        raise ValueError("expected a 2-D tensor with contiguous rows")
+    return t.stride(0)
+
+
+def idx64(t: Optional[torch.Tensor]) -> Optional[torch.Tensor]:
+    if t is None:
+        return None
+    t = t.reshape(-1)
+    if t.dtype != torch.int64:
+        t = t.long()
+    return t.contiguous()
+
+
+# ------------------------------------------------------------------ thin wrappers
+
+
+def prep_query(model, direction, ent, eidx, rel, ridx, n, d_e, d_r, out=None):
+    require_device(ent, rel)
+    q = out if out is not None else torch.empty(n, d_e, device=ent.device, dtype=torch.float32)
+    _check(lib().kge_prep_query(model, direction, ptr(ent), rows(ent), ptr(eidx), ptr(rel), rows(rel),
+                                ptr(ridx), n, d_e, d_r, ptr(q), rows(q), stream()), "kge_prep_query")
+    return q
+
+
+def prep_query_bwd(model, direction, ent, eidx, rel, ridx, n, d_e, d_r, dq, d_ent, d_rel):
+    _check(lib().kge_prep_query_bwd(
+        model, direction, ptr(ent), rows(ent), ptr(eidx), ptr(rel), rows(rel), ptr(ridx), n, d_e, d_r,
+        ptr(dq), rows(dq), ptr(d_ent), rows(d_ent) if d_ent is not None else 0, ptr(d_rel),
+        rows(d_rel) if d_rel is not None else 0, stream()), "kge_prep_query_bwd")
+
+
+def score_dot(q, t, tidx, precision, out=None):
+    require_device(q, t)
+    n, d = q.shape
+    m = tidx.numel() if tidx is not None else t.shape[0]
+    s = out if out is not None else torch.empty(n, m, device=q.device, dtype=torch.float32)
+    _check(lib().kge_score_dot(ptr(q), rows(q), ptr(t), rows(t), ptr(tidx), n, m, d, ptr(s), rows(s),
+                               precision, stream()), "kge_score_dot")
+    return s
+
+
+def score_dot_bwd_q(g, t, tidx, precision, dq=None, accumulate=False):
+    n, m = g.shape
+    d = t.shape[1]
+    if dq is None:
+        dq = torch.empty(n, d, device=g.device, dtype=torch.float32)
+        accumulate = False
+    _check(lib().kge_score_dot_bwd_q(ptr(g), rows(g), ptr(t), rows(t), ptr(tidx), n, m, d, ptr(dq),
+                                     rows(dq), int(accumulate), precision, stream()), "kge_score_dot_bwd_q")
+    return dq
+
+
+def score_dot_bwd_t(g, q, tidx, dt, precision):
+    n, m = g.shape
+    d = q.shape[1]
+    _check(lib().kge_score_dot_bwd_t(ptr(g), rows(g), ptr(q), rows(q), ptr(tidx), n, m, d, ptr(dt),
+                                     rows(dt), precision, stream()), "kge_score_dot_bwd_t")
+    return dt
+
+
+def score_dist(kind, sign, q, t, tidx, out=None):
+    require_device(q, t)
+    n, d = q.shape
+    m = tidx.numel() if tidx is not None else t.shape[0]
+    s = out if out is not None else torch.empty(n, m, device=q.device, dtype=torch.float32)
+    _check(lib().kge_score_dist(kind, sign, ptr(q), rows(q), ptr(t), rows(t), ptr(tidx), n, m, d, ptr(s),
+                                rows(s), stream()), "kge_score_dist")
+    return s
+
+
+def score_dist_bwd(kind, sign, g, q, t, tidx, dq, dt):
+    n, m = g.shape
+    d = q.shape[1]
+    _check(lib().kge_score_dist_bwd(kind, sign, ptr(g), rows(g), ptr(q), rows(q), ptr(t), rows(t), ptr(tidx),
+                                    n, m, d, ptr(dq), rows(dq) if dq is not None else 0, ptr(dt),
+                                    rows(dt) if dt is not None else 0, stream()), "kge_score_dist_bwd")
+
+
+def score_spo(model, l_norm, ent, sidx, rel, pidx, oidx, d_e, d_r, out=None):
+    require_device(ent, rel)
+    n = sidx.numel()
+    o = out if out is not None else torch.empty(n, device=ent.device, dtype=torch.float32)
+    _check(lib().kge_score_spo(model, float(l_norm), ptr(ent), rows(ent), ptr(sidx), ptr(rel), rows(rel),
+                               ptr(pidx), ptr(oidx), n, d_e, d_r, ptr(o), stream()), "kge_score_spo")
+    return o
+
+
+def score_spo_bwd(model, l_norm, ent, sidx, rel, pidx, oidx, d_e, d_r, g, d_ent, d_rel):
+    n = sidx.numel()
+    _check(lib().kge_score_spo_bwd(
+        model, float(l_norm), ptr(ent), rows(ent), ptr(sidx), ptr(rel), rows(rel), ptr(pidx), ptr(oidx), n,
+        d_e, d_r, ptr(g), ptr(d_ent), rows(d_ent) if d_ent is not None else 0, ptr(d_rel),
+        rows(d_rel) if d_rel is not None else 0, stream()), "kge_score_spo_bwd")
+
+
+def rank_counts(s, c0, true_idx, true_score, f_ptr, f_col, t_ptr, t_col, greater, ties):
+    n, m = s.shape
+    _check(lib().kge_rank_counts(ptr(s), rows(s), n, m, c0, ptr(true_idx), ptr(true_score), ptr(f_ptr),
+                                 ptr(f_col), ptr(t_ptr), ptr(t_col), ptr(greater), ptr(ties), stream()),
+           "kge_rank_counts")
+
+
+def rank_hist(greater, ties, tie_handling, ranks, hist):
+    n = greater.numel()
+    _check(lib().kge_rank_hist(ptr(greater), ptr(ties), n, TIE[tie_handling], ptr(ranks), ptr(hist),
+                               hist.numel() if hist is not None else 0, stream()), "kge_rank_hist")

@@ -1,0 +1,206 @@
+"""GPU parity of the C-ABI kernels (libkgescore.so) against the reference's golden
+vectors and the CPU oracle.  Every call goes through the C ABI via kge._lib.
+
+Tolerances (north star: 1e-4 relative to the row max, fp32):
+  * dyadic fixtures: bit-exact for the bilinear models in both precisions (all partial
+    sums are exact), bit-exact for TransE L1 sp_/_po;
+  * N(0, 0.1) fixtures: <= 2e-5 of the row max for bf16x3, <= 2e-6 for fp32, <= 1e-5
+    for the VALU distance kernels; gradients <= 1e-4 of the max |grad| (bf16x3) /
+    2e-6 (fp32).
+"""
+import glob
+import json
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import GOLDEN
+from oracle import kge_oracle as K
+
+pytestmark = pytest.mark.gpu
+
+MODEL_IDS = {"complex": 0, "distmult": 1, "rescal": 2, "transe": 3, "rotate": 4}
+SCORER_FILES = sorted(glob.glob(os.path.join(GOLDEN, "scorer_*.npz")))
+
+
+@pytest.fixture(scope="module")
+def L():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from kge import _lib
+    _lib.lib()
+    return _lib
+
+
+def dev(x, dtype=None):
+    t = torch.from_numpy(np.ascontiguousarray(x))
+    if dtype is not None:
+        t = t.to(dtype)
+    return t.cuda()
+
+
+def rel_err(x, ref):
+    x = np.asarray(x, np.float64)
+    ref = np.asarray(ref, np.float64)
+    scale = np.abs(ref).max(axis=-1, keepdims=True) if ref.ndim == 2 else np.abs(ref).max()
+    return float((np.abs(x - ref) / np.maximum(scale, 1e-30)).max())
+
+
+def dist_kind(model, l_norm):
+    if model == "transe":
+        return (0 if l_norm == 1 else 1), -1.0
+    return (2 if l_norm == 1 else 3), 1.0
+
+
+def forward_all(L, meta, f, prec):
+    model = meta["model"]
+    mk = MODEL_IDS[model]
+    ln = meta["l_norm"] or 1.0
+    ent, rel = dev(f["ent"]), dev(f["rel"])
+    s, p, o, sub = (dev(f[k], torch.int64) for k in ("s", "p", "o", "subset"))
+    d_e, d_r = ent.shape[1], rel.shape[1]
+    n = s.numel()
+    out = {}
+    q_sp = L.prep_query(mk, L.DIR_SP, ent, s, rel, p, n, d_e, d_r)
+    q_po = L.prep_query(mk, L.DIR_PO, ent, o, rel, p, n, d_e, d_r)
+    if model in K.BILINEAR:
+        out["sp_all"] = L.score_dot(q_sp, ent, None, prec)
+        out["po_all"] = L.score_dot(q_po, ent, None, prec)
+        out["sp_sub"] = L.score_dot(q_sp, ent, sub, prec)
+        out["po_sub"] = L.score_dot(q_po, ent, sub, prec)
+    else:
+        kind, sign = dist_kind(model, ln)
+        out["sp_all"] = L.score_dist(kind, sign, q_sp, ent, None)
+        out["po_all"] = L.score_dist(kind, sign, q_po, ent, None)
+        out["sp_sub"] = L.score_dist(kind, sign, q_sp, ent, sub)
+        out["po_sub"] = L.score_dist(kind, sign, q_po, ent, sub)
+    out["spo"] = L.score_spo(mk, ln, ent, s, rel, p, o, d_e, d_r)
+    torch.cuda.synchronize()
+    return {k: v.cpu().numpy() for k, v in out.items()}
+
+
+@pytest.mark.parametrize("prec", ["bf16x3", "fp32"])
+@pytest.mark.parametrize("fn", SCORER_FILES, ids=lambda f: os.path.basename(f)[7:-4])
+def test_forward_vs_golden(L, fn, prec):
+    f = np.load(fn)
+    meta = json.loads(str(f["meta"]))
+    out = forward_all(L, meta, f, L.PRECISIONS[prec])
+    model = meta["model"]
+    for k, v in out.items():
+        ref = f[k]
+        if meta["regime"] == "dyadic" and (model in K.BILINEAR or (model == "transe" and meta["l_norm"] == 1 and k != "spo")):
+            np.testing.assert_array_equal(v, ref, err_msg=f"{k} not bit-exact")
+        else:
+            tol = 1e-5 if model in K.DISTANCE else (2e-5 if prec == "bf16x3" else 2e-6)
+            if k == "spo":
+                tol = 2e-6
+            assert rel_err(v, ref) < tol, (k, rel_err(v, ref))
+
+
+@pytest.mark.parametrize("prec", ["bf16x3", "fp32"])
+@pytest.mark.parametrize("fn", SCORER_FILES, ids=lambda f: os.path.basename(f)[7:-4])
+def test_gradients_vs_golden(L, fn, prec):
+    f = np.load(fn)
+    meta = json.loads(str(f["meta"]))
+    model = meta["model"]
+    mk = MODEL_IDS[model]
+    ln = meta["l_norm"] or 1.0
+    P = L.PRECISIONS[prec]
+    ent, rel = dev(f["ent"]), dev(f["rel"])
+    s, p, o = (dev(f[k], torch.int64) for k in ("s", "p", "o"))
+    w_sp, w_po, w_spo = dev(f["w_sp"]), dev(f["w_po"]), dev(f["w_spo"])
+    d_e, d_r = ent.shape[1], rel.shape[1]
+    n = s.numel()
+    g_ent = torch.zeros_like(ent)
+    g_rel = torch.zeros_like(rel)
+    for direction, e_idx, w in ((L.DIR_SP, s, w_sp), (L.DIR_PO, o, w_po)):
+        q = L.prep_query(mk, direction, ent, e_idx, rel, p, n, d_e, d_r)
+        dq = torch.zeros_like(q)
+        if model in K.BILINEAR:
+            L.score_dot_bwd_q(w, ent, None, P, dq=dq, accumulate=False)
+            L.score_dot_bwd_t(w, q, None, g_ent, P)
+        else:
+            kind, sign = dist_kind(model, ln)
+            L.score_dist_bwd(kind, sign, w, q, ent, None, dq, g_ent)
+        L.prep_query_bwd(mk, direction, ent, e_idx, rel, p, n, d_e, d_r, dq, g_ent, g_rel)
+    L.score_spo_bwd(mk, ln, ent, s, rel, p, o, d_e, d_r, w_spo, g_ent, g_rel)
+    torch.cuda.synchronize()
+    tol = 1e-4 if (prec == "bf16x3" and model in K.BILINEAR) else 1e-5
+    ge, gr = g_ent.cpu().numpy(), g_rel.cpu().numpy()
+    assert np.abs(ge - f["g_ent"]).max() <= tol * np.abs(f["g_ent"]).max()
+    assert np.abs(gr - f["g_rel"]).max() <= tol * np.abs(f["g_rel"]).max()
+
+
+def test_rank_counts_vs_oracle(L):
+    rng = np.random.default_rng(3)
+    n, m, c0 = 37, 1000, 500
+    # quantised scores -> many ties; some NaN / inf
+    S = (rng.integers(-20, 20, size=(n, m)) / 4).astype(np.float32)
+    S[rng.random((n, m)) < 0.01] = np.nan
+    S[rng.random((n, m)) < 0.005] = np.inf
+    true_idx = rng.integers(c0 - 50, c0 + m + 50, size=n)
+    true_score = (rng.integers(-20, 20, size=n) / 4).astype(np.float32)
+    true_score[0] = np.nan
+    true_score[1] = -np.inf
+    fl = [np.unique(rng.integers(c0 - 100, c0 + m + 100, size=rng.integers(0, 40))) for _ in range(n)]
+    tl = [np.setdiff1d(np.unique(rng.integers(c0, c0 + m, size=rng.integers(0, 10))), f) for f in fl]
+    fl[2] = np.append(fl[2], true_idx[2]) if true_idx[2] not in fl[2] else fl[2]
+
+    def csr(lists):
+        ptr = np.zeros(n + 1, np.int64)
+        ptr[1:] = np.cumsum([len(x) for x in lists])
+        col = np.concatenate(lists).astype(np.int64) if ptr[-1] else np.zeros(1, np.int64)
+        return ptr, col
+
+    fp, fc = csr(fl)
+    tp, tc = csr(tl)
+    greater = torch.zeros(3 * n, dtype=torch.int64, device="cuda")
+    ties = torch.zeros(3 * n, dtype=torch.int64, device="cuda")
+    L.rank_counts(dev(S), c0, dev(true_idx), dev(true_score), dev(fp), dev(fc), dev(tp), dev(tc), greater, ties)
+    g = greater.view(3, n).cpu().numpy()
+    t = ties.view(3, n).cpu().numpy()
+    # oracle: overwrite the true entry, then -inf the filtered ones (never the true one)
+    Sx = S.astype(np.float64).copy()
+    for i in range(n):
+        if c0 <= true_idx[i] < c0 + m:
+            Sx[i, true_idx[i] - c0] = true_score[i]
+    raw = K.rank_and_ties(Sx, true_score.astype(np.float64))
+    for r, lists in ((1, fl), (2, None)):
+        for i in range(n):
+            cols = fl[i] if r == 1 else tl[i]
+            for j in cols:
+                if c0 <= j < c0 + m and j != true_idx[i]:
+                    Sx[i, j - c0] = -np.inf
+        gr, tr = K.rank_and_ties(Sx, true_score.astype(np.float64))
+        np.testing.assert_array_equal(g[r], gr)
+        np.testing.assert_array_equal(t[r], tr)
+    np.testing.assert_array_equal(g[0], raw[0])
+    np.testing.assert_array_equal(t[0], raw[1])
+
+
+@pytest.mark.parametrize("prec", ["bf16x3", "fp32"])
+def test_score_sp_c2_shape(L, prec):
+    """ComplEx-512 at the C2 shape (B=1024, E=14,541): check 64 random rows against the
+    float64 oracle, plus a dyadic copy bit-exact (size-independent exactness)."""
+    torch.manual_seed(0)
+    E, R, B, d = 14541, 237, 1024, 512
+    ent = (torch.randn(E, d) * 0.1).cuda()
+    rel = (torch.randn(R, d) * 0.1).cuda()
+    s = torch.randint(0, E, (B,)).cuda()
+    p = torch.randint(0, R, (B,)).cuda()
+    q = L.prep_query(0, L.DIR_SP, ent, s, rel, p, B, d, d)
+    S = L.score_dot(q, ent, None, L.PRECISIONS[prec])
+    rows = torch.randint(0, B, (64,))
+    ref = K.prep_sp("complex", ent[s[rows]].double().cpu().numpy(), rel[p[rows]].double().cpu().numpy()) @ \
+        ent.double().cpu().numpy().T
+    err = rel_err(S[rows.cuda()].cpu().numpy(), ref)
+    assert err < (2e-5 if prec == "bf16x3" else 2e-6), err
+    # dyadic: exact
+    entd = (torch.randint(-16, 17, (E, d)) / 8).float().cuda()
+    reld = (torch.randint(-16, 17, (R, d)) / 8).float().cuda()
+    qd = L.prep_query(0, L.DIR_SP, entd, s, reld, p, B, d, d)
+    Sd = L.score_dot(qd, entd, None, L.PRECISIONS[prec])
+    ref = qd.double() @ entd.double().T
+    assert torch.equal(Sd.double(), ref)
