@@ -1,0 +1,312 @@
+#!/usr/bin/env python
+"""Headline benchmark: 1vsAll scoring throughput, ComplEx-512 on FB15K-237 (synthetic,
+published shape), batch 1024 -- BASELINE.json configs[1] at N=1.
+
+A step is one pass of the hot path over one batch of 1024 fresh (s, p) queries:
+KgeModel.score_sp(s, p) -> fused LookupEmbedder gather + ComplEx query prep + the
+all-entities contraction against the 14,541-row entity table (libkgescore, gfx950).
+value = scored triples / s = (queries x entities) / step time, all ranks.
+
+N > 1 (torchrun, one process per GPU, RCCL): the entity table is row-sharded
+(kge.sharded); each rank contributes 1024 queries per step, the global batch of N*1024
+queries is exchanged (index all_gather + owner-computed query rows all_reduce) and
+scored against every shard -> per-GPU work is constant (weak scaling).
+
+Also reported (rank 0): the contraction kernel's roofline from HIP events recorded
+around every launch in the timed region, score_po, a full 1vsAll training step
+(sp + po forward/backward + CE + Adagrad), the filtered eval MRR on the synthetic test
+split, and the reference CPU path (oracle/refseq.py: the reference's exact ATen op
+sequence, verified bit-exact against it) timed on this host's cores.
+"""
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "kge-1_amd"))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
+BF16_DENSE_TFLOPS = 2500.0  # dense bf16 MFMA (spec, no sparsity)
+FP32_MFMA_TFLOPS = 157.3
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--batch", type=int, default=1024)
+    ap.add_argument("--dim", type=int, default=512)
+    ap.add_argument("--dataset", default="fb15k-237")
+    ap.add_argument("--precision", default="bf16x3", choices=["bf16x3", "fp32"])
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--no-extras", action="store_true")
+    ap.add_argument("--no-cpu", action="store_true")
+    return ap.parse_args()
+
+
+def make_config(args, device):
+    from kge import Config
+
+    c = Config()
+    c.set("model", "complex")
+    c._import("complex")
+    c.set("job.device", device)
+    c.set("lookup_embedder.dim", args.dim)
+    c.set("lookup_embedder.initialize", "normal_")
+    c.set("lookup_embedder.initialize_args", {"mean": 0.0, "std": 0.1})  # examples/toy-complex-train.yaml
+    c.set("engine.precision", args.precision)
+    c.set("verbose", False)
+    return c
+
+
+def timed_loop(fn, steps, warmup, world):
+    for i in range(warmup):
+        fn(i)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(steps):
+        fn(warmup + i)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    return (time.perf_counter() - t0) / steps
+
+
+def cpu_baseline(args, E, R, seconds):
+    """Reference CPU path: refseq replica of KgeModel.score_sp (ComplEx) on host cores."""
+    from oracle import refseq
+
+    torch.set_num_threads(max(1, min(os.cpu_count() or 1, 16)))
+    g = torch.Generator().manual_seed(0)
+    ent = torch.randn(E, args.dim, generator=g) * 0.1
+    rel = torch.randn(R, args.dim, generator=g) * 0.1
+    times = []
+    t_end = time.perf_counter() + seconds
+    i = 0
+    while (time.perf_counter() < t_end or len(times) < 3) and len(times) < 200:
+        s = torch.randint(0, E, (args.batch,), generator=g)
+        p = torch.randint(0, R, (args.batch,), generator=g)
+        t0 = time.perf_counter()
+        refseq.complex_score_sp(ent, rel, s, p)
+        times.append(time.perf_counter() - t0)
+        i += 1
+    med = float(np.median(times))
+    return {"value": args.batch * E / med, "unit": "scored triples/s", "cores": torch.get_num_threads(),
+            "kind": "port", "ms_per_step": med * 1e3,
+            "sample": f"{len(times)} x score_sp (B={args.batch}, E={E}, d={args.dim}, N(0,0.1)), "
+                      f"reference ATen op sequence (oracle/refseq.py) on CPU, median"}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl")
+    device = f"cuda:{local_rank}"
+
+    from kge import Dataset, KgeModel, _lib, engine
+    from kge.dataset import SHAPES
+
+    E, R, _ = SHAPES[args.dataset]
+    B, d = args.batch, args.dim
+    c = make_config(args, device)
+    c.set("dataset.num_entities", E)
+    c.set("dataset.num_relations", R)
+    torch.manual_seed(0)
+    model = KgeModel.create(c, Dataset(c, None))
+    model.eval()
+    ent = model._entity_embedder._embeddings.weight
+    rel = model._relation_embedder._embeddings.weight
+    steps, warmup = args.steps, args.warmup
+    g = torch.Generator(device=device).manual_seed(1 + rank)
+    s_all = torch.randint(0, E, (steps + warmup, B), device=device, generator=g)
+    p_all = torch.randint(0, R, (steps + warmup, B), device=device, generator=g)
+    prec = _lib.PRECISIONS[args.precision]
+
+    if world == 1:
+        def step(i):
+            with torch.no_grad():
+                return model.score_sp(s_all[i], p_all[i])
+        scored_per_step = B * E
+    else:
+        from kge.sharded import EngineOps, RowShardedScorer, shard_bounds
+
+        lo, hi = shard_bounds(E, world, rank)
+        shard = ent.detach()[lo:hi].contiguous()
+        sharded = RowShardedScorer(shard, lo, hi, E, rel.detach(), EngineOps(_lib.COMPLEX, prec))
+
+        def step(i):
+            with torch.no_grad():
+                return sharded.score_sp(s_all[i], p_all[i])
+        scored_per_step = world * B * E
+
+    # timed region, with HIP events around every contraction launch
+    for i in range(warmup):
+        step(i)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    engine.KERNEL_EVENTS = []
+    if world > 1:
+        _lib_events = []
+    t0 = time.perf_counter()
+    for i in range(steps):
+        if world == 1:
+            step(warmup + i)
+        else:
+            a = torch.cuda.Event(enable_timing=True)
+            b = torch.cuda.Event(enable_timing=True)
+            with torch.no_grad():
+                q, _, _ = sharded.queries(s_all[warmup + i], p_all[warmup + i], 0)
+                a.record()
+                sharded.ops.score(q, sharded.ent)
+                b.record()
+            _lib_events.append((a, b))
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    sec = (time.perf_counter() - t0) / steps
+    events = engine.KERNEL_EVENTS if world == 1 else _lib_events
+    engine.KERNEL_EVENTS = None
+    launch_ms = float(np.mean([a.elapsed_time(b) for a, b in events])) if events else float("nan")
+    # back-to-back launches of the same contraction between two HIP events on the launch
+    # stream: the kernel's average duration without per-launch event overhead (this is the
+    # figure the rocprofv3 kernel-trace average is compared with)
+    with torch.no_grad():
+        if world == 1:
+            q = _lib.prep_query(_lib.COMPLEX, _lib.DIR_SP, ent.detach(), s_all[0], rel.detach(), p_all[0], B, d, d)
+            tab = ent.detach()
+        else:
+            q, _, _ = sharded.queries(s_all[0], p_all[0], 0)
+            tab = sharded.ent
+        out_buf = torch.empty(q.shape[0], tab.shape[0], device=device)
+        for _ in range(3):
+            _lib.score_dot(q, tab, None, prec, out=out_buf)
+        a = torch.cuda.Event(enable_timing=True)
+        b = torch.cuda.Event(enable_timing=True)
+        reps = 20
+        a.record()
+        for _ in range(reps):
+            _lib.score_dot(q, tab, None, prec, out=out_buf)
+        b.record()
+        torch.cuda.synchronize()
+        kern_ms = a.elapsed_time(b) / reps
+        del out_buf
+    if world > 1:
+        t = torch.tensor([sec, kern_ms, launch_ms], device=device, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        sec, kern_ms, launch_ms = float(t[0]), float(t[1]), float(t[2])
+
+    # roofline of the dominant kernel (the contraction) -- per launch
+    rows_q = B * world
+    cols = E if world == 1 else math.ceil(E / world)
+    alg_flops = 2.0 * rows_q * cols * d
+    alg_bytes = 4.0 * (rows_q * d + cols * d + rows_q * cols)
+    k_s = kern_ms / 1e3
+    if args.precision == "bf16x3":
+        peak = BF16_DENSE_TFLOPS / 3.0
+        note = "bf16x3 split MFMA: 3 bf16 passes per fp32 product; peak = 2.5 PF dense bf16 / 3"
+    else:
+        peak = FP32_MFMA_TFLOPS
+        note = "fp32-input MFMA (v_mfma_f32_32x32x2_f32); peak = 157.3 TF"
+    achieved = alg_flops / k_s / 1e12
+    roofline = {"bound": "mfma", "achieved": round(achieved, 1), "peak": round(peak, 1), "unit": "TFLOP/s",
+                "frac": round(achieved / peak, 4), "traffic": None,
+                "kernel": "score_dot_kernel", "kernel_us": round(kern_ms * 1e3, 2),
+                "kernel_us_per_launch_events": round(launch_ms * 1e3, 2),
+                "hbm_achieved_GBs": round(alg_bytes / k_s / 1e9, 1),
+                "hbm_frac": round(alg_bytes / k_s / 1e9 / HBM_PEAK_GBS, 4),
+                "alg_bytes_per_launch": int(alg_bytes), "alg_flops_per_launch": int(alg_flops), "note": note}
+
+    value = scored_per_step / sec
+    out = {"metric": "1vsAll scored triples/sec (score_sp, ComplEx-512, FB15K-237 shape, B=1024)",
+           "value": value, "unit": "scored triples/s", "n_gpus": world, "steps": steps, "warmup": warmup,
+           "ms_per_step": sec * 1e3, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+           "dtype": "f32 (bf16x3 MFMA)" if args.precision == "bf16x3" else "f32",
+           "data": "synthetic (FB15K-237 shape: 14,541 entities / 237 relations), N(0,0.1) random-init tables",
+           "config": {"workload": "configs[1]: ComplEx dim=512 1vsAll FB15K-237, batch 1024, score_sp per step",
+                      "model": "complex", "dim": d, "global_batch": B * world, "entities": E,
+                      "parallelism": "single GPU" if world == 1 else f"entity-row-sharded x{world} (RCCL)",
+                      "precision": args.precision},
+           "roofline": roofline}
+
+    if rank == 0 and world == 1 and not args.no_extras:
+        out["extras"] = extras(args, model, c, E, R, device)
+    if rank == 0 and world == 1 and not args.no_cpu:
+        cb = cpu_baseline(args, E, R, args.cpu_seconds)
+        out["cpu_baseline"] = cb
+        out["speedup_vs_cpu"] = round(value / cb["value"], 1)
+    if rank == 0:
+        print(json.dumps(out))
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def extras(args, model, c, E, R, device):
+    """Secondary numbers: score_po, 1vsAll train step, eval MRR (synthetic test split)."""
+    from kge import Dataset
+    from kge.job import EntityRankingJob, TrainingJob
+
+    B = args.batch
+    res = {}
+    g = torch.Generator(device=device).manual_seed(7)
+    p = torch.randint(0, R, (40, B), device=device, generator=g)
+    o = torch.randint(0, E, (40, B), device=device, generator=g)
+    with torch.no_grad():
+        sec = timed_loop(lambda i: model.score_po(p[i], o[i]), 30, 10, 1)
+    res["score_po_ms"] = round(sec * 1e3, 4)
+    # 1vsAll training step (sp + po, fwd + bwd + CE + Adagrad), train_step_ms
+    c2 = c.clone()
+    c2.set("train.type", "1vsAll")
+    c2.set("train.optimizer", "Adagrad")
+    c2.set("train.optimizer_args", {"lr": 0.2})
+    c2.set("train.batch_size", B)
+    ds = Dataset.synthetic(c2, args.dataset, seed=0)
+    job = TrainingJob.create(c2, ds, model=model)
+    job._prepare()
+    job.model.train()
+    train = ds.split("train")
+    perm = torch.randperm(len(train), generator=torch.Generator().manual_seed(0))
+
+    def tstep(i):
+        job.optimizer.zero_grad()
+        job._process_batch(i, {"triples": train[perm[i * B:(i + 1) * B]].long()})
+        job.optimizer.step()
+    sec = timed_loop(tstep, 10, 3, 1)
+    res["train_step_ms"] = round(sec * 1e3, 3)
+    res["train_scored_triples_per_s"] = 2 * B * E / sec
+    res["train_triples_per_s"] = B / sec
+    # filtered eval (test split, batch 1024)
+    c3 = c.clone()
+    c3.set("eval.split", "test")
+    c3.set("eval.batch_size", B)
+    job.model.eval()
+    ej = EntityRankingJob(c3, ds, model=job.model)
+    ej._prepare()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    tr = ej._run()
+    torch.cuda.synchronize()
+    res["eval_test_triples"] = int(len(ds.split("test")))
+    res["eval_seconds"] = round(time.perf_counter() - t0, 4)
+    res["eval_mrr_filtered"] = tr["mean_reciprocal_rank_filtered"]
+    res["eval_hits_at_10_filtered"] = tr["hits_at_10_filtered"]
+    return res
+
+
+if __name__ == "__main__":
+    main()

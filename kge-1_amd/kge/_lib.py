@@ -107,6 +107,11 @@ def rows(t: torch.Tensor) -> int:
     return t.stride(0)
 
 
+#: KGE_CHECK_INDEX=1 validates every index vector against its table on the host side
+#: (one device reduction + sync per call: debugging / tests; the kernels trust indexes).
+CHECK_INDEX = os.environ.get("KGE_CHECK_INDEX", "0") == "1"
+
+
 def idx64(t: Optional[torch.Tensor]) -> Optional[torch.Tensor]:
     if t is None:
         return None
@@ -116,11 +121,21 @@ def idx64(t: Optional[torch.Tensor]) -> Optional[torch.Tensor]:
     return t.contiguous()
 
 
+def check_index(idx: Optional[torch.Tensor], num_rows: int, what: str):
+    if CHECK_INDEX and idx is not None and idx.numel() > 0:
+        lo, hi = int(idx.min()), int(idx.max())
+        if lo < 0 or hi >= num_rows:
+            raise IndexError(f"{what}: index out of range [{lo}, {hi}] for {num_rows} rows")
+
+
 # ------------------------------------------------------------------ thin wrappers
 
 
 def prep_query(model, direction, ent, eidx, rel, ridx, n, d_e, d_r, out=None):
     require_device(ent, rel)
+    eidx, ridx = idx64(eidx), idx64(ridx)
+    check_index(eidx, ent.shape[0], "entity index")
+    check_index(ridx, rel.shape[0], "relation index")
     q = out if out is not None else torch.empty(n, d_e, device=ent.device, dtype=torch.float32)
     _check(lib().kge_prep_query(model, direction, ptr(ent), rows(ent), ptr(eidx), ptr(rel), rows(rel),
                                 ptr(ridx), n, d_e, d_r, ptr(q), rows(q), stream()), "kge_prep_query")
@@ -128,6 +143,7 @@ def prep_query(model, direction, ent, eidx, rel, ridx, n, d_e, d_r, out=None):
 
 
 def prep_query_bwd(model, direction, ent, eidx, rel, ridx, n, d_e, d_r, dq, d_ent, d_rel):
+    eidx, ridx = idx64(eidx), idx64(ridx)
     _check(lib().kge_prep_query_bwd(
         model, direction, ptr(ent), rows(ent), ptr(eidx), ptr(rel), rows(rel), ptr(ridx), n, d_e, d_r,
         ptr(dq), rows(dq), ptr(d_ent), rows(d_ent) if d_ent is not None else 0, ptr(d_rel),
@@ -136,6 +152,8 @@ def prep_query_bwd(model, direction, ent, eidx, rel, ridx, n, d_e, d_r, dq, d_en
 
 def score_dot(q, t, tidx, precision, out=None):
     require_device(q, t)
+    tidx = idx64(tidx)
+    check_index(tidx, t.shape[0], "candidate index")
     n, d = q.shape
     m = tidx.numel() if tidx is not None else t.shape[0]
     s = out if out is not None else torch.empty(n, m, device=q.device, dtype=torch.float32)
@@ -145,6 +163,7 @@ def score_dot(q, t, tidx, precision, out=None):
 
 
 def score_dot_bwd_q(g, t, tidx, precision, dq=None, accumulate=False):
+    tidx = idx64(tidx)
     n, m = g.shape
     d = t.shape[1]
     if dq is None:
@@ -156,6 +175,7 @@ def score_dot_bwd_q(g, t, tidx, precision, dq=None, accumulate=False):
 
 
 def score_dot_bwd_t(g, q, tidx, dt, precision):
+    tidx = idx64(tidx)
     n, m = g.shape
     d = q.shape[1]
     _check(lib().kge_score_dot_bwd_t(ptr(g), rows(g), ptr(q), rows(q), ptr(tidx), n, m, d, ptr(dt),
@@ -165,6 +185,7 @@ def score_dot_bwd_t(g, q, tidx, dt, precision):
 
 def score_dist(kind, sign, q, t, tidx, out=None):
     require_device(q, t)
+    tidx = idx64(tidx)
     n, d = q.shape
     m = tidx.numel() if tidx is not None else t.shape[0]
     s = out if out is not None else torch.empty(n, m, device=q.device, dtype=torch.float32)
@@ -174,6 +195,7 @@ def score_dist(kind, sign, q, t, tidx, out=None):
 
 
 def score_dist_bwd(kind, sign, g, q, t, tidx, dq, dt):
+    tidx = idx64(tidx)
     n, m = g.shape
     d = q.shape[1]
     _check(lib().kge_score_dist_bwd(kind, sign, ptr(g), rows(g), ptr(q), rows(q), ptr(t), rows(t), ptr(tidx),
@@ -183,6 +205,10 @@ def score_dist_bwd(kind, sign, g, q, t, tidx, dq, dt):
 
 def score_spo(model, l_norm, ent, sidx, rel, pidx, oidx, d_e, d_r, out=None):
     require_device(ent, rel)
+    sidx, pidx, oidx = idx64(sidx), idx64(pidx), idx64(oidx)
+    check_index(sidx, ent.shape[0], "subject index")
+    check_index(oidx, ent.shape[0], "object index")
+    check_index(pidx, rel.shape[0], "relation index")
     n = sidx.numel()
     o = out if out is not None else torch.empty(n, device=ent.device, dtype=torch.float32)
     _check(lib().kge_score_spo(model, float(l_norm), ptr(ent), rows(ent), ptr(sidx), ptr(rel), rows(rel),
@@ -191,6 +217,7 @@ def score_spo(model, l_norm, ent, sidx, rel, pidx, oidx, d_e, d_r, out=None):
 
 
 def score_spo_bwd(model, l_norm, ent, sidx, rel, pidx, oidx, d_e, d_r, g, d_ent, d_rel):
+    sidx, pidx, oidx = idx64(sidx), idx64(pidx), idx64(oidx)
     n = sidx.numel()
     _check(lib().kge_score_spo_bwd(
         model, float(l_norm), ptr(ent), rows(ent), ptr(sidx), ptr(rel), rows(rel), ptr(pidx), ptr(oidx), n,
@@ -200,12 +227,18 @@ def score_spo_bwd(model, l_norm, ent, sidx, rel, pidx, oidx, d_e, d_r, g, d_ent,
 
 def rank_counts(s, c0, true_idx, true_score, f_ptr, f_col, t_ptr, t_col, greater, ties):
     n, m = s.shape
+    true_idx = idx64(true_idx)
+    true_score = true_score.reshape(-1).float().contiguous()
+    f_ptr, f_col, t_ptr, t_col = (idx64(x) for x in (f_ptr, f_col, t_ptr, t_col))
+    if not (greater.is_contiguous() and ties.is_contiguous() and greater.dtype == torch.int64):
+        raise ValueError("greater / ties must be contiguous int64")
     _check(lib().kge_rank_counts(ptr(s), rows(s), n, m, c0, ptr(true_idx), ptr(true_score), ptr(f_ptr),
                                  ptr(f_col), ptr(t_ptr), ptr(t_col), ptr(greater), ptr(ties), stream()),
            "kge_rank_counts")
 
 
 def rank_hist(greater, ties, tie_handling, ranks, hist):
+    greater, ties = greater.contiguous(), ties.contiguous()
     n = greater.numel()
     _check(lib().kge_rank_hist(ptr(greater), ptr(ties), n, TIE[tie_handling], ptr(ranks), ptr(hist),
                                hist.numel() if hist is not None else 0, stream()), "kge_rank_hist")

@@ -1,0 +1,143 @@
+"""Autograd wrappers around libkgescore (the gfx950 HIP engine).
+
+Two scoring ops cover every in-scope scorer:
+
+* ``score_all``  -- prep + contraction against every row of a candidate table:
+  the ``sp_`` / ``_po`` combines of RelationalScorer.score_emb (kge_model.py:120-182),
+  fused with the LookupEmbedder gather when row indexes are given.  Bilinear models
+  contract on MFMA (kge_score_dot), distance models on the VALU (kge_score_dist).
+* ``score_spo``  -- row-wise triple scores (combine="spo").
+
+Backward passes are the engine's backward kernels; when the query table and the
+candidate table are the same tensor (the entity table), both gradient contributions are
+accumulated into ONE dense buffer, the layout torch's embedding_dense_backward produces.
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+import torch
+
+from . import _lib as L
+
+BILINEAR = (L.COMPLEX, L.DISTMULT, L.RESCAL)
+
+#: When set to a list, every all-entities contraction launch appends a pair of HIP events
+#: recorded on the launching stream right before / after it (bench.py's kernel timing).
+KERNEL_EVENTS = None
+
+
+def _timed(fn, *args, **kwargs):
+    if KERNEL_EVENTS is None:
+        return fn(*args, **kwargs)
+    a = torch.cuda.Event(enable_timing=True)
+    b = torch.cuda.Event(enable_timing=True)
+    a.record()
+    out = fn(*args, **kwargs)
+    b.record()
+    KERNEL_EVENTS.append((a, b))
+    return out
+
+
+def dist_kind(kind: int, l_norm: float):
+    """(kernel distance kind, sign) for TransE (-dist, transe.py:220-225) and RotatE
+    (+dist, quirk Q1, rotate.py:275-307)."""
+    if l_norm not in (1.0, 2.0):
+        raise ValueError(f"l_norm={l_norm} not supported (1 or 2)")
+    if kind == L.TRANSE:
+        return (L.DIST_L1 if l_norm == 1.0 else L.DIST_L2), -1.0
+    if kind == L.ROTATE:
+        return (L.DIST_ROT_L1 if l_norm == 1.0 else L.DIST_ROT_L2), 1.0
+    raise ValueError(kind)
+
+
+def _rows(x: torch.Tensor) -> torch.Tensor:
+    if x.dim() != 2 or x.stride(1) != 1:
+        x = x.contiguous()
+    return x
+
+
+class _ScoreAll(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, kind, direction, precision, l_norm, ent, eidx, rel, ridx, tab, tidx):
+        ent, rel, tab = _rows(ent), _rows(rel), _rows(tab)
+        n = eidx.numel() if eidx is not None else ent.shape[0]
+        d_e, d_r = ent.shape[1], rel.shape[1]
+        if tab.shape[1] != d_e:
+            raise ValueError(f"candidate dim {tab.shape[1]} != entity dim {d_e}")
+        q = L.prep_query(kind, direction, ent, eidx, rel, ridx, n, d_e, d_r)
+        if kind in BILINEAR:
+            s = _timed(L.score_dot, q, tab, tidx, precision)
+        else:
+            dk, sign = dist_kind(kind, l_norm)
+            s = _timed(L.score_dist, dk, sign, q, tab, tidx)
+        ctx.meta = (kind, direction, precision, l_norm, n, d_e, d_r, ent is tab)
+        ctx.save_for_backward(ent, eidx, rel, ridx, tab, tidx, q)
+        return s
+
+    @staticmethod
+    def backward(ctx, g):
+        kind, direction, precision, l_norm, n, d_e, d_r, same = ctx.meta
+        ent, eidx, rel, ridx, tab, tidx, q = ctx.saved_tensors
+        g = _rows(g)
+        need_ent, need_rel, need_tab = ctx.needs_input_grad[4], ctx.needs_input_grad[6], ctx.needs_input_grad[8]
+        d_tab = torch.zeros_like(tab) if (need_tab or (same and need_ent)) else None
+        d_ent = d_tab if same else (torch.zeros_like(ent) if need_ent else None)
+        d_rel = torch.zeros_like(rel) if need_rel else None
+        dq = torch.zeros_like(q) if (need_ent or need_rel) else None
+        if kind in BILINEAR:
+            if dq is not None:
+                L.score_dot_bwd_q(g, tab, tidx, precision, dq=dq, accumulate=False)
+            if d_tab is not None:
+                L.score_dot_bwd_t(g, q, tidx, d_tab, precision)
+        else:
+            dk, sign = dist_kind(kind, l_norm)
+            L.score_dist_bwd(dk, sign, g, q, tab, tidx, dq, d_tab)
+        if dq is not None:
+            L.prep_query_bwd(kind, direction, ent, eidx, rel, ridx, n, d_e, d_r, dq, d_ent, d_rel)
+        return (None, None, None, None, None if same else d_ent, None, d_rel, None,
+                d_tab, None)
+
+
+def score_all(kind: int, direction: int, precision: int, l_norm: float, ent: torch.Tensor,
+              eidx: Optional[torch.Tensor], rel: torch.Tensor, ridx: Optional[torch.Tensor],
+              tab: torch.Tensor, tidx: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """S[i, j] = score of query i (prep(ent[eidx[i]], rel[ridx[i]])) against candidate
+    tab[tidx[j]] (all rows of tab when tidx is None)."""
+    L.require_device(ent, rel, tab)
+    return _ScoreAll.apply(kind, direction, precision, float(l_norm), ent, L.idx64(eidx), rel,
+                           L.idx64(ridx), tab, L.idx64(tidx))
+
+
+class _ScoreSpo(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, kind, l_norm, ent, sidx, rel, pidx, oidx):
+        ent, rel = _rows(ent), _rows(rel)
+        d_e, d_r = ent.shape[1], rel.shape[1]
+        out = L.score_spo(kind, l_norm, ent, sidx, rel, pidx, oidx, d_e, d_r)
+        ctx.meta = (kind, l_norm, d_e, d_r)
+        ctx.save_for_backward(ent, sidx, rel, pidx, oidx)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        kind, l_norm, d_e, d_r = ctx.meta
+        ent, sidx, rel, pidx, oidx = ctx.saved_tensors
+        d_ent = torch.zeros_like(ent) if ctx.needs_input_grad[2] else None
+        d_rel = torch.zeros_like(rel) if ctx.needs_input_grad[4] else None
+        if d_ent is not None or d_rel is not None:
+            L.score_spo_bwd(kind, l_norm, ent, sidx, rel, pidx, oidx, d_e, d_r, g.contiguous(), d_ent, d_rel)
+        return None, None, d_ent, None, d_rel, None, None
+
+
+def score_spo(kind: int, l_norm: float, ent, sidx, rel, pidx, oidx) -> torch.Tensor:
+    L.require_device(ent, rel)
+    return _ScoreSpo.apply(kind, float(l_norm), ent, L.idx64(sidx), rel, L.idx64(pidx), L.idx64(oidx))
+
+
+def score_spo_emb(kind: int, l_norm: float, s_emb, p_emb, o_emb) -> torch.Tensor:
+    """combine="spo" on embedding rows: s, o stacked into one table."""
+    n = p_emb.shape[0]
+    so = torch.cat((s_emb, o_emb), 0)
+    ar = torch.arange(n, device=p_emb.device)
+    return score_spo(kind, l_norm, so, ar, p_emb, ar, ar + n)

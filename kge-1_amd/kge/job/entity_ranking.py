@@ -1,0 +1,178 @@
+"""Entity-ranking evaluation (EvaluationJob eval.py:10-132, EntityRankingJob
+entity_ranking.py:11-577) as an on-device pipeline.
+
+Per batch of evaluation triples:
+  1. true scores via KgeModel.score_spo (entity_ranking.py:139-140);
+  2. per entity chunk, KgeModel.score_sp_po on the engine (entity_ranking.py:153-168);
+  3. kge_rank_counts: raw / filtered / filtered-with-test greater & tie counts straight
+     from the score chunk, the true entry replaced by the true score, filtering applied
+     from per-query CSR lists of known answers (entity_ranking.py:172-216, 469-529);
+  4. kge_rank_hist: tie handling + rank histogram (entity_ranking.py:531-551, eval.py:148-171).
+The filter lists are built once per job from the dataset splits (vectorised numpy)
+instead of the reference's per-triple Python collate (job/util.py:5-38).  Counts are sums
+over chunks, which is exactly the reference's chunk_size decomposition and the
+per-shard reduction of the row-sharded multi-GPU path (kge.sharded).
+"""
+from __future__ import annotations
+
+import time
+from typing import Dict, List, Optional
+
+import numpy as np
+import torch
+
+from .. import _lib
+from ..dataset import KvsAllIndex
+from .job import Job
+
+RANKING_SUFFIX = {"_raw": "", "_filt": "_filtered", "_filt_test": "_filtered_with_test"}
+
+
+class EvaluationJob(Job):
+    def __init__(self, config, dataset, parent_job=None, model=None):
+        super().__init__(config, dataset, parent_job)
+        self.model = model
+        self.batch_size = config.get("eval.batch_size")
+        max_k = min(dataset.num_entities(), max(config.get("entity_ranking.hits_at_k_s")))
+        self.hits_at_k_s = [k for k in config.get("entity_ranking.hits_at_k_s") if k <= max_k]
+        self.eval_split = config.get("eval.split")
+        self.filter_splits = list(config.get("entity_ranking.filter_splits"))
+        if self.eval_split not in self.filter_splits:
+            self.filter_splits.append(self.eval_split)
+        self.filter_with_test = config.get("entity_ranking.filter_with_test")
+        self.epoch = -1
+        self.post_epoch_trace_hooks = []
+
+    @staticmethod
+    def create(config, dataset, parent_job=None, model=None):
+        if config.get("eval.type") == "entity_ranking":
+            return EntityRankingJob(config, dataset, parent_job=parent_job, model=model)
+        raise ValueError("eval.type")
+
+
+def _csr_minus(ptr_a, col_a, ptr_b, col_b, num_entities):
+    """Per-row set difference A \\ B of two CSRs with the same rows."""
+    n = len(ptr_a) - 1
+    ra = np.repeat(np.arange(n, dtype=np.int64), np.diff(ptr_a))
+    rb = np.repeat(np.arange(n, dtype=np.int64), np.diff(ptr_b))
+    keep = ~np.isin(ra * num_entities + col_a, rb * num_entities + col_b)
+    col = col_a[keep]
+    ptr = np.zeros(n + 1, np.int64)
+    np.cumsum(np.bincount(ra[keep], minlength=n), out=ptr[1:])
+    return ptr, col
+
+
+class EntityRankingJob(EvaluationJob):
+    def __init__(self, config, dataset, parent_job=None, model=None):
+        super().__init__(config, dataset, parent_job, model)
+        self.tie_handling = config.check(
+            "entity_ranking.tie_handling", ["rounded_mean_rank", "best_rank", "worst_rank"])
+        self.capture_ranks = False  # keep per-query ranks in self.ranks (tests / tracing)
+        self.ranks: Dict[str, np.ndarray] = {}
+
+    # ---------------------------------------------------------------- preparation
+    def _filter_index(self, splits: List[str]):
+        key = "filter:" + "+".join(sorted(splits))
+        cache = self.dataset._indexes
+        if key not in cache:
+            t = np.concatenate([self.dataset.split(s).numpy() for s in splits]).astype(np.int64)
+            cache[key] = (KvsAllIndex(t, (0, 1), 2), KvsAllIndex(t, (1, 2), 0))
+        return cache[key]
+
+    def _prepare(self):
+        self.model.prepare_job(self)
+        self.triples = self.dataset.split(self.eval_split).long()
+        tri = self.triples.numpy()
+        E = self.dataset.num_entities()
+        self.use_test = "test" not in self.filter_splits and self.filter_with_test
+        self.rankings = ["_raw", "_filt", "_filt_test"] if self.use_test else ["_raw", "_filt"]
+        f_sp, f_po = self._filter_index(self.filter_splits)
+        csr = {"sp": f_sp.csr_for(tri[:, [0, 1]]), "po": f_po.csr_for(tri[:, [1, 2]])}
+        dev = self.device
+        self._f = {k: (torch.from_numpy(p).to(dev), torch.from_numpy(c if len(c) else np.zeros(1, np.int64)).to(dev))
+                   for k, (p, c) in csr.items()}
+        self._t = None
+        if self.use_test:
+            t_sp, t_po = self._filter_index(["test"])
+            tcsr = {"sp": _csr_minus(*t_sp.csr_for(tri[:, [0, 1]]), *csr["sp"], E),
+                    "po": _csr_minus(*t_po.csr_for(tri[:, [1, 2]]), *csr["po"], E)}
+            self._t = {k: (torch.from_numpy(p).to(dev),
+                           torch.from_numpy(c if len(c) else np.zeros(1, np.int64)).to(dev))
+                       for k, (p, c) in tcsr.items()}
+
+    # ---------------------------------------------------------------- evaluation
+    @torch.no_grad()
+    def _run(self) -> dict:
+        was_training = self.model.training
+        self.model.eval()
+        E = self.dataset.num_entities()
+        dev = self.device
+        nrank = len(self.rankings)
+        chunk = self.config.get("entity_ranking.chunk_size")
+        chunk = E if chunk is None or chunk < 0 else chunk
+        hists = torch.zeros(nrank, E, device=dev)
+        ranks_out = {f"{d}{r}": [] for d in "so" for r in self.rankings}
+        epoch_time = -time.time()
+        triples = self.triples.to(dev)
+        N = len(triples)
+        for b0 in range(0, N, self.batch_size):
+            b1 = min(N, b0 + self.batch_size)
+            B = b1 - b0
+            s, p, o = triples[b0:b1, 0], triples[b0:b1, 1], triples[b0:b1, 2]
+            o_true = self.model.score_spo(s, p, o, "o").view(-1).float().contiguous()
+            s_true = self.model.score_spo(s, p, o, "s").view(-1).float().contiguous()
+            g = {d: torch.zeros(3 * B, dtype=torch.int64, device=dev) for d in "so"}
+            t = {d: torch.zeros(3 * B, dtype=torch.int64, device=dev) for d in "so"}
+            for c0 in range(0, E, chunk):
+                c1 = min(E, c0 + chunk)
+                subset = None if (c0 == 0 and c1 == E) else torch.arange(c0, c1, device=dev)
+                scores = self.model.score_sp_po(s, p, o, subset)
+                C = c1 - c0
+                self._count(scores[:, :C], c0, o, o_true, "sp", b0, b1, g["o"], t["o"])
+                self._count(scores[:, C:], c0, s, s_true, "po", b0, b1, g["s"], t["s"])
+                del scores
+            for ri, r in enumerate(self.rankings):
+                for d in "os":
+                    rk = torch.empty(B, dtype=torch.int64, device=dev)
+                    _lib.rank_hist(g[d][ri * B:(ri + 1) * B], t[d][ri * B:(ri + 1) * B], self.tie_handling, rk,
+                                   hists[ri])
+                    if self.capture_ranks:
+                        ranks_out[f"{d}{r}"].append(rk)
+        epoch_time += time.time()
+        metrics = {}
+        for ri, r in enumerate(self.rankings):
+            metrics.update(self._compute_metrics(hists[ri], RANKING_SUFFIX[r]))
+        if self.capture_ranks:
+            self.ranks = {k: torch.cat(v).cpu().numpy() if v else np.zeros(0, np.int64)
+                          for k, v in ranks_out.items()}
+        trace = dict(type="entity_ranking", scope="epoch", split=self.eval_split,
+                     filter_splits=self.filter_splits, epoch=self.epoch, batches=(N + self.batch_size - 1)
+                     // self.batch_size, size=N, epoch_time=epoch_time, event="eval_completed", **metrics)
+        for f in self.post_epoch_trace_hooks:
+            f(self, trace)
+        if was_training:
+            self.model.train()
+        return trace
+
+    def _count(self, scores, c0, true_idx, true_score, kind, b0, b1, greater, ties):
+        scores = scores.float()
+        if scores.stride(1) != 1:
+            scores = scores.contiguous()
+        fp, fc = self._f[kind]
+        tp, tc = self._t[kind] if self._t is not None else (None, None)
+        _lib.rank_counts(scores, c0, true_idx, true_score, fp[b0:], fc,
+                         tp[b0:] if tp is not None else None, tc, greater, ties)
+
+    def _compute_metrics(self, rank_hist: torch.Tensor, suffix: str = "") -> Dict[str, float]:
+        """entity_ranking.py:553-577 (fp32 histogram arithmetic like the reference)."""
+        metrics = {}
+        n = torch.sum(rank_hist).item()
+        ranks = torch.arange(1, self.dataset.num_entities() + 1, device=rank_hist.device).float()
+        metrics["mean_rank" + suffix] = (torch.sum(rank_hist * ranks).item() / n) if n > 0.0 else 0.0
+        rr = 1.0 / ranks
+        metrics["mean_reciprocal_rank" + suffix] = (torch.sum(rank_hist * rr).item() / n) if n > 0.0 else 0.0
+        kmax = max(self.hits_at_k_s)
+        hits = (torch.cumsum(rank_hist[:kmax], dim=0) / n).tolist() if n > 0.0 else [0.0] * kmax
+        for k in self.hits_at_k_s:
+            metrics["hits_at_{}{}".format(k, suffix)] = hits[k - 1]
+        return metrics

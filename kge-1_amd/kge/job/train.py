@@ -1,0 +1,245 @@
+"""Training jobs that drive the scoring hot path: TrainingJob1vsAll (train.py:1002-1062)
+and TrainingJobKvsAll (train.py:493-756) over the TrainingJob epoch loop (train.py:45-490).
+
+Per batch they call KgeModel.score_sp / score_po exactly as the reference does; the
+engine runs the fused gather + contraction forward and the MFMA backward.  Difference
+from the reference, by design (Q11): the per-direction ``loss.item()`` host syncs are
+deferred to one sync per batch.
+"""
+from __future__ import annotations
+
+import math
+import time
+from dataclasses import dataclass
+from typing import Any, Dict, Optional
+
+import numpy as np
+import torch
+
+from ..model.kge_model import KgeModel
+from ..util.loss import KgeLoss
+from ..util.optimizer import KgeLRScheduler, KgeOptimizer
+from .job import Job
+
+S, P, O = 0, 1, 2
+
+
+class TrainingJob(Job):
+    @dataclass
+    class _ProcessBatchResult:
+        avg_loss: float
+        size: int
+        prepare_time: float
+        forward_time: float
+        backward_time: float
+
+    def __init__(self, config, dataset, parent_job=None, model=None):
+        super().__init__(config, dataset, parent_job)
+        self.model: KgeModel = model if model is not None else KgeModel.create(config, dataset)
+        self.optimizer = KgeOptimizer.create(config, self.model)
+        self.kge_lr_scheduler = KgeLRScheduler(config, self.optimizer)
+        self.loss = KgeLoss.create(config)
+        self.abort_on_nan: bool = config.get("train.abort_on_nan")
+        self.batch_size: int = config.get("train.batch_size")
+        self.train_split = config.get("train.split")
+        self.epoch = 0
+        self.loader = None
+        self.num_examples = None
+        self.type_str: Optional[str] = None
+        self.pre_batch_hooks = []
+        self.post_batch_trace_hooks = []
+        self.post_epoch_trace_hooks = []
+        self.generator = torch.Generator()
+        seed = config.get("random_seed.torch")
+        if seed >= 0:
+            self.generator.manual_seed(seed)
+        self.model.train()
+
+    @staticmethod
+    def create(config, dataset, parent_job=None, model=None) -> "TrainingJob":
+        t = config.get("train.type")
+        if t == "KvsAll":
+            return TrainingJobKvsAll(config, dataset, parent_job, model=model)
+        if t == "1vsAll":
+            return TrainingJob1vsAll(config, dataset, parent_job, model=model)
+        if t == "negative_sampling":
+            from .negative_sampling import TrainingJobNegativeSampling
+
+            return TrainingJobNegativeSampling(config, dataset, parent_job, model=model)
+        raise ValueError("train.type")
+
+    def _prepare(self):
+        self.model.prepare_job(self)
+
+    def _run(self):
+        traces = []
+        for _ in range(self.config.get("train.max_epochs")):
+            self.epoch += 1
+            traces.append(self.run_epoch())
+        return traces
+
+    def _batches(self):
+        perm = torch.randperm(self.num_examples, generator=self.generator)
+        for b in range(0, self.num_examples, self.batch_size):
+            yield perm[b:b + self.batch_size]
+
+    def run_epoch(self) -> Dict[str, Any]:
+        """One pass over the training examples (train.py:295-429)."""
+        if not self._is_prepared:
+            self._prepare()
+            self._is_prepared = True
+        sum_loss = 0.0
+        sum_penalty = 0.0
+        epoch_time = -time.time()
+        fwd = bwd = prep = opt_t = 0.0
+        n_batches = 0
+        for batch_index, example_ids in enumerate(self._batches()):
+            for f in self.pre_batch_hooks:
+                f(self)
+            self.optimizer.zero_grad()
+            batch = self._collate(example_ids)
+            res = self.process_batch(batch_index, batch)
+            sum_loss += res.avg_loss * res.size
+            penalty = 0.0
+            for _, pv in self.model.penalty(epoch=self.epoch, batch_index=batch_index, batch=batch):
+                pv.backward()
+                penalty += pv.item()
+            sum_penalty += penalty
+            if self.abort_on_nan and math.isnan(res.avg_loss + penalty):
+                raise FloatingPointError("Cost became nan, aborting training job")
+            t0 = time.time()
+            self.optimizer.step()
+            opt_t += time.time() - t0
+            prep += res.prepare_time
+            fwd += res.forward_time
+            bwd += res.backward_time
+            n_batches += 1
+        epoch_time += time.time()
+        trace = dict(type=self.type_str, scope="epoch", epoch=self.epoch, split=self.train_split,
+                     batches=n_batches, size=self.num_examples, avg_loss=sum_loss / max(1, self.num_examples),
+                     avg_penalty=sum_penalty / max(1, n_batches), epoch_time=epoch_time, prepare_time=prep,
+                     forward_time=fwd, backward_time=bwd, optimizer_time=opt_t, event="epoch_completed")
+        for f in self.post_epoch_trace_hooks:
+            f(self, trace)
+        return trace
+
+    def _collate(self, example_ids):
+        raise NotImplementedError
+
+    def process_batch(self, batch_index, batch) -> "TrainingJob._ProcessBatchResult":
+        return self._process_batch(batch_index, batch)
+
+
+class TrainingJob1vsAll(TrainingJob):
+    """Each (s, p, o) scores (s, p, ?) and (?, p, o) against all entities; CE loss."""
+
+    def __init__(self, config, dataset, parent_job=None, model=None):
+        super().__init__(config, dataset, parent_job, model=model)
+        self.type_str = "1vsAll"
+
+    def _prepare(self):
+        super()._prepare()
+        self.num_examples = self.dataset.split(self.train_split).size(0)
+
+    def _collate(self, example_ids):
+        return {"triples": self.dataset.split(self.train_split)[example_ids, :].long()}
+
+    def _process_batch(self, batch_index, batch) -> TrainingJob._ProcessBatchResult:
+        """train.py:1032-1062: sp then po, each loss / B followed by backward."""
+        t = -time.time()
+        triples = batch["triples"].to(self.device, non_blocking=True)
+        bs = len(triples)
+        t += time.time()
+        fwd = -time.time()
+        scores_sp = self.model.score_sp(triples[:, S], triples[:, P])
+        loss_sp = self.loss(scores_sp, triples[:, O]) / bs
+        fwd += time.time()
+        bwd = -time.time()
+        loss_sp.backward()
+        bwd += time.time()
+        del scores_sp
+        fwd -= time.time()
+        scores_po = self.model.score_po(triples[:, P], triples[:, O])
+        loss_po = self.loss(scores_po, triples[:, S]) / bs
+        fwd += time.time()
+        bwd -= time.time()
+        loss_po.backward()
+        bwd += time.time()
+        loss_value = (loss_sp.detach() + loss_po.detach()).item()  # one host sync per batch
+        return TrainingJob._ProcessBatchResult(loss_value, bs, t, fwd, bwd)
+
+
+class TrainingJobKvsAll(TrainingJob):
+    """Queries (s, p, ?) / (?, p, o) with all their training answers as a label matrix
+    (train.py:493-756); KL loss on log_softmax of the scores."""
+
+    def __init__(self, config, dataset, parent_job=None, model=None):
+        super().__init__(config, dataset, parent_job, model=model)
+        self.label_smoothing = config.get("KvsAll.label_smoothing")
+        if self.label_smoothing < 0:
+            self.label_smoothing = 0.0
+        elif 0 < self.label_smoothing <= 1.0 / dataset.num_entities():
+            self.label_smoothing = 1.0 / dataset.num_entities()
+        self.type_str = "KvsAll"
+
+    def _prepare(self):
+        super()._prepare()
+        self.query_types = [k for k, v in self.config.get("KvsAll.query_types").items() if v]
+        if "s_o" in self.query_types:
+            raise NotImplementedError("KvsAll query type s_o is outside the scoring path")
+        self.query_indexes = []
+        self.query_last_example = []
+        self.num_examples = 0
+        for qt in self.query_types:
+            idx = self.dataset.index(f"{self.train_split}_{'sp_to_o' if qt == 'sp_' else 'po_to_s'}")
+            self.query_indexes.append(idx)
+            self.num_examples += len(idx)
+            self.query_last_example.append(self.num_examples)
+        # device copies of the label CSRs (one per query type)
+        self._dev = [(torch.from_numpy(ix.keys).to(self.device), torch.from_numpy(ix.offsets).to(self.device),
+                      torch.from_numpy(ix.values).to(self.device)) for ix in self.query_indexes]
+
+    def _collate(self, example_ids):
+        return {"examples": example_ids}
+
+    def _process_batch(self, batch_index, batch) -> TrainingJob._ProcessBatchResult:
+        t = -time.time()
+        ex = batch["examples"].numpy()
+        bs = len(ex)
+        E = self.dataset.num_entities()
+        t += time.time()
+        fwd = bwd = 0.0
+        total = None
+        start = 0
+        for qi, qt in enumerate(self.query_types):
+            end = self.query_last_example[qi]
+            sel = ex[(ex >= start) & (ex < end)] - start
+            start = end
+            if len(sel) == 0:
+                continue
+            t -= time.time()
+            keys, offs, vals = self._dev[qi]
+            sel_d = torch.from_numpy(sel).to(self.device)
+            q = keys[sel_d]
+            lo, hi = offs[sel_d], offs[sel_d + 1]
+            lens = hi - lo
+            rows = torch.repeat_interleave(torch.arange(len(sel), device=self.device), lens)
+            pos = torch.arange(int(lens.sum().item()), device=self.device) - torch.repeat_interleave(
+                torch.cumsum(lens, 0) - lens, lens) + torch.repeat_interleave(lo, lens)
+            labels = torch.zeros(len(sel), E, device=self.device)
+            labels[rows, vals[pos]] = 1.0
+            if self.label_smoothing > 0.0:
+                labels = (1.0 - self.label_smoothing) * labels + 1.0 / E
+            t += time.time()
+            fwd -= time.time()
+            if qt == "sp_":
+                scores = self.model.score_sp(q[:, 0], q[:, 1])
+            else:
+                scores = self.model.score_po(q[:, 0], q[:, 1])
+            loss = self.loss(scores, labels) / bs
+            fwd += time.time()
+            bwd -= time.time()
+            loss.backward()
+            bwd += time.time()
+            total = loss.detach()  # reference keeps the last query type's value (Q10)
+        return TrainingJob._ProcessBatchResult(float(total.item()) if total is not None else 0.0, bs, t, fwd, bwd)

@@ -1,0 +1,89 @@
+"""LookupEmbedder: one stored fp32 row per object (lookup_embedder.py:13-158).
+
+The table is an ``nn.Embedding`` so checkpoints keep the reference's state_dict keys
+(``_entity_embedder._embeddings.weight``).  On the fused scoring path the table is not
+gathered here at all: KgeModel hands the weight to the engine, whose prep kernel gathers
+the query rows and whose contraction streams the whole table (no embed_all copy, Q3).
+"""
+from __future__ import annotations
+
+from typing import List
+
+import torch
+import torch.nn.functional
+from torch import Tensor
+
+from ..kge_model import KgeEmbedder
+
+
+class LookupEmbedder(KgeEmbedder):
+    def __init__(self, config, dataset, configuration_key: str, vocab_size: int, init_for_load_only=False):
+        super().__init__(config, dataset, configuration_key, init_for_load_only=init_for_load_only)
+        self.normalize_p = self.get_option("normalize.p")
+        self.normalize_with_grad = self.get_option("normalize.with_grad")
+        self.regularize = self.check_option("regularize", ["", "lp"])
+        self.sparse = self.get_option("sparse")
+        self.vocab_size = vocab_size
+        self._embeddings = torch.nn.Embedding(self.vocab_size, self.dim, sparse=self.sparse)
+        if not init_for_load_only:
+            self._init_embeddings(self._embeddings.weight.data)
+        dropout = self.get_option("dropout")
+        if dropout < 0:
+            dropout = 0.0
+        self.dropout = torch.nn.Dropout(dropout)
+
+    def prepare_job(self, job, **kwargs):
+        super().prepare_job(job, **kwargs)
+        if self.normalize_p > 0:  # lookup_embedder.py:58-75
+
+            def normalize_embeddings(job):
+                if self.normalize_with_grad:
+                    self._embeddings.weight = torch.nn.functional.normalize(
+                        self._embeddings.weight, p=self.normalize_p, dim=-1)
+                else:
+                    with torch.no_grad():
+                        self._embeddings.weight = torch.nn.Parameter(torch.nn.functional.normalize(
+                            self._embeddings.weight, p=self.normalize_p, dim=-1))
+
+            job.pre_batch_hooks.append(normalize_embeddings)
+
+    def is_plain(self) -> bool:
+        """True when embed(i) == weight[i] exactly (no dropout in training mode)."""
+        return not (self.dropout.p > 0 and self.training)
+
+    def weight_for_scoring(self) -> Tensor:
+        return self._embeddings.weight
+
+    def embed(self, indexes: Tensor) -> Tensor:
+        return self._postprocess(self._embeddings(indexes.long()))
+
+    def embed_all(self) -> Tensor:
+        # identical values and gradient to weight[arange(V)] (lookup_embedder.py:102-107)
+        return self._postprocess(self._embeddings.weight)
+
+    def _postprocess(self, embeddings: Tensor) -> Tensor:
+        if self.dropout.p > 0:
+            embeddings = self.dropout(embeddings)
+        return embeddings
+
+    def _embeddings_all(self) -> Tensor:
+        return self._embeddings.weight
+
+    def penalty(self, **kwargs) -> List:
+        """Lp regularisation (lookup_embedder.py:112-158)."""
+        result = super().penalty(**kwargs)
+        if self.regularize == "" or self.get_option("regularize_weight") == 0.0:
+            return result
+        p = self.get_option("regularize_args.p") if self.has_option("regularize_args.p") else 2
+        w = self.get_option("regularize_weight")
+        if not self.get_option("regularize_args.weighted"):
+            params = self._embeddings_all()
+            result += [(f"{self.configuration_key}.L{p}_penalty", (w / p * params.norm(p=p) ** p).sum())]
+        else:
+            unique_indexes, counts = torch.unique(kwargs["indexes"], return_counts=True)
+            params = self._embeddings(unique_indexes)
+            if p % 2 == 1:
+                params = torch.abs(params)
+            result += [(f"{self.configuration_key}.L{p}_penalty",
+                        (w / p * (params ** p * counts.float().view(-1, 1))).sum() / len(kwargs["indexes"]))]
+        return result

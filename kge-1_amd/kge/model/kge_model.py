@@ -1,0 +1,352 @@
+"""KgeModel / RelationalScorer / KgeEmbedder: the plugin API of the scoring path.
+
+Mirrors LibKGE's kge/model/kge_model.py (KgeBase 26-88, RelationalScorer 91-182,
+KgeEmbedder 185-339, KgeModel 342-746): same class names, factories resolving
+``<model>.class_name`` in ``kge.model``, same method signatures, shapes and error
+behaviour.  What differs is underneath: scorers that implement ``engine_kind`` run on
+libkgescore (gfx950 HIP), and KgeModel.score_sp / score_po / score_sp_po fuse the
+LookupEmbedder gather into the engine call instead of materialising embed_all().
+"""
+from __future__ import annotations
+
+import importlib
+from typing import Any, Dict, List, Optional
+
+import torch
+from torch import Tensor
+
+from ..config import Config, Configurable
+
+SLOTS = [0, 1, 2]
+S, P, O = SLOTS
+
+
+class KgeBase(torch.nn.Module, Configurable):
+    """Base class for models, scorers and embedders (kge_model.py:26-88)."""
+
+    def __init__(self, config: Config, dataset, configuration_key=None):
+        Configurable.__init__(self, config, configuration_key)
+        torch.nn.Module.__init__(self)
+        self.dataset = dataset
+        self.meta: Dict[str, Any] = dict()
+
+    def initialize(self, what: Tensor, initialize: str, initialize_args):
+        try:
+            getattr(torch.nn.init, initialize)(what, **initialize_args)
+        except Exception as e:
+            raise ValueError(
+                "invalid initialization options: {} with args {}".format(initialize, initialize_args)) from e
+
+    def prepare_job(self, job, **kwargs):
+        pass
+
+    def penalty(self, **kwargs) -> List[Tensor]:
+        return []
+
+    def save(self):
+        return self.state_dict(), self.meta
+
+    def load(self, savepoint):
+        self.load_state_dict(savepoint[0])
+        self.meta = savepoint[1]
+
+
+class RelationalScorer(KgeBase):
+    """Scores (s, p, o) embedding triples (kge_model.py:91-182).
+
+    Subclasses either implement ``score_emb_spo`` (row-wise) or override ``score_emb``.
+    Engine-backed scorers set ``engine_kind`` and get score_emb for "spo", "sp_", "_po"
+    from libkgescore; other combines fall back to the generic row-wise expansion.
+    """
+
+    engine_kind: Optional[int] = None
+
+    def __init__(self, config: Config, dataset, configuration_key: str):
+        super().__init__(config, dataset, configuration_key)
+
+    # --- engine parameters
+    def l_norm(self) -> float:
+        return 1.0
+
+    def precision(self) -> int:
+        from .. import _lib
+
+        return _lib.PRECISIONS[self.config.get("engine.precision")]
+
+    def score_emb_spo(self, s_emb: Tensor, p_emb: Tensor, o_emb: Tensor) -> Tensor:
+        return self.score_emb(s_emb, p_emb, o_emb, "spo")
+
+    def score_emb(self, s_emb: Tensor, p_emb: Tensor, o_emb: Tensor, combine: str) -> Tensor:
+        """combine: "spo" -> [n, 1]; "sp_" -> [n, n_o]; "_po" -> [n, n_s]; "s_o" -> [n, n_p]
+        (kge_model.py:120-182)."""
+        n = p_emb.size(0)
+        if self.engine_kind is not None and combine in ("spo", "sp_", "_po"):
+            from .. import engine, _lib
+
+            if combine == "spo":
+                assert s_emb.size(0) == n and o_emb.size(0) == n
+                out = engine.score_spo_emb(self.engine_kind, self.l_norm(), s_emb, p_emb, o_emb)
+            elif combine == "sp_":
+                assert s_emb.size(0) == n
+                out = engine.score_all(self.engine_kind, _lib.DIR_SP, self.precision(), self.l_norm(),
+                                       s_emb, None, p_emb, None, o_emb, None)
+            else:
+                assert o_emb.size(0) == n
+                out = engine.score_all(self.engine_kind, _lib.DIR_PO, self.precision(), self.l_norm(),
+                                       o_emb, None, p_emb, None, s_emb, None)
+            return out.view(n, -1)
+
+        # generic fallback: expand to row-wise triples (kge_model.py:154-178)
+        if combine == "spo":
+            assert s_emb.size(0) == n and o_emb.size(0) == n
+            out = self.score_emb_spo(s_emb, p_emb, o_emb)
+        elif combine == "sp_":
+            assert s_emb.size(0) == n
+            n_o = o_emb.size(0)
+            out = self.score_emb_spo(s_emb.repeat_interleave(n_o, 0), p_emb.repeat_interleave(n_o, 0),
+                                     o_emb.repeat((n, 1)))
+        elif combine == "_po":
+            assert o_emb.size(0) == n
+            n_s = s_emb.size(0)
+            out = self.score_emb_spo(s_emb.repeat((n, 1)), p_emb.repeat_interleave(n_s, 0),
+                                     o_emb.repeat_interleave(n_s, 0))
+        elif combine == "s_o":
+            n = s_emb.size(0)
+            assert o_emb.size(0) == n
+            n_p = p_emb.size(0)
+            out = self.score_emb_spo(s_emb.repeat_interleave(n_p, 0), p_emb.repeat((n, 1)),
+                                     o_emb.repeat_interleave(n_p, 0))
+        else:
+            raise ValueError('cannot handle combine="{}".format(combine)')
+        return out.view(n, -1)
+
+    # --- fused lookup path (indexes instead of embeddings)
+    def score_lookup(self, ent: Tensor, rel: Tensor, e_idx: Tensor, p_idx: Tensor, direction: str,
+                     cand_idx: Optional[Tensor] = None) -> Tensor:
+        """Scores of queries (ent[e_idx], rel[p_idx]) in direction "sp_" / "_po" against
+        ent[cand_idx] (all entities when None), gather fused into the engine."""
+        from .. import engine, _lib
+
+        d = _lib.DIR_SP if direction == "sp_" else _lib.DIR_PO
+        return engine.score_all(self.engine_kind, d, self.precision(), self.l_norm(), ent, e_idx, rel, p_idx,
+                                ent, cand_idx)
+
+    def score_lookup_spo(self, ent: Tensor, rel: Tensor, s: Tensor, p: Tensor, o: Tensor) -> Tensor:
+        from .. import engine
+
+        return engine.score_spo(self.engine_kind, self.l_norm(), ent, s, rel, p, o)
+
+
+class KgeEmbedder(KgeBase):
+    """Embeds a fixed vocabulary (kge_model.py:185-339)."""
+
+    def __init__(self, config: Config, dataset, configuration_key: str, init_for_load_only=False):
+        super().__init__(config, dataset, configuration_key)
+        self.embedder_type: str = self.get_option("type")
+        self.dim: int = self.get_option("dim")
+
+    def _init_embeddings(self, data: Tensor):
+        initialize = self.get_option("initialize")
+        try:
+            initialize_args = dict(self.get_option("initialize_args." + initialize))
+        except KeyError:
+            initialize_args = dict(self.get_option("initialize_args"))
+        if initialize == "uniform_" and "a" not in initialize_args and "b" in initialize_args:
+            initialize_args["a"] = initialize_args["b"] * -1  # kge_model.py:237-240
+        self.initialize(data, initialize, initialize_args)
+
+    @staticmethod
+    def create(config: Config, dataset, configuration_key: str, vocab_size: int,
+               init_for_load_only=False) -> "KgeEmbedder":
+        try:
+            embedder_type = config.get_default(configuration_key + ".type")
+            class_name = config.get(embedder_type + ".class_name")
+            module = importlib.import_module("kge.model")
+        except Exception as e:
+            raise Exception("Can't find {}.type in config".format(configuration_key)) from e
+        try:
+            return getattr(module, class_name)(config, dataset, configuration_key, vocab_size,
+                                               init_for_load_only=init_for_load_only)
+        except (ImportError, AttributeError) as e:
+            raise ValueError("Can't find class {} in 'kge.model' for embedder {}".format(
+                class_name, embedder_type)) from e
+
+    def forward(self, indexes: Tensor) -> Tensor:
+        return self.embed(indexes)
+
+    def embed(self, indexes: Tensor) -> Tensor:
+        raise NotImplementedError
+
+    def embed_all(self) -> Tensor:
+        raise NotImplementedError
+
+
+class KgeModel(KgeBase):
+    """Entity + relation embedders and a RelationalScorer (kge_model.py:342-746)."""
+
+    def __init__(self, config: Config, dataset, scorer, create_embedders=True, configuration_key=None,
+                 init_for_load_only=False):
+        super().__init__(config, dataset, configuration_key)
+        if create_embedders:
+            self._entity_embedder = KgeEmbedder.create(
+                config, dataset, self.configuration_key + ".entity_embedder", dataset.num_entities(),
+                init_for_load_only=init_for_load_only)
+            self._relation_embedder = KgeEmbedder.create(
+                config, dataset, self.configuration_key + ".relation_embedder", dataset.num_relations(),
+                init_for_load_only=init_for_load_only)
+        if isinstance(scorer, type):
+            self._scorer = scorer(config=config, dataset=dataset, configuration_key=self.configuration_key)
+        else:
+            self._scorer = scorer
+
+    def _init_configuration(self, config: Config, configuration_key: Optional[str]):
+        Configurable._init_configuration(self, config, configuration_key)
+        if not getattr(self, "model", None):
+            if self.configuration_key:
+                self.model: str = config.get(self.configuration_key + ".type")
+            else:
+                self.model: str = config.get("model")
+                self.configuration_key = self.model
+
+    @staticmethod
+    def create(config: Config, dataset, configuration_key: Optional[str] = None,
+               init_for_load_only=False) -> "KgeModel":
+        try:
+            model_name = config.get(configuration_key + ".type") if configuration_key else config.get("model")
+            config._import(model_name)
+            class_name = config.get(model_name + ".class_name")
+            module = importlib.import_module("kge.model")
+        except Exception as e:
+            raise Exception("Can't find {}.type in config".format(configuration_key)) from e
+        try:
+            model = getattr(module, class_name)(config=config, dataset=dataset,
+                                                configuration_key=configuration_key,
+                                                init_for_load_only=init_for_load_only)
+        except (ImportError, AttributeError) as e:
+            raise ValueError("Can't find class {} in 'kge.model' for model {}".format(class_name, model_name)) from e
+        model.to(config.get("job.device"))
+        return model
+
+    @staticmethod
+    def create_from(checkpoint: Dict, dataset=None, use_tmp_log_folder=True, new_config: Config = None):
+        """Rebuild a model from a checkpoint dict written by ``save`` (plain tensors and
+        an options dict; loads with ``torch.load(weights_only=True)``)."""
+        from ..dataset import Dataset
+
+        config = Config(load_default=True)
+        config.load_options(checkpoint["config"])
+        if new_config is not None:
+            config.load_options(new_config.options)
+        if dataset is None:
+            dataset = Dataset(config, None)
+        model = KgeModel.create(config, dataset, init_for_load_only=True)
+        model.load_state_dict(checkpoint["model"])
+        model.eval()
+        return model
+
+    def prepare_job(self, job, **kwargs):
+        super().prepare_job(job, **kwargs)
+        self._entity_embedder.prepare_job(job, **kwargs)
+        self._relation_embedder.prepare_job(job, **kwargs)
+
+    def penalty(self, **kwargs) -> List[Tensor]:
+        if "batch" in kwargs and "triples" in kwargs["batch"]:
+            triples = kwargs["batch"]["triples"].to(self.config.get("job.device"))
+            return (super().penalty(**kwargs)
+                    + self.get_s_embedder().penalty(indexes=triples[:, S], **kwargs)
+                    + self.get_p_embedder().penalty(indexes=triples[:, P], **kwargs)
+                    + self.get_o_embedder().penalty(indexes=triples[:, O], **kwargs))
+        return (super().penalty(**kwargs) + self.get_s_embedder().penalty(**kwargs)
+                + self.get_p_embedder().penalty(**kwargs) + self.get_o_embedder().penalty(**kwargs))
+
+    def get_s_embedder(self) -> KgeEmbedder:
+        return self._entity_embedder
+
+    def get_o_embedder(self) -> KgeEmbedder:
+        return self._entity_embedder
+
+    def get_p_embedder(self) -> KgeEmbedder:
+        return self._relation_embedder
+
+    def get_scorer(self) -> RelationalScorer:
+        return self._scorer
+
+    # ----------------------------------------------------------------- fused lookup path
+    def _lookup_tables(self):
+        """(entity weight, relation weight) when the fused engine path applies: both
+        embedders are plain lookups without dropout and the scorer is engine-backed."""
+        from .embedder.lookup_embedder import LookupEmbedder
+
+        e, r = self.get_s_embedder(), self.get_p_embedder()
+        if (self._scorer.engine_kind is not None and isinstance(e, LookupEmbedder)
+                and isinstance(r, LookupEmbedder) and e is self.get_o_embedder()
+                and e.is_plain() and r.is_plain()):
+            return e.weight_for_scoring(), r.weight_for_scoring()
+        return None
+
+    # ----------------------------------------------------------------- scoring API
+    def score_spo(self, s: Tensor, p: Tensor, o: Tensor, direction=None) -> Tensor:
+        """Scores of triples (s_i, p_i, o_i) -> [n] (kge_model.py:620-637)."""
+        tabs = self._lookup_tables()
+        if tabs is not None:
+            return self._scorer.score_lookup_spo(tabs[0], tabs[1], s, p, o).view(-1)
+        s = self.get_s_embedder().embed(s)
+        p = self.get_p_embedder().embed(p)
+        o = self.get_o_embedder().embed(o)
+        return self._scorer.score_emb(s, p, o, combine="spo").view(-1)
+
+    def score_sp(self, s: Tensor, p: Tensor, o: Tensor = None) -> Tensor:
+        """[n, E] (or [n, |o|]) scores of (s_i, p_i, e_j) (kge_model.py:639-659)."""
+        tabs = self._lookup_tables()
+        if tabs is not None:
+            return self._scorer.score_lookup(tabs[0], tabs[1], s, p, "sp_", o)
+        s = self.get_s_embedder().embed(s)
+        p = self.get_p_embedder().embed(p)
+        o = self.get_o_embedder().embed_all() if o is None else self.get_o_embedder().embed(o)
+        return self._scorer.score_emb(s, p, o, combine="sp_")
+
+    def score_po(self, p: Tensor, o: Tensor, s: Tensor = None) -> Tensor:
+        """[n, E] (or [n, |s|]) scores of (e_j, p_i, o_i) (kge_model.py:661-682)."""
+        tabs = self._lookup_tables()
+        if tabs is not None:
+            return self._scorer.score_lookup(tabs[0], tabs[1], o, p, "_po", s)
+        s = self.get_s_embedder().embed_all() if s is None else self.get_s_embedder().embed(s)
+        o = self.get_o_embedder().embed(o)
+        p = self.get_p_embedder().embed(p)
+        return self._scorer.score_emb(s, p, o, combine="_po")
+
+    def score_so(self, s: Tensor, o: Tensor, p: Tensor = None) -> Tensor:
+        """[n, R] (or [n, |p|]) scores of (s_i, r_j, o_i) (kge_model.py:684-704)."""
+        s = self.get_s_embedder().embed(s)
+        o = self.get_o_embedder().embed(o)
+        p = self.get_p_embedder().embed_all() if p is None else self.get_p_embedder().embed(p)
+        return self._scorer.score_emb(s, p, o, combine="s_o")
+
+    def score_sp_po(self, s: Tensor, p: Tensor, o: Tensor, entity_subset: Tensor = None) -> Tensor:
+        """cat(score_sp(s,p,subset), score_po(p,o,subset)) -> [n, 2|subset|]
+        (kge_model.py:706-746)."""
+        tabs = self._lookup_tables()
+        if tabs is not None:
+            sp = self._scorer.score_lookup(tabs[0], tabs[1], s, p, "sp_", entity_subset)
+            po = self._scorer.score_lookup(tabs[0], tabs[1], o, p, "_po", entity_subset)
+            return torch.cat((sp, po), dim=1)
+        s = self.get_s_embedder().embed(s)
+        p = self.get_p_embedder().embed(p)
+        o = self.get_o_embedder().embed(o)
+        if self.get_s_embedder() is self.get_o_embedder():
+            if entity_subset is not None:
+                all_entities = self.get_s_embedder().embed(entity_subset)
+            else:
+                all_entities = self.get_s_embedder().embed_all()
+            sp_scores = self._scorer.score_emb(s, p, all_entities, combine="sp_")
+            po_scores = self._scorer.score_emb(all_entities, p, o, combine="_po")
+        else:
+            if entity_subset is not None:
+                all_objects = self.get_o_embedder().embed(entity_subset)
+                all_subjects = self.get_s_embedder().embed(entity_subset)
+            else:
+                all_objects = self.get_o_embedder().embed_all()
+                all_subjects = self.get_s_embedder().embed_all()
+            sp_scores = self._scorer.score_emb(s, p, all_objects, combine="sp_")
+            po_scores = self._scorer.score_emb(all_subjects, p, o, combine="_po")
+        return torch.cat((sp_scores, po_scores), dim=1)

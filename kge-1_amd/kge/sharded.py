@@ -1,0 +1,152 @@
+"""Entity-table row sharding over the GPUs of one node.
+
+One process per GPU (torch.distributed, backend "nccl" = RCCL over xGMI).  GPU k owns
+entity rows [k*ceil(E/W), (k+1)*ceil(E/W)) -- exactly the reference's
+``entity_ranking.chunk_size`` decomposition (entity_ranking.py:153-216), whose per-chunk
+rank/tie counts sum exactly.  The relation table is replicated.
+
+Data path of one all-entities scoring step for a global batch of W*B queries (each rank
+contributes B):
+  1. all_gather of the (entity, relation) query indexes       -- W*B*16 bytes
+  2. the owner of each query entity row computes the query vector q = prep(e, r), the
+     others contribute zeros; all_reduce(SUM) of Q [W*B, d]     -- W*B*d*4 bytes
+     (x + 0 + ... + 0 == x exactly, so every rank holds bit-identical Q)
+  3. local contraction against the rank's shard: S_k [W*B, E_k] on the engine.
+Entity ranking then needs only an all_reduce(SUM) of the int64 greater/tie counts
+(rank_counts over the local shard) -- no score ever crosses the link.  The
+"all-gather of per-shard top-k" in the north star is ``topk``: per-shard top-k (score,
+global id), all_gather, merge.
+
+The compute ops are injected (``ops``) so the exchange logic is testable with the gloo
+backend on CPU (tests/test_sharded_gloo.py); the default ops are the HIP engine.
+"""
+from __future__ import annotations
+
+import math
+from typing import Optional
+
+import torch
+import torch.distributed as dist
+
+
+class EngineOps:
+    """Default compute: libkgescore."""
+
+    def __init__(self, kind: int, precision: int, l_norm: float = 1.0):
+        from . import _lib
+
+        self.L = _lib
+        self.kind = kind
+        self.precision = precision
+        self.l_norm = l_norm
+
+    def prep(self, direction, ent, eidx, rel, ridx):
+        n = eidx.numel()
+        return self.L.prep_query(self.kind, direction, ent, eidx, rel, ridx, n, ent.shape[1], rel.shape[1])
+
+    def score(self, q, tab):
+        from .engine import BILINEAR, dist_kind
+
+        if self.kind in BILINEAR:
+            return self.L.score_dot(q, tab, None, self.precision)
+        dk, sign = dist_kind(self.kind, self.l_norm)
+        return self.L.score_dist(dk, sign, q, tab, None)
+
+    def spo(self, ent_s, rel, p, ent_o):
+        n = p.numel()
+        ar = torch.arange(n, device=rel.device)
+        so = torch.cat((ent_s, ent_o), 0)
+        return self.L.score_spo(self.kind, self.l_norm, so, ar, rel, p, ar + n, so.shape[1], rel.shape[1])
+
+    def rank_counts(self, s, c0, true_idx, true_score, fp, fc, tp, tc, greater, ties):
+        self.L.rank_counts(s, c0, true_idx, true_score, fp, fc, tp, tc, greater, ties)
+
+
+def shard_bounds(num_entities: int, world: int, rank: int):
+    per = math.ceil(num_entities / world)
+    lo = min(num_entities, rank * per)
+    return lo, min(num_entities, lo + per)
+
+
+class RowShardedScorer:
+    def __init__(self, ent_shard: torch.Tensor, lo: int, hi: int, num_entities: int, rel: torch.Tensor, ops,
+                 group=None):
+        self.ent = ent_shard
+        self.lo, self.hi = lo, hi
+        self.E = num_entities
+        self.rel = rel
+        self.ops = ops
+        self.group = group
+        self.world = dist.get_world_size(group)
+        self.rank = dist.get_rank(group)
+
+    # ---------------------------------------------------------------- helpers
+    def _all_gather_1d(self, x: torch.Tensor) -> torch.Tensor:
+        out = [torch.empty_like(x) for _ in range(self.world)]
+        dist.all_gather(out, x.contiguous(), group=self.group)
+        return torch.cat(out)
+
+    def _owned_rows(self, ids: torch.Tensor):
+        owned = (ids >= self.lo) & (ids < self.hi)
+        local = (ids - self.lo).clamp(0, max(0, self.hi - self.lo - 1))
+        return owned, local
+
+    def gather_rows(self, ids: torch.Tensor) -> torch.Tensor:
+        """Full entity rows for global ids (every rank gets bit-identical rows)."""
+        owned, local = self._owned_rows(ids)
+        rows = self.ent[local]
+        rows = torch.where(owned[:, None], rows, torch.zeros_like(rows))
+        dist.all_reduce(rows, group=self.group)
+        return rows
+
+    def queries(self, e: torch.Tensor, p: torch.Tensor, direction: int):
+        """Steps 1-2: global index exchange + owner-computed query rows (all_reduce)."""
+        e_all = self._all_gather_1d(e)
+        p_all = self._all_gather_1d(p)
+        owned, local = self._owned_rows(e_all)
+        q = self.ops.prep(direction, self.ent, local, self.rel, p_all)
+        q = torch.where(owned[:, None], q, torch.zeros_like(q))
+        dist.all_reduce(q, group=self.group)
+        return q, e_all, p_all
+
+    # ---------------------------------------------------------------- scoring
+    def score_sp(self, s: torch.Tensor, p: torch.Tensor, direction: int = 0) -> torch.Tensor:
+        """Local shard of the global score matrix: [W*B, hi - lo]."""
+        q, _, _ = self.queries(s, p, direction)
+        return self.ops.score(q, self.ent)
+
+    def topk(self, scores_local: torch.Tensor, k: int):
+        """All-gather of per-shard top-k (score, global entity id), merged on every rank."""
+        kk = min(k, scores_local.shape[1])
+        v, i = torch.topk(scores_local, kk, dim=1)
+        i = i + self.lo
+        if kk < k:  # pad so every rank contributes the same shape
+            pad = k - kk
+            v = torch.cat([v, torch.full((v.shape[0], pad), -math.inf, device=v.device)], 1)
+            i = torch.cat([i, torch.full((i.shape[0], pad), -1, device=i.device, dtype=i.dtype)], 1)
+        vs = [torch.empty_like(v) for _ in range(self.world)]
+        is_ = [torch.empty_like(i) for _ in range(self.world)]
+        dist.all_gather(vs, v.contiguous(), group=self.group)
+        dist.all_gather(is_, i.contiguous(), group=self.group)
+        V, I = torch.cat(vs, 1), torch.cat(is_, 1)
+        tv, ti = torch.topk(V, k, dim=1)
+        return tv, torch.gather(I, 1, ti)
+
+    # ---------------------------------------------------------------- eval
+    def rank_counts(self, s, p, o, f_sp, f_po, t_sp=None, t_po=None):
+        """Global greater/tie counts of the true o (sp_) and s (_po) for a batch that
+        every rank holds identically (s, p, o [B]); CSR filter lists as in
+        EntityRankingJob.  Returns greater/ties [2 directions, 3 rankings, B] summed over
+        shards with one all_reduce."""
+        B = s.numel()
+        rows = self.gather_rows(torch.cat([s, o]))  # full s rows then o rows, on every rank
+        ar = torch.arange(B, device=s.device)
+        true = self.ops.spo(rows[:B], self.rel, p, rows[B:])
+        counts = torch.zeros(2, 2, 3 * B, dtype=torch.int64, device=s.device)
+        for di, (eidx, direction, tgt, f, t) in enumerate(((ar, 0, o, f_sp, t_sp), (ar + B, 1, s, f_po, t_po))):
+            q = self.ops.prep(direction, rows, eidx, self.rel, p)
+            sc = self.ops.score(q, self.ent)
+            self.ops.rank_counts(sc, self.lo, tgt, true, f[0], f[1], t[0] if t is not None else None,
+                                 t[1] if t is not None else None, counts[di, 0], counts[di, 1])
+        dist.all_reduce(counts, group=self.group)
+        return counts

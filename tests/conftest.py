@@ -15,3 +15,6 @@ GOLDEN = os.path.join(ROOT, "tests", "golden")
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (runs the HIP kernels)")
     config.addinivalue_line("markers", "slow: long-running")
+
+# tests validate every index vector against its table before launching a kernel
+os.environ.setdefault("KGE_CHECK_INDEX", "1")

@@ -1,0 +1,221 @@
+"""GPU parity of the drop-in plugin API (kge.model.KgeModel / RelationalScorer /
+LookupEmbedder, kge.job.EntityRankingJob / TrainingJob1vsAll) against the reference's
+golden vectors.  Everything here runs on libkgescore; a missing library raises."""
+import glob
+import json
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import GOLDEN
+from oracle import kge_oracle as K
+
+pytestmark = pytest.mark.gpu
+SCORER_FILES = sorted(glob.glob(os.path.join(GOLDEN, "scorer_*.npz")))
+
+
+@pytest.fixture(scope="module", autouse=True)
+def need_gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from kge import _lib
+    _lib.lib()
+
+
+def make_model(model, dim, E, R, ent, rel, extra=None, precision="bf16x3"):
+    from kge import Config, Dataset, KgeModel
+
+    c = Config()
+    c.set("model", model)
+    c._import(model)
+    c.set("job.device", "cuda")
+    c.set("dataset.num_entities", E)
+    c.set("dataset.num_relations", R)
+    c.set("lookup_embedder.dim", dim)
+    c.set("engine.precision", precision)
+    for k, v in (extra or {}).items():
+        c.set(k, v)
+    m = KgeModel.create(c, Dataset(c, None))
+    with torch.no_grad():
+        m._entity_embedder._embeddings.weight.copy_(torch.from_numpy(ent))
+        m._relation_embedder._embeddings.weight.copy_(torch.from_numpy(rel))
+    return m
+
+
+def model_from_fixture(f, precision):
+    meta = json.loads(str(f["meta"]))
+    extra = {}
+    if meta["model"] in ("transe", "rotate"):
+        extra[f"{meta['model']}.l_norm"] = float(meta["l_norm"])
+    m = make_model(meta["model"], f["ent"].shape[1], f["ent"].shape[0], f["rel"].shape[0], f["ent"], f["rel"], extra,
+                   precision)
+    return m, meta
+
+
+def rel_err(x, ref):
+    x = np.asarray(x, np.float64)
+    ref = np.asarray(ref, np.float64)
+    scale = np.abs(ref).max(axis=-1, keepdims=True) if ref.ndim == 2 else np.abs(ref).max()
+    return float((np.abs(x - ref) / np.maximum(scale, 1e-30)).max())
+
+
+def check(meta, name, got, ref, prec):
+    model = meta["model"]
+    exact = meta["regime"] == "dyadic" and (model in K.BILINEAR or (model == "transe" and meta["l_norm"] == 1
+                                                                      and name != "spo"))
+    if exact:
+        np.testing.assert_array_equal(got, ref, err_msg=name)
+    else:
+        tol = 1e-5 if (model in K.DISTANCE or name == "spo") else (2e-5 if prec == "bf16x3" else 2e-6)
+        assert rel_err(got, ref) < tol, (name, rel_err(got, ref))
+
+
+@pytest.mark.parametrize("path", ["lookup", "emb"])
+@pytest.mark.parametrize("prec", ["bf16x3", "fp32"])
+@pytest.mark.parametrize("fn", SCORER_FILES, ids=lambda f: os.path.basename(f)[7:-4])
+def test_model_scores_and_grads(fn, prec, path):
+    f = np.load(fn)
+    m, meta = model_from_fixture(f, prec)
+    dev = "cuda"
+    s, p, o, sub = (torch.from_numpy(f[k]).to(dev) for k in ("s", "p", "o", "subset"))
+    m.train()
+    if path == "lookup":
+        spo = m.score_spo(s, p, o)
+        sp_all = m.score_sp(s, p)
+        po_all = m.score_po(p, o)
+    else:  # generic plugin path: embeddings into RelationalScorer.score_emb
+        es, ep, eo = m.get_s_embedder().embed(s), m.get_p_embedder().embed(p), m.get_o_embedder().embed(o)
+        allE = m.get_o_embedder().embed_all()
+        spo = m.get_scorer().score_emb(es, ep, eo, "spo").view(-1)
+        sp_all = m.get_scorer().score_emb(es, ep, allE, "sp_")
+        po_all = m.get_scorer().score_emb(allE, ep, eo, "_po")
+    w_sp, w_po, w_spo = (torch.from_numpy(f[k]).to(dev) for k in ("w_sp", "w_po", "w_spo"))
+    loss = (w_sp * sp_all).sum() + (w_po * po_all).sum() + (w_spo * spo).sum()
+    m.zero_grad()
+    loss.backward()
+    with torch.no_grad():
+        outs = dict(spo=spo, sp_all=sp_all, po_all=po_all, sp_sub=m.score_sp(s, p, sub), po_sub=m.score_po(p, o, sub),
+                    sppo_sub=m.score_sp_po(s, p, o, sub), sppo_all=m.score_sp_po(s, p, o))
+    for k, v in outs.items():
+        check(meta, k, v.detach().cpu().numpy(), f[k], prec)
+    ge = m._entity_embedder._embeddings.weight.grad.cpu().numpy()
+    gr = m._relation_embedder._embeddings.weight.grad.cpu().numpy()
+    tol = 1e-4 if (prec == "bf16x3" and meta["model"] in K.BILINEAR) else 1e-5
+    assert np.abs(ge - f["g_ent"]).max() <= tol * np.abs(f["g_ent"]).max()
+    assert np.abs(gr - f["g_rel"]).max() <= tol * np.abs(f["g_rel"]).max()
+
+
+def eval_job(f, tag, precision):
+    from kge import Config, Dataset
+    from kge.job import EntityRankingJob
+
+    meta = json.loads(str(f["meta"]))
+    c = Config()
+    c.set("model", "complex")
+    c._import("complex")
+    c.set("job.device", "cuda")
+    c.set("lookup_embedder.dim", meta["dim"])
+    c.set("engine.precision", precision)
+    c.set("eval.batch_size", meta["batch_size"])
+    c.set("eval.split", "valid")
+    c.set("entity_ranking.chunk_size", -1 if tag == "full" else meta["chunk8"])
+    c.set("dataset.num_entities", meta["E"])
+    c.set("dataset.num_relations", meta["R"])
+    ds = Dataset(c, None)
+    ds._triples = {k: torch.from_numpy(f["tri_" + k].astype(np.int32)) for k in ("train", "valid", "test")}
+    m = make_model("complex", meta["dim"], meta["E"], meta["R"], f["ent"], f["rel"], precision=precision)
+    m.config = c
+    m.get_scorer().config = c
+    job = EntityRankingJob(c, ds, model=m)
+    job.capture_ranks = True
+    trace = job.run()
+    return job, trace
+
+
+@pytest.mark.parametrize("regime,precision", [("dyadic", "bf16x3"), ("dyadic", "fp32"), ("normal", "fp32")])
+@pytest.mark.parametrize("tag", ["full", "chunk8"])
+def test_entity_ranking_vs_golden(regime, precision, tag):
+    f = np.load(os.path.join(GOLDEN, f"eval_{regime}.npz"))
+    ref_metrics = json.loads(str(f["metrics"]))[tag]
+    job, trace = eval_job(f, tag, precision)
+    for k, v in job.ranks.items():
+        np.testing.assert_array_equal(v, f[f"{tag}_{k}"], err_msg=k)
+    for k, v in ref_metrics.items():
+        assert trace[k] == pytest.approx(v, rel=1e-6, abs=1e-9), k
+
+
+def test_entity_ranking_bf16x3_normal_near_ties_only():
+    """bf16x3 on real-valued data: a rank may only move where a competitor lies within
+    the 1e-4 score tolerance of the true score."""
+    f = np.load(os.path.join(GOLDEN, "eval_normal.npz"))
+    ref_metrics = json.loads(str(f["metrics"]))["full"]
+    job, trace = eval_job(f, "full", "bf16x3")
+    diff = sum(int((job.ranks[k] != f["full_" + k]).sum()) for k in job.ranks)
+    total = sum(len(v) for v in job.ranks.values())
+    assert diff <= 0.02 * total
+    assert trace["mean_reciprocal_rank_filtered"] == pytest.approx(ref_metrics["mean_reciprocal_rank_filtered"],
+                                                                   rel=1e-3)
+
+
+def test_train_1vsall_vs_golden():
+    from kge import Config, Dataset
+    from kge.job import TrainingJob
+
+    f = np.load(os.path.join(GOLDEN, "train1vsall_complex.npz"))
+    meta = json.loads(str(f["meta"]))
+    c = Config()
+    c.set("model", "complex")
+    c._import("complex")
+    c.set("job.device", "cuda")
+    c.set("lookup_embedder.dim", meta["dim"])
+    c.set("train.type", "1vsAll")
+    c.set("train.optimizer", "Adagrad")
+    c.set("train.optimizer_args", {"lr": meta["lr"]})
+    c.set("dataset.num_entities", meta["E"])
+    c.set("dataset.num_relations", meta["R"])
+    ds = Dataset(c, None)
+    ds._triples = {"train": torch.from_numpy(f["batches"].reshape(-1, 3).astype(np.int32))}
+    job = TrainingJob.create(c, ds)
+    with torch.no_grad():
+        job.model._entity_embedder._embeddings.weight.copy_(torch.from_numpy(f["ent0"]))
+        job.model._relation_embedder._embeddings.weight.copy_(torch.from_numpy(f["rel0"]))
+    job._prepare()
+    losses = []
+    for b in range(len(f["batches"])):
+        job.optimizer.zero_grad()
+        res = job._process_batch(b, {"triples": torch.from_numpy(f["batches"][b])})
+        job.optimizer.step()
+        losses.append(res.avg_loss)
+    np.testing.assert_allclose(losses, f["losses"], rtol=1e-5)
+    e1 = job.model._entity_embedder._embeddings.weight.detach().cpu().numpy()
+    r1 = job.model._relation_embedder._embeddings.weight.detach().cpu().numpy()
+    np.testing.assert_allclose(e1, f["ent1"], atol=1e-4)
+    np.testing.assert_allclose(r1, f["rel1"], atol=1e-4)
+
+
+def test_reciprocal_relations_model():
+    """(?, p, o) answered as (o, p + R, ?) with the sp_ kernel (reciprocal_relations_model.py:67-74)."""
+    from kge import Config, Dataset, KgeModel
+
+    torch.manual_seed(0)
+    c = Config()
+    c.set("model", "reciprocal_relations_model")
+    c._import("reciprocal_relations_model")
+    c.set("reciprocal_relations_model.base_model.type", "complex")
+    c._import("complex")
+    c.set("job.device", "cuda")
+    c.set("lookup_embedder.dim", 32)
+    c.set("dataset.num_entities", 50)
+    c.set("dataset.num_relations", 5)
+    m = KgeModel.create(c, Dataset(c, None))
+    ent = m._entity_embedder._embeddings.weight.detach().double().cpu().numpy()
+    rel = m._relation_embedder._embeddings.weight.detach().double().cpu().numpy()
+    p = torch.tensor([0, 1, 4], device="cuda")
+    o = torch.tensor([3, 7, 49], device="cuda")
+    got = m.score_po(p, o).detach().cpu().numpy()
+    ref = K.prep_sp("complex", ent[o.cpu().numpy()], rel[p.cpu().numpy() + 5]) @ ent.T
+    assert rel_err(got, ref) < 2e-5
+    with pytest.raises(Exception):
+        m.score_spo(p, p, o)

@@ -1,0 +1,127 @@
+"""CPU tests of the host side: the C-ABI library loads and exports every declared symbol,
+config / dataset / index logic, model construction, and the no-fallback contract."""
+import json
+import os
+import re
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import GOLDEN, ROOT
+
+
+def test_library_exports_every_header_symbol():
+    from kge import _lib
+
+    header = open(os.path.join(ROOT, "include", "kgescore.h")).read()
+    declared = set(re.findall(r"^\s*(?:int|const char\*)\s+(kge_\w+)\s*\(", header, re.M))
+    assert declared == set(_lib.SIGNATURES), declared ^ set(_lib.SIGNATURES)
+    lib = _lib.lib()
+    for name in declared:
+        assert hasattr(lib, name), name
+    assert lib.kge_version() >= 100
+    assert lib.kge_error_string(1001).decode().startswith("kgescore: invalid argument")
+
+
+def test_config_defaults_and_imports():
+    from kge import Config
+
+    c = Config()
+    c.set("model", "complex")
+    c._import("complex")
+    assert c.get_default("complex.entity_embedder.dim") == 100  # via lookup_embedder.dim
+    c.set("lookup_embedder.dim", 512)
+    assert c.get_default("complex.relation_embedder.dim") == 512
+    c._import("rotate")
+    assert c.get_default("rotate.relation_embedder.dim") == -1
+    assert c.get_default("rotate.relation_embedder.initialize") == "uniform_"
+    assert c.get("engine.precision") == "bf16x3"
+    with pytest.raises(KeyError):
+        c.get("no.such.key")
+    with pytest.raises(ValueError):
+        c.check("entity_ranking.tie_handling", ["best_rank"])
+
+
+def test_model_dims_match_reference_shapes():
+    from kge import Config, Dataset, KgeModel
+
+    rows = json.loads(str(np.load(os.path.join(GOLDEN, "shapes.npz"))["table"]))
+    for model, d, d_e, d_r in rows:
+        c = Config()
+        c.set("model", model)
+        c.set("job.device", "cpu")
+        c.set("dataset.num_entities", 10)
+        c.set("dataset.num_relations", 3)
+        c.set("lookup_embedder.dim", d)
+        m = KgeModel.create(c, Dataset(c, None))
+        assert m._entity_embedder.dim == d_e and m._relation_embedder.dim == d_r, model
+        assert list(m.state_dict()) == ["_entity_embedder._embeddings.weight",
+                                        "_relation_embedder._embeddings.weight"]
+
+
+def test_scoring_on_cpu_raises_no_fallback():
+    from kge import Config, Dataset, KgeModel
+    from kge._lib import EngineError
+
+    c = Config()
+    c.set("model", "complex")
+    c.set("job.device", "cpu")
+    c.set("dataset.num_entities", 10)
+    c.set("dataset.num_relations", 3)
+    c.set("lookup_embedder.dim", 8)
+    m = KgeModel.create(c, Dataset(c, None))
+    with pytest.raises(EngineError):
+        m.score_sp(torch.tensor([0, 1]), torch.tensor([0, 2]))
+
+
+def test_dataset_loads_reference_fixture():
+    from kge import Config, Dataset
+
+    c = Config()
+    ds = Dataset.create(c, folder=os.path.join(GOLDEN, "dataset_test"))
+    assert ds.num_entities() == 4 and ds.num_relations() == 3
+    assert ds.split("train").dtype == torch.int32
+    assert [len(ds.split(s)) for s in ("train", "valid", "test")] == [4, 2, 2]
+    idx = ds.index("train_sp_to_o")
+    assert idx.get((0, 0)).tolist() == [1]
+    assert idx.get((3, 3)).numel() == 0
+
+
+def test_synthetic_fb15k237_shape_exact_and_unique():
+    from kge import Config, Dataset
+
+    ds = Dataset.synthetic(Config(), "fb15k-237", seed=0)
+    sizes = [len(ds.split(s)) for s in ("train", "valid", "test")]
+    assert sizes == [272115, 17535, 20466]
+    allt = torch.cat([ds.split(s) for s in ("train", "valid", "test")]).long().numpy()
+    code = (allt[:, 0] * 237 + allt[:, 1]) * 14541 + allt[:, 2]
+    assert len(np.unique(code)) == len(code)
+    assert allt[:, 0].max() < 14541 and allt[:, 1].max() < 237
+    again = Dataset.synthetic(Config(), "fb15k-237", seed=0)
+    assert torch.equal(again.split("test"), ds.split("test"))
+
+
+def test_kvsall_index_csr_matches_dict():
+    from kge.dataset import KvsAllIndex
+
+    rng = np.random.default_rng(0)
+    t = np.stack([rng.integers(0, 30, 500), rng.integers(0, 4, 500), rng.integers(0, 30, 500)], 1)
+    idx = KvsAllIndex(t, (0, 1), 2)
+    ref = {}
+    for s, p, o in t.tolist():
+        ref.setdefault((s, p), set()).add(o)
+    q = np.stack([rng.integers(0, 32, 200), rng.integers(0, 5, 200)], 1)
+    ptr, col = idx.csr_for(q)
+    for i, (a, b) in enumerate(q.tolist()):
+        assert sorted(col[ptr[i]:ptr[i + 1]].tolist()) == sorted(ref.get((a, b), set()))
+        assert idx.get((a, b)).tolist() == sorted(ref.get((a, b), set()))
+
+
+def test_csr_minus():
+    from kge.job.entity_ranking import _csr_minus
+
+    pa, ca = np.array([0, 3, 3, 5]), np.array([1, 2, 3, 7, 8])
+    pb, cb = np.array([0, 1, 2, 3]), np.array([2, 9, 8])
+    p, c = _csr_minus(pa, ca, pb, cb, 10)
+    assert p.tolist() == [0, 2, 2, 3] and c.tolist() == [1, 3, 7]

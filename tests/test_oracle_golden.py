@@ -80,3 +80,18 @@ def test_relation_dims():
     for model, d, d_e, d_r in rows:
         assert K.relation_dim(model, d) == d_r
         assert d_e == d
+
+
+@pytest.mark.parametrize("regime", ["normal", "dyadic"])
+@pytest.mark.parametrize("name", ["complex", "complex512"])
+def test_refseq_bitwise(name, regime):
+    """The CPU-baseline replica (oracle/refseq.py) reproduces the reference bit-for-bit."""
+    import torch
+    from oracle import refseq
+
+    f = np.load(os.path.join(GOLDEN, f"scorer_{name}_{regime}.npz"))
+    ent, rel = torch.from_numpy(f["ent"]), torch.from_numpy(f["rel"])
+    s, p, o = (torch.from_numpy(f[k]) for k in ("s", "p", "o"))
+    torch.set_num_threads(4)
+    np.testing.assert_array_equal(refseq.complex_score_sp(ent, rel, s, p).numpy(), f["sp_all"])
+    np.testing.assert_array_equal(refseq.complex_score_po(ent, rel, p, o).numpy(), f["po_all"])
