@@ -91,6 +91,20 @@ int kge_score_dot(const float* q, int64_t ldq, const float* t, int64_t ldt,
                   const int64_t* tidx, int64_t n, int64_t m, int d, float* s,
                   int64_t lds, int precision, void* stream);
 
+/* Split n fp32 rows into bf16 hi / lo planes with x ~= hi + lo (|x - hi - lo| <= 2^-16|x|).
+ * Planes are row-major [n][ldo], ldo >= round_up(d, 32) and a multiple of 8; columns
+ * d .. ldo-1 are written as zero.  Feeds kge_score_dot_split. */
+int kge_split_rows(const float* x, int64_t ldx, int64_t n, int d, void* hi, void* lo,
+                   int64_t ldo, void* stream);
+
+/* The production bf16x3 contraction: S[i, j] = sum_k (qhi + qlo)[i, k] * T[row(j), k]
+ * with the query rows pre-split (kge_split_rows) and the entity rows split on the fly.
+ * Persistent, XCD-grouped 256 x 256 (n > 128) or 128 x 256 tiles.  Requires d % 4 == 0,
+ * ldt % 4 == 0, 16-B aligned t / q planes. */
+int kge_score_dot_split(const void* q_hi, const void* q_lo, int64_t ldq, const float* t,
+                        int64_t ldt, const int64_t* tidx, int64_t n, int64_t m, int d,
+                        float* s, int64_t lds, void* stream);
+
 /* dQ[i, k] (+)= sum_j G[i, j] * T[row(j), k]   (accumulate != 0: add into dQ) */
 int kge_score_dot_bwd_q(const float* g, int64_t ldg, const float* t, int64_t ldt,
                         const int64_t* tidx, int64_t n, int64_t m, int d, float* dq,

@@ -35,6 +35,8 @@ SIGNATURES = {
     "kge_prep_query_bwd": ([_I, _I, _P, _I64, _P, _P, _I64, _P, _I64, _I, _I, _P, _I64, _P, _I64,
                             _P, _I64, _P], _I),
     "kge_score_dot": ([_P, _I64, _P, _I64, _P, _I64, _I64, _I, _P, _I64, _I, _P], _I),
+    "kge_split_rows": ([_P, _I64, _I64, _I, _P, _P, _I64, _P], _I),
+    "kge_score_dot_split": ([_P, _P, _I64, _P, _I64, _P, _I64, _I64, _I, _P, _I64, _P], _I),
     "kge_score_dot_bwd_q": ([_P, _I64, _P, _I64, _P, _I64, _I64, _I, _P, _I64, _I, _I, _P], _I),
     "kge_score_dot_bwd_t": ([_P, _I64, _P, _I64, _P, _I64, _I64, _I, _P, _I64, _I, _P], _I),
     "kge_score_dist": ([_I, _F, _P, _I64, _P, _I64, _P, _I64, _I64, _I, _P, _I64, _P], _I),
@@ -160,6 +162,39 @@ def score_dot(q, t, tidx, precision, out=None):
     _check(lib().kge_score_dot(ptr(q), rows(q), ptr(t), rows(t), ptr(tidx), n, m, d, ptr(s), rows(s),
                                precision, stream()), "kge_score_dot")
     return s
+
+
+def split_rows(x):
+    """fp32 rows -> bf16 (hi, lo) planes, ld rounded up to a multiple of 32 (zero padded)."""
+    n, d = x.shape
+    ldo = (d + 31) // 32 * 32
+    hi = torch.empty(n, ldo, device=x.device, dtype=torch.bfloat16)
+    lo = torch.empty_like(hi)
+    _check(lib().kge_split_rows(ptr(x), rows(x), n, d, ptr(hi), ptr(lo), ldo, stream()), "kge_split_rows")
+    return hi, lo
+
+
+def score_dot_split(q_hi, q_lo, t, tidx, d, out=None):
+    """Production bf16x3 contraction on pre-split query planes."""
+    require_device(q_hi, t)
+    tidx = idx64(tidx)
+    check_index(tidx, t.shape[0], "candidate index")
+    n = q_hi.shape[0]
+    m = tidx.numel() if tidx is not None else t.shape[0]
+    s = out if out is not None else torch.empty(n, m, device=t.device, dtype=torch.float32)
+    _check(lib().kge_score_dot_split(ptr(q_hi), ptr(q_lo), q_hi.stride(0), ptr(t), rows(t), ptr(tidx), n, m, d,
+                                     ptr(s), rows(s), stream()), "kge_score_dot_split")
+    return s
+
+
+def contract(q, t, tidx, precision, out=None):
+    """S = Q . T[tidx]^T on the engine: bf16x3 via split planes when the layout allows
+    (d % 4 == 0, 16-B aligned rows), otherwise the generic kernel."""
+    d = q.shape[1]
+    if (precision == PREC_BF16X3 and d % 4 == 0 and rows(t) % 4 == 0 and t.data_ptr() % 16 == 0):
+        hi, lo = split_rows(q)
+        return score_dot_split(hi, lo, t, tidx, d, out=out)
+    return score_dot(q, t, tidx, precision, out=out)
 
 
 def score_dot_bwd_q(g, t, tidx, precision, dq=None, accumulate=False):

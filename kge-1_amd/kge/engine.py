@@ -67,7 +67,7 @@ class _ScoreAll(torch.autograd.Function):
             raise ValueError(f"candidate dim {tab.shape[1]} != entity dim {d_e}")
         q = L.prep_query(kind, direction, ent, eidx, rel, ridx, n, d_e, d_r)
         if kind in BILINEAR:
-            s = _timed(L.score_dot, q, tab, tidx, precision)
+            s = _timed(L.contract, q, tab, tidx, precision)
         else:
             dk, sign = dist_kind(kind, l_norm)
             s = _timed(L.score_dist, dk, sign, q, tab, tidx)

@@ -48,7 +48,7 @@ class EngineOps:
         from .engine import BILINEAR, dist_kind
 
         if self.kind in BILINEAR:
-            return self.L.score_dot(q, tab, None, self.precision)
+            return self.L.contract(q, tab, None, self.precision)
         dk, sign = dist_kind(self.kind, self.l_norm)
         return self.L.score_dist(dk, sign, q, tab, None)
 

@@ -204,3 +204,35 @@ def test_score_sp_c2_shape(L, prec):
     Sd = L.score_dot(qd, entd, None, L.PRECISIONS[prec])
     ref = qd.double() @ entd.double().T
     assert torch.equal(Sd.double(), ref)
+
+
+@pytest.mark.parametrize("n,m,d", [(1, 1, 4), (100, 300, 100), (129, 255, 64), (1024, 14541, 512),
+                                   (256, 1000, 36), (300, 2049, 128)])
+def test_score_dot_split_shapes(L, n, m, d):
+    """Production bf16x3 path (kge_split_rows + kge_score_dot_split): ragged tile edges,
+    K tails (d not a multiple of 32), subsets with duplicates; dyadic inputs bit-exact."""
+    g = torch.Generator().manual_seed(n * 7 + m + d)
+    E = m + 17
+    t = (torch.randn(E, d, generator=g) * 0.1).cuda()
+    q = (torch.randn(n, d, generator=g) * 0.1).cuda()
+    tidx = torch.randint(0, E, (m,), generator=g).cuda()
+    hi, lo = L.split_rows(q)
+    for ti in (None, tidx):
+        s = L.score_dot_split(hi, lo, t, ti, d)
+        tt = t if ti is None else t[ti]
+        ref = (q.double() @ tt.double().T).cpu().numpy()
+        assert rel_err(s.cpu().numpy(), ref) < 2e-5
+    qd = (torch.randint(-16, 17, (n, d), generator=g) / 8).float().cuda()
+    td = (torch.randint(-16, 17, (E, d), generator=g) / 8).float().cuda()
+    hi, lo = L.split_rows(qd)
+    s = L.score_dot_split(hi, lo, td, tidx, d)
+    assert torch.equal(s.double(), qd.double() @ td[tidx].double().T)
+
+
+def test_contract_dispatch_and_errors(L):
+    q = torch.randn(8, 6).cuda()
+    t = torch.randn(20, 6).cuda()
+    s = L.contract(q, t, None, L.PREC_BF16X3)  # d % 4 != 0 -> generic kernel
+    assert rel_err(s.cpu().numpy(), (q.double() @ t.double().T).cpu().numpy()) < 2e-5
+    with pytest.raises(ValueError):
+        L.score_dot(q, torch.randn(20, 5).cuda(), None, L.PREC_BF16X3)
