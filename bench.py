@@ -8,12 +8,12 @@ all-entities contraction against the 14,541-row entity table (libkgescore, gfx95
 value = scored triples / s = (queries x entities) / step time, all ranks.
 
 N > 1 (torchrun, one process per GPU, RCCL): the entity table is row-sharded
-(kge.sharded); each rank contributes 1024 queries per step, the global batch of N*1024
-queries is exchanged (index all_gather + owner-computed query rows all_reduce) and
-scored against every shard -> per-GPU work is constant (weak scaling).
+(kge.sharded); each rank contributes 1024 queries per step whose subjects it owns (a
+shard-affine loader), their query rows are all_gathered over RCCL, and the global batch of
+N*1024 queries is scored against every shard -> per-GPU work is constant (weak scaling).
 
-Also reported (rank 0): the contraction kernel's roofline from HIP events recorded
-around every launch in the timed region, score_po, a full 1vsAll training step
+Also reported (rank 0): the contraction kernel's roofline from HIP events on the launch stream
+(20 back-to-back launches after the timed region), score_po, a full 1vsAll training step
 (sp + po forward/backward + CE + Adagrad), the filtered eval MRR on the synthetic test
 split, and the reference CPU path (oracle/refseq.py: the reference's exact ATen op
 sequence, verified bit-exact against it) timed on this host's cores.
@@ -113,10 +113,13 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    ndev = max(1, torch.cuda.device_count())
+    dev_index = local_rank % ndev  # == local_rank on a node with one GPU per rank
     if world > 1:
-        torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl")
-    device = f"cuda:{local_rank}"
+        torch.cuda.set_device(dev_index)
+        # "nccl" is RCCL on ROCm; KGE_DIST_BACKEND=gloo only to rehearse >1 rank on one GPU
+        dist.init_process_group(os.environ.get("KGE_DIST_BACKEND", "nccl"))
+    device = f"cuda:{dev_index}"
 
     from kge import Dataset, KgeModel, _lib, engine
     from kge.dataset import SHAPES
@@ -133,7 +136,13 @@ def main():
     rel = model._relation_embedder._embeddings.weight
     steps, warmup = args.steps, args.warmup
     g = torch.Generator(device=device).manual_seed(1 + rank)
-    s_all = torch.randint(0, E, (steps + warmup, B), device=device, generator=g)
+    if world == 1:
+        s_all = torch.randint(0, E, (steps + warmup, B), device=device, generator=g)
+    else:  # shard-affine loader: rank k's queries have their subject in shard k
+        from kge.sharded import shard_bounds
+
+        lo_, hi_ = shard_bounds(E, world, rank)
+        s_all = torch.randint(lo_, hi_, (steps + warmup, B), device=device, generator=g)
     p_all = torch.randint(0, R, (steps + warmup, B), device=device, generator=g)
     prec = _lib.PRECISIONS[args.precision]
 
@@ -151,35 +160,27 @@ def main():
 
         def step(i):
             with torch.no_grad():
-                return sharded.score_sp(s_all[i], p_all[i])
+                return sharded.score_sp_local(s_all[i], p_all[i])
         scored_per_step = world * B * E
 
-    # timed region, with HIP events around every contraction launch
-    for i in range(warmup):
-        step(i)
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
+    # timed region: K steps bracketed by barrier + synchronize, nothing else inside
+    sec = timed_loop(step, steps, warmup, world)
+    # instrumented re-run of the same steps: HIP events around every contraction launch
     engine.KERNEL_EVENTS = []
-    if world > 1:
-        _lib_events = []
-    t0 = time.perf_counter()
-    for i in range(steps):
+    _lib_events = []
+    for i in range(min(steps, 20)):
         if world == 1:
             step(warmup + i)
         else:
             a = torch.cuda.Event(enable_timing=True)
             b = torch.cuda.Event(enable_timing=True)
             with torch.no_grad():
-                q, _, _ = sharded.queries(s_all[warmup + i], p_all[warmup + i], 0)
+                q = sharded.queries_local(s_all[warmup + i], p_all[warmup + i], 0)
                 a.record()
                 sharded.ops.score(q, sharded.ent)
                 b.record()
             _lib_events.append((a, b))
     torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    sec = (time.perf_counter() - t0) / steps
     events = engine.KERNEL_EVENTS if world == 1 else _lib_events
     engine.KERNEL_EVENTS = None
     launch_ms = float(np.mean([a.elapsed_time(b) for a, b in events])) if events else float("nan")
@@ -191,7 +192,7 @@ def main():
             q = _lib.prep_query(_lib.COMPLEX, _lib.DIR_SP, ent.detach(), s_all[0], rel.detach(), p_all[0], B, d, d)
             tab = ent.detach()
         else:
-            q, _, _ = sharded.queries(s_all[0], p_all[0], 0)
+            q = sharded.queries_local(s_all[0], p_all[0], 0)
             tab = sharded.ent
         out_buf = torch.empty(q.shape[0], tab.shape[0], device=device)
         if prec == _lib.PREC_BF16X3:  # the production path: pre-split Q planes + persistent kernel
@@ -245,7 +246,8 @@ def main():
            "data": "synthetic (FB15K-237 shape: 14,541 entities / 237 relations), N(0,0.1) random-init tables",
            "config": {"workload": "configs[1]: ComplEx dim=512 1vsAll FB15K-237, batch 1024, score_sp per step",
                       "model": "complex", "dim": d, "global_batch": B * world, "entities": E,
-                      "parallelism": "single GPU" if world == 1 else f"entity-row-sharded x{world} (RCCL)",
+                      "parallelism": "single GPU" if world == 1 else
+                      f"entity-row-sharded x{world}, shard-affine queries, Q all_gather ({os.environ.get('KGE_DIST_BACKEND', 'nccl')})",
                       "precision": args.precision},
            "roofline": roofline}
 

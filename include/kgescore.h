@@ -74,6 +74,15 @@ int kge_prep_query(int model, int dir, const float* ent, int64_t ld_ent,
                    const int64_t* ridx, int64_t n, int d_e, int d_r, float* q,
                    int64_t ldq, void* stream);
 
+/* kge_prep_query that can also (or only) emit the bf16 hi / lo planes of Q consumed by
+ * kge_score_dot_split: q may be NULL; planes are [n][ldp], ldp >= d_e and a multiple of 8
+ * (use round_up(d_e, 32)); columns d_e .. ldp-1 are zeroed.  Saves the separate
+ * kge_split_rows pass on the score_sp / score_po path. */
+int kge_prep_query_split(int model, int dir, const float* ent, int64_t ld_ent,
+                         const int64_t* eidx, const float* rel, int64_t ld_rel,
+                         const int64_t* ridx, int64_t n, int d_e, int d_r, float* q,
+                         int64_t ldq, void* q_hi, void* q_lo, int64_t ldp, void* stream);
+
 /* backward of kge_prep_query: scatter-adds dL/d(ent row) and dL/d(rel row) into
  * d_ent / d_rel (atomic fp32 adds; either may be NULL to skip). */
 int kge_prep_query_bwd(int model, int dir, const float* ent, int64_t ld_ent,

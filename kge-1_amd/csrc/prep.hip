@@ -20,16 +20,41 @@ __device__ __forceinline__ Rows fetch_rows(const float* ent, int64_t ld_ent, con
   return Rows{ent + ei * ld_ent, rel + ri * ld_rel};
 }
 
+// Query-row sink: fp32 rows and/or bf16 hi / lo planes (the bf16x3 contraction's input),
+// planes zero-padded from d_e to ldp.
+struct QOut {
+  float* q;
+  int64_t ldq;
+  __bf16* hi;
+  __bf16* lo;
+  int64_t ldp;
+  __device__ __forceinline__ void put(int64_t i, int k, float v) const {
+    if (q) q[i * ldq + k] = v;
+    if (hi) {
+      __bf16 h, l;
+      split_bf16(v, h, l);
+      hi[i * ldp + k] = h;
+      lo[i * ldp + k] = l;
+    }
+  }
+  __device__ __forceinline__ void pad(int64_t i, int d) const {
+    if (!hi) return;
+    for (int k = d + threadIdx.x; k < ldp; k += blockDim.x) {
+      hi[i * ldp + k] = (__bf16)0.f;
+      lo[i * ldp + k] = (__bf16)0.f;
+    }
+  }
+};
+
 // Elementwise models: complex / distmult / transe / rotate.  One block per query row.
 template <int MODEL, int DIR>
 __global__ void __launch_bounds__(256) prep_elementwise(const float* __restrict__ ent, int64_t ld_ent,
                                                          const int64_t* __restrict__ eidx,
                                                          const float* __restrict__ rel, int64_t ld_rel,
-                                                         const int64_t* __restrict__ ridx, int d_e,
-                                                         float* __restrict__ q, int64_t ldq) {
+                                                         const int64_t* __restrict__ ridx, int d_e, QOut out) {
   const int64_t i = blockIdx.x;
   Rows rw = fetch_rows(ent, ld_ent, eidx, rel, ld_rel, ridx, i);
-  float* qi = q + i * ldq;
+  out.pad(i, d_e);
   if (MODEL == KGE_COMPLEX || MODEL == KGE_ROTATE) {
     const int h = d_e / 2;
     for (int k = threadIdx.x; k < h; k += blockDim.x) {
@@ -42,20 +67,20 @@ __global__ void __launch_bounds__(256) prep_elementwise(const float* __restrict_
         sincosf(rw.r[k], &s, &c);  // rotate.py:273 (radians -> unit complex)
       }
       if (DIR == KGE_DIR_SP) {  // a * (c + i s)
-        qi[k] = a_re * c - a_im * s;
-        qi[k + h] = a_re * s + a_im * c;
+        out.put(i, k, a_re * c - a_im * s);
+        out.put(i, k + h, a_re * s + a_im * c);
       } else {  // conj(c + i s) * a
-        qi[k] = c * a_re + s * a_im;
-        qi[k + h] = c * a_im - s * a_re;
+        out.put(i, k, c * a_re + s * a_im);
+        out.put(i, k + h, c * a_im - s * a_re);
       }
     }
   } else {
     for (int k = threadIdx.x; k < d_e; k += blockDim.x) {
       const float a = rw.e[k], b = rw.r[k];
       if (MODEL == KGE_DISTMULT)
-        qi[k] = a * b;
+        out.put(i, k, a * b);
       else  // TRANSE
-        qi[k] = (DIR == KGE_DIR_SP) ? a + b : a - b;
+        out.put(i, k, (DIR == KGE_DIR_SP) ? a + b : a - b);
     }
   }
 }
@@ -65,19 +90,18 @@ template <int DIR>
 __global__ void __launch_bounds__(256) prep_rescal(const float* __restrict__ ent, int64_t ld_ent,
                                                     const int64_t* __restrict__ eidx,
                                                     const float* __restrict__ rel, int64_t ld_rel,
-                                                    const int64_t* __restrict__ ridx, int d,
-                                                    float* __restrict__ q, int64_t ldq) {
+                                                    const int64_t* __restrict__ ridx, int d, QOut out) {
   extern __shared__ float xs[];
   const int64_t i = blockIdx.x;
   Rows rw = fetch_rows(ent, ld_ent, eidx, rel, ld_rel, ridx, i);
   for (int k = threadIdx.x; k < d; k += blockDim.x) xs[k] = rw.e[k];
+  out.pad(i, d);
   __syncthreads();
-  float* qi = q + i * ldq;
   if (DIR == KGE_DIR_SP) {  // q_j = sum_a x_a M[a][j]  (coalesced over j)
     for (int j = threadIdx.x; j < d; j += blockDim.x) {
       float acc = 0.f;
       for (int a = 0; a < d; ++a) acc = fmaf(xs[a], rw.r[(int64_t)a * d + j], acc);
-      qi[j] = acc;
+      out.put(i, j, acc);
     }
   } else {  // q_a = sum_j M[a][j] x_j : one wave per output row
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
@@ -85,7 +109,7 @@ __global__ void __launch_bounds__(256) prep_rescal(const float* __restrict__ ent
       float acc = 0.f;
       for (int j = lane; j < d; j += 64) acc = fmaf(rw.r[(int64_t)a * d + j], xs[j], acc);
       acc = wave_sum(acc);
-      if (lane == 0) qi[a] = acc;
+      if (lane == 0) out.put(i, a, acc);
     }
   }
 }
@@ -202,24 +226,23 @@ __global__ void __launch_bounds__(256) prep_rescal_bwd(
 
 template <int DIR>
 int launch_prep(int model, const float* ent, int64_t ld_ent, const int64_t* eidx, const float* rel,
-                int64_t ld_rel, const int64_t* ridx, int64_t n, int d_e, float* q, int64_t ldq,
-                hipStream_t st) {
+                int64_t ld_rel, const int64_t* ridx, int64_t n, int d_e, QOut q, hipStream_t st) {
   dim3 grid((unsigned)n), block(256);
   switch (model) {
     case KGE_COMPLEX:
-      prep_elementwise<KGE_COMPLEX, DIR><<<grid, block, 0, st>>>(ent, ld_ent, eidx, rel, ld_rel, ridx, d_e, q, ldq);
+      prep_elementwise<KGE_COMPLEX, DIR><<<grid, block, 0, st>>>(ent, ld_ent, eidx, rel, ld_rel, ridx, d_e, q);
       break;
     case KGE_DISTMULT:
-      prep_elementwise<KGE_DISTMULT, DIR><<<grid, block, 0, st>>>(ent, ld_ent, eidx, rel, ld_rel, ridx, d_e, q, ldq);
+      prep_elementwise<KGE_DISTMULT, DIR><<<grid, block, 0, st>>>(ent, ld_ent, eidx, rel, ld_rel, ridx, d_e, q);
       break;
     case KGE_TRANSE:
-      prep_elementwise<KGE_TRANSE, DIR><<<grid, block, 0, st>>>(ent, ld_ent, eidx, rel, ld_rel, ridx, d_e, q, ldq);
+      prep_elementwise<KGE_TRANSE, DIR><<<grid, block, 0, st>>>(ent, ld_ent, eidx, rel, ld_rel, ridx, d_e, q);
       break;
     case KGE_ROTATE:
-      prep_elementwise<KGE_ROTATE, DIR><<<grid, block, 0, st>>>(ent, ld_ent, eidx, rel, ld_rel, ridx, d_e, q, ldq);
+      prep_elementwise<KGE_ROTATE, DIR><<<grid, block, 0, st>>>(ent, ld_ent, eidx, rel, ld_rel, ridx, d_e, q);
       break;
     case KGE_RESCAL:
-      prep_rescal<DIR><<<grid, block, d_e * sizeof(float), st>>>(ent, ld_ent, eidx, rel, ld_rel, ridx, d_e, q, ldq);
+      prep_rescal<DIR><<<grid, block, d_e * sizeof(float), st>>>(ent, ld_ent, eidx, rel, ld_rel, ridx, d_e, q);
       break;
     default:
       return KGE_ERR_ARG;
@@ -271,12 +294,23 @@ int check_dims(int model, int d_e, int d_r) {
 extern "C" int kge_prep_query(int model, int dir, const float* ent, int64_t ld_ent, const int64_t* eidx,
                               const float* rel, int64_t ld_rel, const int64_t* ridx, int64_t n, int d_e,
                               int d_r, float* q, int64_t ldq, void* stream) {
+  return kge_prep_query_split(model, dir, ent, ld_ent, eidx, rel, ld_rel, ridx, n, d_e, d_r, q, ldq, nullptr,
+                              nullptr, 0, stream);
+}
+
+extern "C" int kge_prep_query_split(int model, int dir, const float* ent, int64_t ld_ent, const int64_t* eidx,
+                                    const float* rel, int64_t ld_rel, const int64_t* ridx, int64_t n, int d_e,
+                                    int d_r, float* q, int64_t ldq, void* q_hi, void* q_lo, int64_t ldp,
+                                    void* stream) {
   if (int e = check_dims(model, d_e, d_r)) return e;
-  KGE_REQUIRE(n >= 0 && ent && rel && q && ldq >= d_e);
+  KGE_REQUIRE(n >= 0 && ent && rel && (q || q_hi));
+  KGE_REQUIRE(!q || ldq >= d_e);
+  KGE_REQUIRE(!q_hi || (q_lo && ldp >= d_e && ldp % 8 == 0));
   if (n == 0) return 0;
+  QOut out{q, ldq, (__bf16*)q_hi, (__bf16*)q_lo, ldp};
   hipStream_t st = as_stream(stream);
-  if (dir == KGE_DIR_SP) return launch_prep<KGE_DIR_SP>(model, ent, ld_ent, eidx, rel, ld_rel, ridx, n, d_e, q, ldq, st);
-  if (dir == KGE_DIR_PO) return launch_prep<KGE_DIR_PO>(model, ent, ld_ent, eidx, rel, ld_rel, ridx, n, d_e, q, ldq, st);
+  if (dir == KGE_DIR_SP) return launch_prep<KGE_DIR_SP>(model, ent, ld_ent, eidx, rel, ld_rel, ridx, n, d_e, out, st);
+  if (dir == KGE_DIR_PO) return launch_prep<KGE_DIR_PO>(model, ent, ld_ent, eidx, rel, ld_rel, ridx, n, d_e, out, st);
   return KGE_ERR_ARG;
 }
 

@@ -32,6 +32,7 @@ SIGNATURES = {
     "kge_version": ([], _I),
     "kge_error_string": ([_I], ctypes.c_char_p),
     "kge_prep_query": ([_I, _I, _P, _I64, _P, _P, _I64, _P, _I64, _I, _I, _P, _I64, _P], _I),
+    "kge_prep_query_split": ([_I, _I, _P, _I64, _P, _P, _I64, _P, _I64, _I, _I, _P, _I64, _P, _P, _I64, _P], _I),
     "kge_prep_query_bwd": ([_I, _I, _P, _I64, _P, _P, _I64, _P, _I64, _I, _I, _P, _I64, _P, _I64,
                             _P, _I64, _P], _I),
     "kge_score_dot": ([_P, _I64, _P, _I64, _P, _I64, _I64, _I, _P, _I64, _I, _P], _I),
@@ -144,6 +145,27 @@ def prep_query(model, direction, ent, eidx, rel, ridx, n, d_e, d_r, out=None):
     return q
 
 
+def prep_query_split(model, direction, ent, eidx, rel, ridx, n, d_e, d_r, want_fp32=True):
+    """Query rows as fp32 (optional) plus bf16 hi / lo planes [n, round32(d_e)] in one pass."""
+    require_device(ent, rel)
+    eidx, ridx = idx64(eidx), idx64(ridx)
+    check_index(eidx, ent.shape[0], "entity index")
+    check_index(ridx, rel.shape[0], "relation index")
+    ldp = (d_e + 31) // 32 * 32
+    q = torch.empty(n, d_e, device=ent.device, dtype=torch.float32) if want_fp32 else None
+    hi = torch.empty(n, ldp, device=ent.device, dtype=torch.bfloat16)
+    lo = torch.empty_like(hi)
+    _check(lib().kge_prep_query_split(model, direction, ptr(ent), rows(ent), ptr(eidx), ptr(rel), rows(rel),
+                                      ptr(ridx), n, d_e, d_r, ptr(q), rows(q) if q is not None else 0, ptr(hi),
+                                      ptr(lo), ldp, stream()), "kge_prep_query_split")
+    return q, hi, lo
+
+
+def split_ok(d, t, precision):
+    """Whether the production split-plane bf16x3 contraction applies to table t."""
+    return precision == PREC_BF16X3 and d % 4 == 0 and rows(t) % 4 == 0 and t.data_ptr() % 16 == 0
+
+
 def prep_query_bwd(model, direction, ent, eidx, rel, ridx, n, d_e, d_r, dq, d_ent, d_rel):
     eidx, ridx = idx64(eidx), idx64(ridx)
     _check(lib().kge_prep_query_bwd(
@@ -191,7 +213,7 @@ def contract(q, t, tidx, precision, out=None):
     """S = Q . T[tidx]^T on the engine: bf16x3 via split planes when the layout allows
     (d % 4 == 0, 16-B aligned rows), otherwise the generic kernel."""
     d = q.shape[1]
-    if (precision == PREC_BF16X3 and d % 4 == 0 and rows(t) % 4 == 0 and t.data_ptr() % 16 == 0):
+    if split_ok(d, t, precision):
         hi, lo = split_rows(q)
         return score_dot_split(hi, lo, t, tidx, d, out=out)
     return score_dot(q, t, tidx, precision, out=out)

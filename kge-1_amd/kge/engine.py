@@ -65,10 +65,19 @@ class _ScoreAll(torch.autograd.Function):
         d_e, d_r = ent.shape[1], rel.shape[1]
         if tab.shape[1] != d_e:
             raise ValueError(f"candidate dim {tab.shape[1]} != entity dim {d_e}")
-        q = L.prep_query(kind, direction, ent, eidx, rel, ridx, n, d_e, d_r)
-        if kind in BILINEAR:
+        if kind in BILINEAR and L.split_ok(d_e, tab, precision):
+            # one pass emits Q (kept for backward only when a gradient is needed) and its
+            # bf16 hi / lo planes for the split contraction
+            need_q = any(ctx.needs_input_grad[i] for i in (4, 6, 8))
+            q, q_hi, q_lo = L.prep_query_split(kind, direction, ent, eidx, rel, ridx, n, d_e, d_r, need_q)
+            s = _timed(L.score_dot_split, q_hi, q_lo, tab, tidx, d_e)
+            if q is None:
+                q = q_hi.new_empty(0)
+        elif kind in BILINEAR:
+            q = L.prep_query(kind, direction, ent, eidx, rel, ridx, n, d_e, d_r)
             s = _timed(L.contract, q, tab, tidx, precision)
         else:
+            q = L.prep_query(kind, direction, ent, eidx, rel, ridx, n, d_e, d_r)
             dk, sign = dist_kind(kind, l_norm)
             s = _timed(L.score_dist, dk, sign, q, tab, tidx)
         ctx.meta = (kind, direction, precision, l_norm, n, d_e, d_r, ent is tab)

@@ -129,3 +129,54 @@ def test_row_sharded_world2():
         ref[di, 0], ref[di, 1] = gr.numpy(), ti.numpy()
     for r in res:
         np.testing.assert_array_equal(r[6][:, :, :2 * B], ref[:, :, :2 * B])
+
+
+def _worker_local(rank, world, port, out_q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from kge.sharded import RowShardedScorer, shard_bounds
+
+        g = torch.Generator().manual_seed(0)
+        E, R, d, B = 41, 4, 8, 5
+        ent = torch.randn(E, d, generator=g)
+        rel = torch.randn(R, d, generator=g)
+        lo, hi = shard_bounds(E, world, rank)
+        sc = RowShardedScorer(ent[lo:hi].clone(), lo, hi, E, rel, OracleOps())
+        gq = torch.Generator().manual_seed(200 + rank)
+        s = torch.randint(lo, hi, (B,), generator=gq)
+        p = torch.randint(0, R, (B,), generator=gq)
+        out_q.put((rank, lo, hi, sc.score_sp_local(s, p).numpy(), s.numpy(), p.numpy()))
+        try:
+            sc.score_sp_local(torch.tensor([hi % E] * B), p)  # not owned -> error on one rank at least
+            bad = False
+        except ValueError:
+            bad = True
+        out_q.put((rank, "err", bad))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_row_sharded_local_queries_world2():
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_local, args=(r, world, port, q)) for r in range(world)]
+    for pr in procs:
+        pr.start()
+    items = [q.get(timeout=120) for _ in range(2 * world)]
+    for pr in procs:
+        pr.join(timeout=60)
+    res = sorted([x for x in items if x[1] != "err"], key=lambda x: x[0])
+    errs = [x[2] for x in items if x[1] == "err"]
+    g = torch.Generator().manual_seed(0)
+    E, R, d, B = 41, 4, 8, 5
+    ent = torch.randn(E, d, generator=g).double().numpy()
+    rel = torch.randn(R, d, generator=g).double().numpy()
+    s_all = np.concatenate([r[4] for r in res])
+    p_all = np.concatenate([r[5] for r in res])
+    full = K.prep_sp("complex", ent[s_all], rel[p_all]) @ ent.T
+    for rank, lo, hi, local, _, _ in res:
+        np.testing.assert_allclose(local, full[:, lo:hi], rtol=1e-5, atol=1e-5)
+    assert all(errs)
