@@ -156,6 +156,17 @@ int kge_score_spo_bwd(int model, float l_norm, const float* ent, int64_t ld_ent,
                       int d_r, const float* g, float* d_ent, int64_t ld_dent,
                       float* d_rel, int64_t ld_drel, void* stream);
 
+/* ---- 1vsAll loss fused with its gradient ---------------------------------------------
+ * loss[i] = logsumexp_j S[i, j] - S[i, labels[i]]                      (NaN if label out of range)
+ * g[i, j] = scale * (softmax_j(S[i, :]) - [j == labels[i]])            (g may be NULL, or == s
+ *                                                                      with ldg == lds: in place)
+ * i in [0, n), j in [0, m).  scale = 1 / batch_size gives the gradient of
+ * sum_i loss[i] / batch_size, the reference's 1vsAll objective:
+ * KLDivWithSoftmaxKgeLoss with index labels (kge/util/loss.py:192-208) / batch size
+ * (kge/job/train.py:1042, 1052).  Replaces log_softmax + nll_loss forward and backward. */
+int kge_softmax_xent(const float* s, int64_t lds, int64_t n, int64_t m, const int64_t* labels,
+                     float scale, float* loss, float* g, int64_t ldg, void* stream);
+
 /* ---- entity-ranking counts (eval) --------------------------------------------------
  * For row i of a score chunk S[n, m] covering entities [c0, c0 + m):
  *   v_j = S[i, j], with v_{true_i - c0} := true_score[i] when true_i is in the chunk;

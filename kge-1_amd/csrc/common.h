@@ -48,6 +48,24 @@ __device__ __forceinline__ void split_bf16x4(const float4& v, bf16x4& hi, bf16x4
   }
 }
 
+// Compute units of the current device (256 on MI355X); cached per translation unit.
+static inline int kge_num_cus() {
+  static int cus = 0;
+  if (!cus) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+      cus = 256;
+  }
+  return cus;
+}
+
+// bf16x3 backward GEMMs (gemm_bwd3.hip), dispatched from kge_score_dot_bwd_q / _t.
+int kge_bwd3_q(const float* g, int64_t ldg, const float* t, int64_t ldt, const int64_t* tidx, int64_t n,
+               int64_t m, int d, float* dq, int64_t lddq, int cus, hipStream_t st);
+int kge_bwd3_t(const float* g, int64_t ldg, const float* q, int64_t ldq, const int64_t* tidx, int64_t n,
+               int64_t m, int d, float* dt, int64_t lddt, hipStream_t st);
+
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);

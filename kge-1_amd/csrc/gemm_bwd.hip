@@ -2,7 +2,8 @@
 // SURVEY.md §8a A12):
 //   dQ = G . T        [n, d]  (K = m: long reduction, split over workgroups)
 //   dT += G^T . Q     [m, d]  (K = n), rows scattered through tidx when given
-// Both run on the exact fp32-input MFMA (v_mfma_f32_32x32x2_f32).  Operands are staged
+// KGE_PREC_FP32 runs here on the exact fp32-input MFMA (v_mfma_f32_32x32x2_f32);
+// KGE_PREC_BF16X3 dispatches to gemm_bwd3.hip.  Operands are staged
 // into LDS K-major ([k][row]) so every fragment read is a 32-lane contiguous
 // ds_read_b32 and whichever global layout an operand has is read coalesced.
 #include "common.h"
@@ -131,6 +132,7 @@ extern "C" int kge_score_dot_bwd_q(const float* g, int64_t ldg, const float* t, 
     if (e != hipSuccess) return (int)e;
   }
   if (n == 0 || m == 0) return 0;
+  if (precision == KGE_PREC_BF16X3) return kge_bwd3_q(g, ldg, t, ldt, tidx, n, m, d, dq, lddq, kge_num_cus(), st);
   const int gm = (int)((n + BM - 1) / BM), gn = (d + BN - 1) / BN;
   // split the long K = m reduction so that the grid fills the chip (>= ~1024 blocks)
   int splits = (int)std::max<int64_t>(1, std::min<int64_t>((m + 255) / 256, 1024 / std::max(1, gm * gn)));
@@ -151,6 +153,7 @@ extern "C" int kge_score_dot_bwd_t(const float* g, int64_t ldg, const float* q, 
   KGE_REQUIRE(precision == KGE_PREC_FP32 || precision == KGE_PREC_BF16X3);
   if (n == 0 || m == 0) return 0;
   hipStream_t st = as_stream(stream);
+  if (precision == KGE_PREC_BF16X3) return kge_bwd3_t(g, ldg, q, ldq, tidx, n, m, d, dt, lddt, st);
   const int gm = (int)((m + BM - 1) / BM), gn = (d + BN - 1) / BN;
   // C[j][k] = sum_i G[i][j] Q[i][k]: A = G^T (M contiguous), B = Q
   if (tidx)

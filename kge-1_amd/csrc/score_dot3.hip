@@ -188,16 +188,6 @@ __global__ void __launch_bounds__(64 * WM * WN, 1)
   }
 }
 
-int num_cus() {
-  static int cus = 0;
-  if (!cus) {
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
-      cus = 256;
-  }
-  return cus;
-}
-
 template <int BM, int BN, int WM, int WN>
 int launch_persist(const __bf16* qhi, const __bf16* qlo, int64_t ldq, const float* t, int64_t ldt,
                    const int64_t* tidx, int64_t n, int64_t m, int d, float* s, int64_t lds, int per_cu,
@@ -214,7 +204,7 @@ int launch_persist(const __bf16* qhi, const __bf16* qlo, int64_t ldq, const floa
     if (e != hipSuccess) return (int)e;
     attr_set = true;
   }
-  int grid = num_cus() * per_cu;
+  int grid = kge_num_cus() * per_cu;
   grid = (int)std::min<int64_t>(grid, (ntiles + 7) / 8 * 8);
   grid = std::max(8, grid / 8 * 8);
   score_dot_persist_kernel<BM, BN, WM, WN><<<dim3(grid), dim3(C::NT), shmem, st>>>(

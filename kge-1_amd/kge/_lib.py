@@ -48,6 +48,7 @@ SIGNATURES = {
                            _I64, _P], _I),
     "kge_rank_counts": ([_P, _I64, _I64, _I64, _I64, _P, _P, _P, _P, _P, _P, _P, _P, _P], _I),
     "kge_rank_hist": ([_P, _P, _I64, _I, _P, _P, _I64, _P], _I),
+    "kge_softmax_xent": ([_P, _I64, _I64, _I64, _P, _F, _P, _P, _I64, _P], _I),
 }
 
 _lib: Optional[ctypes.CDLL] = None
@@ -299,3 +300,18 @@ def rank_hist(greater, ties, tie_handling, ranks, hist):
     n = greater.numel()
     _check(lib().kge_rank_hist(ptr(greater), ptr(ties), n, TIE[tie_handling], ptr(ranks), ptr(hist),
                                hist.numel() if hist is not None else 0, stream()), "kge_rank_hist")
+
+
+def softmax_xent(s, labels, scale, g=None, loss=None):
+    """Per-row softmax cross entropy of score rows S[:, :m] (a possibly padded view) against
+    index labels; optionally G = scale * (softmax - onehot) into g (g may be s: in place).
+    Returns loss [n] (unscaled per-row losses)."""
+    require_device(s)
+    labels = idx64(labels)
+    n, m = s.shape
+    check_index(labels, m, "label")
+    if loss is None:
+        loss = torch.empty(n, device=s.device, dtype=torch.float32)
+    _check(lib().kge_softmax_xent(ptr(s), rows(s), n, m, ptr(labels), float(scale), ptr(loss), ptr(g),
+                                  rows(g) if g is not None else 0, stream()), "kge_softmax_xent")
+    return loss

@@ -57,55 +57,106 @@ def _rows(x: torch.Tensor) -> torch.Tensor:
     return x
 
 
+def _scores_forward(ctx, kind, direction, precision, l_norm, ent, eidx, rel, ridx, tab, tidx, out=None):
+    """Query preparation + all-candidates scores (into ``out`` when given).  Returns
+    (S, Q) with Q kept for the backward pass (empty when no gradient is needed)."""
+    n = eidx.numel() if eidx is not None else ent.shape[0]
+    d_e, d_r = ent.shape[1], rel.shape[1]
+    if tab.shape[1] != d_e:
+        raise ValueError(f"candidate dim {tab.shape[1]} != entity dim {d_e}")
+    if kind in BILINEAR and L.split_ok(d_e, tab, precision):
+        # one pass emits Q (kept for backward only when a gradient is needed) and its
+        # bf16 hi / lo planes for the split contraction
+        need_q = any(ctx.needs_input_grad[i] for i in (4, 6, 8))
+        q, q_hi, q_lo = L.prep_query_split(kind, direction, ent, eidx, rel, ridx, n, d_e, d_r, need_q)
+        s = _timed(L.score_dot_split, q_hi, q_lo, tab, tidx, d_e, out=out)
+        if q is None:
+            q = q_hi.new_empty(0)
+    elif kind in BILINEAR:
+        q = L.prep_query(kind, direction, ent, eidx, rel, ridx, n, d_e, d_r)
+        s = _timed(L.contract, q, tab, tidx, precision, out=out)
+    else:
+        q = L.prep_query(kind, direction, ent, eidx, rel, ridx, n, d_e, d_r)
+        dk, sign = dist_kind(kind, l_norm)
+        s = _timed(L.score_dist, dk, sign, q, tab, tidx, out=out)
+    ctx.meta = (kind, direction, precision, l_norm, n, d_e, d_r, ent is tab)
+    return s, q
+
+
+def _scores_backward(ctx, g, ent, eidx, rel, ridx, tab, tidx, q, gscale=None):
+    """Gradients of the scores w.r.t. (ent, rel, tab) for dL/dS = gscale * g (gscale: an
+    optional 0-dim device tensor, folded into the small operands instead of g)."""
+    kind, direction, precision, l_norm, n, d_e, d_r, same = ctx.meta
+    need_ent, need_rel, need_tab = ctx.needs_input_grad[4], ctx.needs_input_grad[6], ctx.needs_input_grad[8]
+    d_tab = torch.zeros_like(tab) if (need_tab or (same and need_ent)) else None
+    d_ent = d_tab if same else (torch.zeros_like(ent) if need_ent else None)
+    d_rel = torch.zeros_like(rel) if need_rel else None
+    dq = torch.zeros_like(q) if (need_ent or need_rel) else None
+    if kind in BILINEAR:
+        if dq is not None:
+            L.score_dot_bwd_q(g, tab, tidx, precision, dq=dq, accumulate=False)
+            if gscale is not None:
+                dq.mul_(gscale)
+        if d_tab is not None:
+            L.score_dot_bwd_t(g, q if gscale is None else q * gscale, tidx, d_tab, precision)
+    else:
+        dk, sign = dist_kind(kind, l_norm)
+        L.score_dist_bwd(dk, sign, g if gscale is None else g * gscale, q, tab, tidx, dq, d_tab)
+    if dq is not None:
+        L.prep_query_bwd(kind, direction, ent, eidx, rel, ridx, n, d_e, d_r, dq, d_ent, d_rel)
+    return None if same else d_ent, d_rel, d_tab
+
+
 class _ScoreAll(torch.autograd.Function):
     @staticmethod
     def forward(ctx, kind, direction, precision, l_norm, ent, eidx, rel, ridx, tab, tidx):
         ent, rel, tab = _rows(ent), _rows(rel), _rows(tab)
-        n = eidx.numel() if eidx is not None else ent.shape[0]
-        d_e, d_r = ent.shape[1], rel.shape[1]
-        if tab.shape[1] != d_e:
-            raise ValueError(f"candidate dim {tab.shape[1]} != entity dim {d_e}")
-        if kind in BILINEAR and L.split_ok(d_e, tab, precision):
-            # one pass emits Q (kept for backward only when a gradient is needed) and its
-            # bf16 hi / lo planes for the split contraction
-            need_q = any(ctx.needs_input_grad[i] for i in (4, 6, 8))
-            q, q_hi, q_lo = L.prep_query_split(kind, direction, ent, eidx, rel, ridx, n, d_e, d_r, need_q)
-            s = _timed(L.score_dot_split, q_hi, q_lo, tab, tidx, d_e)
-            if q is None:
-                q = q_hi.new_empty(0)
-        elif kind in BILINEAR:
-            q = L.prep_query(kind, direction, ent, eidx, rel, ridx, n, d_e, d_r)
-            s = _timed(L.contract, q, tab, tidx, precision)
-        else:
-            q = L.prep_query(kind, direction, ent, eidx, rel, ridx, n, d_e, d_r)
-            dk, sign = dist_kind(kind, l_norm)
-            s = _timed(L.score_dist, dk, sign, q, tab, tidx)
-        ctx.meta = (kind, direction, precision, l_norm, n, d_e, d_r, ent is tab)
+        s, q = _scores_forward(ctx, kind, direction, precision, l_norm, ent, eidx, rel, ridx, tab, tidx)
         ctx.save_for_backward(ent, eidx, rel, ridx, tab, tidx, q)
         return s
 
     @staticmethod
     def backward(ctx, g):
-        kind, direction, precision, l_norm, n, d_e, d_r, same = ctx.meta
         ent, eidx, rel, ridx, tab, tidx, q = ctx.saved_tensors
-        g = _rows(g)
-        need_ent, need_rel, need_tab = ctx.needs_input_grad[4], ctx.needs_input_grad[6], ctx.needs_input_grad[8]
-        d_tab = torch.zeros_like(tab) if (need_tab or (same and need_ent)) else None
-        d_ent = d_tab if same else (torch.zeros_like(ent) if need_ent else None)
-        d_rel = torch.zeros_like(rel) if need_rel else None
-        dq = torch.zeros_like(q) if (need_ent or need_rel) else None
-        if kind in BILINEAR:
-            if dq is not None:
-                L.score_dot_bwd_q(g, tab, tidx, precision, dq=dq, accumulate=False)
-            if d_tab is not None:
-                L.score_dot_bwd_t(g, q, tidx, d_tab, precision)
-        else:
-            dk, sign = dist_kind(kind, l_norm)
-            L.score_dist_bwd(dk, sign, g, q, tab, tidx, dq, d_tab)
-        if dq is not None:
-            L.prep_query_bwd(kind, direction, ent, eidx, rel, ridx, n, d_e, d_r, dq, d_ent, d_rel)
-        return (None, None, None, None, None if same else d_ent, None, d_rel, None,
-                d_tab, None)
+        d_ent, d_rel, d_tab = _scores_backward(ctx, _rows(g), ent, eidx, rel, ridx, tab, tidx, q)
+        return None, None, None, None, d_ent, None, d_rel, None, d_tab, None
+
+
+class _ScoreXent(torch.autograd.Function):
+    """scale * sum_i CE(S[i, :], labels[i]) with the all-candidates scores S never leaving
+    the engine: S is written into a buffer whose rows are padded to 16 B, the loss kernel
+    turns it in place into G = scale * (softmax(S) - onehot), and backward feeds G to the
+    contraction's backward GEMMs (whose loads vectorise on the padded rows)."""
+
+    @staticmethod
+    def forward(ctx, kind, direction, precision, l_norm, ent, eidx, rel, ridx, tab, tidx, labels, scale):
+        ent, rel, tab = _rows(ent), _rows(rel), _rows(tab)
+        n = eidx.numel() if eidx is not None else ent.shape[0]
+        m = tidx.numel() if tidx is not None else tab.shape[0]
+        buf = torch.empty(n, (m + 3) // 4 * 4, device=tab.device, dtype=torch.float32)
+        s, q = _scores_forward(ctx, kind, direction, precision, l_norm, ent, eidx, rel, ridx, tab, tidx,
+                               out=buf[:, :m])
+        loss_rows = L.softmax_xent(s, labels, scale, g=s)
+        ctx.save_for_backward(ent, eidx, rel, ridx, tab, tidx, q, s)
+        return loss_rows.sum() * scale
+
+    @staticmethod
+    def backward(ctx, gl):
+        ent, eidx, rel, ridx, tab, tidx, q, g = ctx.saved_tensors
+        d_ent, d_rel, d_tab = _scores_backward(ctx, g, ent, eidx, rel, ridx, tab, tidx, q, gscale=gl)
+        return None, None, None, None, d_ent, None, d_rel, None, d_tab, None, None, None
+
+
+def score_all_xent(kind: int, direction: int, precision: int, l_norm: float, ent: torch.Tensor,
+                   eidx: Optional[torch.Tensor], rel: torch.Tensor, ridx: Optional[torch.Tensor],
+                   tab: torch.Tensor, tidx: Optional[torch.Tensor], labels: torch.Tensor,
+                   scale: float) -> torch.Tensor:
+    """scale * sum_i CrossEntropy(score_all(...)[i, :], labels[i]) -- the 1vsAll objective
+    (kge/util/loss.py:192-208 with index labels; kge/job/train.py:1042,1052) fused with its
+    gradient; returns a 0-dim tensor that backpropagates into ent / rel / tab."""
+    L.require_device(ent, rel, tab)
+    return _ScoreXent.apply(kind, direction, precision, float(l_norm), ent, L.idx64(eidx), rel, L.idx64(ridx),
+                            tab, L.idx64(tidx), L.idx64(labels), float(scale))
 
 
 def score_all(kind: int, direction: int, precision: int, l_norm: float, ent: torch.Tensor,

@@ -17,7 +17,7 @@ import numpy as np
 import torch
 
 from ..model.kge_model import KgeModel
-from ..util.loss import KgeLoss
+from ..util.loss import KgeLoss, KLDivWithSoftmaxKgeLoss
 from ..util.optimizer import KgeLRScheduler, KgeOptimizer
 from .job import Job
 
@@ -145,22 +145,30 @@ class TrainingJob1vsAll(TrainingJob):
         return {"triples": self.dataset.split(self.train_split)[example_ids, :].long()}
 
     def _process_batch(self, batch_index, batch) -> TrainingJob._ProcessBatchResult:
-        """train.py:1032-1062: sp then po, each loss / B followed by backward."""
+        """train.py:1032-1062: sp then po, each loss / B followed by backward.  With
+        engine.fused_loss and the kl loss, scoring + cross entropy + its gradient run as one
+        engine op per direction (KgeModel.score_sp_xent / score_po_xent)."""
         t = -time.time()
         triples = batch["triples"].to(self.device, non_blocking=True)
         bs = len(triples)
         t += time.time()
+        fused = self.config.get("engine.fused_loss") and isinstance(self.loss, KLDivWithSoftmaxKgeLoss)
         fwd = -time.time()
-        scores_sp = self.model.score_sp(triples[:, S], triples[:, P])
-        loss_sp = self.loss(scores_sp, triples[:, O]) / bs
+        loss_sp = self.model.score_sp_xent(triples[:, S], triples[:, P], triples[:, O], 1.0 / bs) if fused else None
+        if loss_sp is None:
+            scores_sp = self.model.score_sp(triples[:, S], triples[:, P])
+            loss_sp = self.loss(scores_sp, triples[:, O]) / bs
+            del scores_sp
         fwd += time.time()
         bwd = -time.time()
         loss_sp.backward()
         bwd += time.time()
-        del scores_sp
         fwd -= time.time()
-        scores_po = self.model.score_po(triples[:, P], triples[:, O])
-        loss_po = self.loss(scores_po, triples[:, S]) / bs
+        loss_po = self.model.score_po_xent(triples[:, P], triples[:, O], triples[:, S], 1.0 / bs) if fused else None
+        if loss_po is None:
+            scores_po = self.model.score_po(triples[:, P], triples[:, O])
+            loss_po = self.loss(scores_po, triples[:, S]) / bs
+            del scores_po
         fwd += time.time()
         bwd -= time.time()
         loss_po.backward()

@@ -131,6 +131,16 @@ class RelationalScorer(KgeBase):
         return engine.score_all(self.engine_kind, d, self.precision(), self.l_norm(), ent, e_idx, rel, p_idx,
                                 ent, cand_idx)
 
+    def score_lookup_xent(self, ent: Tensor, rel: Tensor, e_idx: Tensor, p_idx: Tensor, direction: str,
+                          labels: Tensor, scale: float) -> Tensor:
+        """scale * sum_i CE(score_lookup(...)[i, :], labels[i]) in one engine pass (the
+        1vsAll loss of kge/job/train.py:1042,1052 fused into the scorer)."""
+        from .. import engine, _lib
+
+        d = _lib.DIR_SP if direction == "sp_" else _lib.DIR_PO
+        return engine.score_all_xent(self.engine_kind, d, self.precision(), self.l_norm(), ent, e_idx, rel, p_idx,
+                                     ent, None, labels, scale)
+
     def score_lookup_spo(self, ent: Tensor, rel: Tensor, s: Tensor, p: Tensor, o: Tensor) -> Tensor:
         from .. import engine
 
@@ -314,6 +324,22 @@ class KgeModel(KgeBase):
         o = self.get_o_embedder().embed(o)
         p = self.get_p_embedder().embed(p)
         return self._scorer.score_emb(s, p, o, combine="_po")
+
+    def score_sp_xent(self, s: Tensor, p: Tensor, o: Tensor, scale: float) -> Optional[Tensor]:
+        """scale * sum_i CrossEntropy(score_sp(s, p)[i, :], o[i]) fused into the engine, or
+        None when the fused path does not apply (non-lookup embedders, dropout, scorer
+        without an engine kernel): the caller then scores and applies its loss itself."""
+        tabs = self._lookup_tables()
+        if tabs is None:
+            return None
+        return self._scorer.score_lookup_xent(tabs[0], tabs[1], s, p, "sp_", o, scale)
+
+    def score_po_xent(self, p: Tensor, o: Tensor, s: Tensor, scale: float) -> Optional[Tensor]:
+        """scale * sum_i CrossEntropy(score_po(p, o)[i, :], s[i]) (see score_sp_xent)."""
+        tabs = self._lookup_tables()
+        if tabs is None:
+            return None
+        return self._scorer.score_lookup_xent(tabs[0], tabs[1], o, p, "_po", s, scale)
 
     def score_so(self, s: Tensor, o: Tensor, p: Tensor = None) -> Tensor:
         """[n, R] (or [n, |p|]) scores of (s_i, r_j, o_i) (kge_model.py:684-704)."""

@@ -46,6 +46,13 @@ class ReciprocalRelationsModel(KgeModel):
         o = self.get_o_embedder().embed(o)
         return self._scorer.score_emb(o, p, s, combine="sp_")
 
+    def score_po_xent(self, p: Tensor, o: Tensor, s: Tensor, scale: float):
+        tabs = self._lookup_tables()
+        if tabs is None:
+            return None
+        return self._scorer.score_lookup_xent(tabs[0], tabs[1], o, p + self.dataset.num_relations(), "sp_", s,
+                                              scale)
+
     def score_so(self, s, o, p=None):
         raise Exception("The reciprocal relations model cannot score relations.")
 

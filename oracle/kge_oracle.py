@@ -457,6 +457,21 @@ def entity_ranking(model, ent, rel, splits: Dict[str, np.ndarray], eval_split="v
 # ------------------------------------------------------------ 1vsAll training (F4)
 
 
+def softmax_xent(logits: np.ndarray, labels: np.ndarray, scale: float = 1.0):
+    """Per-row CrossEntropy(reduction="sum") of score rows against index labels and the
+    gradient of scale * sum_i loss_i w.r.t. the scores -- KLDivWithSoftmaxKgeLoss with
+    index labels (loss.py:192-208), divided by the batch size (train.py:1042,1052).
+    Returns (loss [n], G [n, m]) with G = scale * (softmax - onehot)."""
+    x = logits.astype(np.float64)
+    n = x.shape[0]
+    mx = x.max(1, keepdims=True)
+    lse = np.log(np.exp(x - mx).sum(1, keepdims=True)) + mx
+    loss = lse[:, 0] - x[np.arange(n), labels]
+    G = np.exp(x - lse)
+    G[np.arange(n), labels] -= 1.0
+    return loss, G * scale
+
+
 def train_1vsall(model, ent, rel, batches: Sequence[np.ndarray], lr=0.2, eps=1e-10):
     """TrainingJob1vsAll._process_batch (train.py:1032-1062) + Adagrad step.
 
@@ -483,13 +498,8 @@ def train_1vsall(model, ent, rel, batches: Sequence[np.ndarray], lr=0.2, eps=1e-
             else:
                 q = prep_po(model, P, O)
                 target = s
-            logits = q @ ent.T
-            mx = logits.max(1, keepdims=True)
-            lse = np.log(np.exp(logits - mx).sum(1, keepdims=True)) + mx
-            total += float((lse[:, 0] - logits[np.arange(B), target]).sum() / B)
-            G = np.exp(logits - lse)
-            G[np.arange(B), target] -= 1.0
-            G /= B
+            loss_rows, G = softmax_xent(q @ ent.T, target, 1.0 / B)
+            total += float(loss_rows.sum() / B)
             g_ent += G.T @ q
             dq = G @ ent
             if direction == "sp":

@@ -236,3 +236,82 @@ def test_contract_dispatch_and_errors(L):
     assert rel_err(s.cpu().numpy(), (q.double() @ t.double().T).cpu().numpy()) < 2e-5
     with pytest.raises(ValueError):
         L.score_dot(q, torch.randn(20, 5).cuda(), None, L.PREC_BF16X3)
+
+
+@pytest.mark.parametrize("m", [1, 7, 1001, 14541])
+@pytest.mark.parametrize("layout", ["padded_inplace", "padded_out", "tight_inplace"])
+def test_softmax_xent_vs_oracle(L, m, layout):
+    """kge_softmax_xent: per-row CE + G = scale * (softmax - onehot), vectorised (rows
+    padded to 16 B) and scalar (tight, odd leading dimension) paths, in place and not."""
+    rng = np.random.default_rng(m)
+    n = 37
+    S = (rng.standard_normal((n, m)) * 5).astype(np.float32)
+    if m > 8:
+        S[3, :] = -np.inf          # -inf entries add 0 ...
+        S[3, : m // 2] = rng.standard_normal(m // 2)
+        S[5, 1::3] = -np.inf
+    labels = rng.integers(0, m, size=n)
+    scale = 1.0 / n
+    ref_loss, ref_g = K.softmax_xent(S.astype(np.float64), labels, scale)
+    ld = (m + 3) // 4 * 4 if layout.startswith("padded") else m
+    buf = torch.full((n, ld), 123.0, device="cuda")
+    s = buf[:, :m]
+    s.copy_(dev(S))
+    g = s if layout.endswith("inplace") else torch.zeros((n, ld), device="cuda")[:, :m]
+    loss = L.softmax_xent(s, dev(labels, torch.int64), scale, g=g)
+    torch.cuda.synchronize()
+    np.testing.assert_allclose(loss.cpu().numpy(), ref_loss, rtol=2e-6, atol=2e-6 * np.abs(ref_loss).max())
+    gg = g.cpu().numpy()
+    assert np.abs(gg - ref_g).max() <= 2e-6 * scale, np.abs(gg - ref_g).max() / scale
+    if ld > m:  # padding columns untouched
+        assert torch.all(buf[:, m:] == 123.0) if layout == "padded_inplace" else True
+
+
+def test_softmax_xent_edge_cases(L):
+    n, m = 4, 50
+    S = np.zeros((n, m), np.float32)
+    S[1, 7] = np.nan
+    S[2, :] = -np.inf
+    labels = np.array([0, 1, 2, m + 5])  # last label out of range
+    s = dev(S)
+    lab = dev(labels, torch.int64)
+    out = torch.empty(n, device="cuda")
+    # raw C ABI: the Python wrapper's index check (KGE_CHECK_INDEX) would reject the label
+    assert L.lib().kge_softmax_xent(L.ptr(s), m, n, m, L.ptr(lab), 1.0, L.ptr(out), None, 0, L.stream()) == 0
+    loss = out.cpu().numpy()
+    assert abs(loss[0] - np.log(m)) < 1e-6   # uniform row
+    assert np.isnan(loss[1])                 # NaN score -> NaN loss (torch CE likewise)
+    assert np.isnan(loss[2])                 # all -inf row -> NaN (torch: nan)
+    assert np.isnan(loss[3])                 # label out of range
+    assert L.lib().kge_softmax_xent(L.ptr(s), m - 1, n, m, L.ptr(lab), 1.0, L.ptr(out), None, 0,
+                                    L.stream()) == 1001  # KGE_ERR_ARG: lds < m
+
+
+@pytest.mark.parametrize("n,m,d", [(300, 1001, 64), (1024, 2053, 512), (5, 17, 8)])
+@pytest.mark.parametrize("g_layout", ["padded", "tight"])
+@pytest.mark.parametrize("gather", [False, True])
+def test_backward_gemms_layouts(L, n, m, d, g_layout, gather):
+    """dQ = G.T[tidx] and dT[tidx] += G^T.Q in bf16x3: the vectorised kernel (G rows padded
+    to 16 B, as kge_softmax_xent writes them; transposed LDS reads) and the scalar one
+    (tight odd leading dimension, as autograd hands G over), with and without a candidate
+    gather (duplicates included), against float64."""
+    rng = np.random.default_rng(n + m + d)
+    G = rng.standard_normal((n, m)).astype(np.float32)
+    Q = rng.standard_normal((n, d)).astype(np.float32)
+    E = m + 7 if gather else m
+    T = rng.standard_normal((E, d)).astype(np.float32)
+    tidx = rng.integers(0, E, size=m) if gather else None
+    ld = (m + 3) // 4 * 4 + 4 if g_layout == "padded" else m
+    gb = torch.zeros((n, ld), device="cuda")
+    gb[:, :m] = dev(G)
+    g = gb[:, :m]
+    Tr = T[tidx] if gather else T
+    dq = L.score_dot_bwd_q(g, dev(T), dev(tidx, torch.int64) if gather else None, L.PREC_BF16X3)
+    dt = torch.zeros(E, d, device="cuda")
+    L.score_dot_bwd_t(g, dev(Q), dev(tidx, torch.int64) if gather else None, dt, L.PREC_BF16X3)
+    torch.cuda.synchronize()
+    ref_q = G.astype(np.float64) @ Tr.astype(np.float64)
+    ref_t = np.zeros((E, d))
+    np.add.at(ref_t, tidx if gather else np.arange(m), G.T.astype(np.float64) @ Q.astype(np.float64))
+    assert rel_err(dq.cpu().numpy(), ref_q) < 2e-5
+    assert rel_err(dt.cpu().numpy(), ref_t) < 2e-5
