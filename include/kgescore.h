@@ -167,6 +167,16 @@ int kge_score_spo_bwd(int model, float l_norm, const float* ent, int64_t ld_ent,
 int kge_softmax_xent(const float* s, int64_t lds, int64_t n, int64_t m, const int64_t* labels,
                      float scale, float* loss, float* g, int64_t ldg, void* stream);
 
+/* KvsAll: KL(t_i || softmax(S[i, :])) with the target built from the CSR list of positive
+ * columns of row i (l_ptr[n+1], l_col; unique per row) and label smoothing eps in [0, 1):
+ * labels = (1 - eps) y + 1/m if eps > 0 (kge/job/train.py:715-721), t = labels / |labels|_1
+ * (KLDivWithSoftmaxKgeLoss with a label matrix, kge/util/loss.py:209-213, reduction sum);
+ * g = scale * (sum_j t_ij * softmax(S[i, :]) - t_i).  Same aliasing rules as above.
+ * Replaces the dense label matrix + log_softmax + kl_div forward and backward. */
+int kge_softmax_kl(const float* s, int64_t lds, int64_t n, int64_t m, const int64_t* l_ptr,
+                   const int64_t* l_col, float smoothing, float scale, float* loss, float* g,
+                   int64_t ldg, void* stream);
+
 /* ---- entity-ranking counts (eval) --------------------------------------------------
  * For row i of a score chunk S[n, m] covering entities [c0, c0 + m):
  *   v_j = S[i, j], with v_{true_i - c0} := true_score[i] when true_i is in the chunk;

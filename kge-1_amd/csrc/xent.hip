@@ -1,14 +1,22 @@
-// Softmax cross entropy over all-entity score rows, fused with its gradient (the loss the
-// 1vsAll job puts on score_sp / score_po: KLDivWithSoftmaxKgeLoss with index labels ==
-// torch.nn.CrossEntropyLoss(reduction="sum"), reference kge/util/loss.py:192-208, divided
-// by the batch size in kge/job/train.py:1042,1052).
+// Softmax losses over all-entity score rows, fused with their gradient.
 //
-//   loss[i] = logsumexp_j S[i, j] - S[i, label_i]
-//   G[i, j] = scale * (softmax_j(S[i, :]) - [j == label_i])      (optional, may alias S)
+// KL(t_i || softmax(S_i)) for a target row t_i built from a list of positive columns P_i
+// (unique) and label smoothing eps, exactly as the reference builds it:
+//   labels = (1 - eps) * y + 1/m      (train.py:715-721, only when eps > 0)
+//   t      = labels / max(|labels|_1, 1e-12)                            (loss.py:211-213)
+// so t0 = (eps > 0 ? 1/m : 0) / Z off P_i, t1 = ((1 - eps) + (eps > 0 ? 1/m : 0)) / Z on
+// P_i, Z = (1 - eps)|P_i| + (eps > 0 ? 1 : 0).  With T = sum_j t_j (1, or 0 for an empty
+// row without smoothing):
+//   loss_i = sum_j t_j log t_j - sum_j t_j S_ij + T lse_i
+//          = H(t) - t0 rowsum_i - (t1 - t0) sum_{P_i} S_ij + T lse_i
+//   G_ij   = scale * (T softmax_ij - t_ij)
+// Index labels (1vsAll, KLDivWithSoftmaxKgeLoss -> CrossEntropyLoss, loss.py:198-208) are
+// the case |P_i| = 1, eps = 0: loss_i = lse_i - S_i,label, G = scale (softmax - onehot).
 //
-// HBM-bound: one workgroup per row reads the row once for an online (max, sum-exp), then
-// reads it again (L2 / MALL-resident: a row is 4m bytes and was just touched) to write G.
-// 8 bytes per element (read + write) + one re-read that should not reach HBM.
+// HBM-bound: one workgroup per row reads the row once for the online (max, sum-exp, sum),
+// then again (L2 / MALL-resident: 4m bytes just touched) to write G, which may alias S.
+// exp is v_exp_f32 (__expf): relative error ~|x| * 6e-8 for exp(x), x = score - max <= 0,
+// far inside the 1e-4 contract; libm expf made the kernel VALU-bound.
 #include <math.h>
 
 #include "common.h"
@@ -20,37 +28,44 @@ constexpr int NT = 256, U = 8;
 __device__ __forceinline__ void lse_merge(float& m, float& s, float m2, float s2) {
   const float mm = fmaxf(m, m2);
   if (mm == -INFINITY) return;  // both empty so far
-  s = s * expf(m - mm) + s2 * expf(m2 - mm);
+  s = s * __expf(m - mm) + s2 * __expf(m2 - mm);
   m = mm;
 }
 
+__device__ __forceinline__ float xlogx(float x) { return x > 0.f ? x * logf(x) : 0.f; }
+
+// l_ptr == NULL: index labels, P_i = {l_col[i]}
 template <bool VEC>
-__global__ void __launch_bounds__(NT) xent_kernel(const float* s, int64_t lds, int m,
-                                                  const int64_t* __restrict__ labels, float scale,
-                                                  float* __restrict__ loss, float* g, int64_t ldg) {
-  __shared__ float red_m[NT / 64], red_s[NT / 64];
+__global__ void __launch_bounds__(NT) softmax_kl_kernel(const float* s, int64_t lds, int m,
+                                                        const int64_t* __restrict__ l_ptr,
+                                                        const int64_t* __restrict__ l_col, float eps, float scale,
+                                                        float* __restrict__ loss, float* g, int64_t ldg) {
+  __shared__ float red[3][NT / 64];
   const int64_t row = blockIdx.x;
   const float* sr = s + row * lds;
   const int tid = threadIdx.x;
-  const int64_t lab = labels[row];
-  const bool lab_ok = lab >= 0 && lab < m;
-  // S[i, label] is read before any thread can overwrite the row (g may alias s)
-  const float s_lab = (tid == 0 && lab_ok) ? sr[lab] : 0.f;
+  const int64_t p0 = l_ptr ? l_ptr[row] : row, p1 = l_ptr ? l_ptr[row + 1] : row + 1;
 
-  // pass 1: per-thread online (max, sum exp(x - max)); NaN propagates through the sum
-  float mx = -INFINITY, sm = 0.f;
+  // pass 1: online (max, sum exp(x - max)), row sum, and the positives' scores -- all read
+  // before the reduction barrier, i.e. before any thread overwrites the row (g may alias s)
+  float mx = -INFINITY, sm = 0.f, rs = 0.f, ps = 0.f;
+  for (int64_t k = p0 + tid; k < p1; k += NT) {
+    const int64_t c = l_col[k];
+    ps += (c >= 0 && c < m) ? sr[c] : NAN;  // a label outside the row poisons the loss
+  }
   auto take = [&](float v) {
+    rs += v;
     if (v > mx) {
-      sm = sm * expf(mx - v) + 1.f;
+      sm = sm * __expf(mx - v) + 1.f;
       mx = v;
     } else if (v != -INFINITY) {  // -inf adds 0 (and would be NaN while mx is -inf)
-      sm += expf(v - mx);
+      sm += __expf(v - mx);
     }
   };
   int j0 = 0;
   if (VEC) {
-    // U float4 loads in flight per thread before any of them is consumed (the running
-    // (max, sum) is a dependency chain: one load per iteration would be latency-bound)
+    // U float4 loads in flight per thread before any is consumed: the running (max, sum)
+    // is a dependency chain, one load per iteration would be latency-bound
     const int m4 = m & ~3;
     for (int base = 0; base < m4; base += NT * 4 * U) {
       float4 v[U];
@@ -58,11 +73,13 @@ __global__ void __launch_bounds__(NT) xent_kernel(const float* s, int64_t lds, i
       for (int u = 0; u < U; ++u) v[u] = *reinterpret_cast<const float4*>(sr + min(base + (u * NT + tid) * 4, m4 - 4));
 #pragma unroll
       for (int u = 0; u < U; ++u) {
-        if (base + (u * NT + tid) * 4 >= m4) v[u] = make_float4(-INFINITY, -INFINITY, -INFINITY, -INFINITY);
+        if (base + (u * NT + tid) * 4 >= m4) continue;
+        rs += (v[u].x + v[u].y) + (v[u].z + v[u].w);
         const float vm = fmaxf(fmaxf(v[u].x, v[u].y), fmaxf(v[u].z, v[u].w));
         const float nm = fmaxf(mx, vm);
         if (nm != -INFINITY) {
-          sm = sm * expf(mx - nm) + expf(v[u].x - nm) + expf(v[u].y - nm) + expf(v[u].z - nm) + expf(v[u].w - nm);
+          sm = sm * __expf(mx - nm) + __expf(v[u].x - nm) + __expf(v[u].y - nm) + __expf(v[u].z - nm) +
+               __expf(v[u].w - nm);
           mx = nm;
         } else if (v[u].x != v[u].x || v[u].y != v[u].y || v[u].z != v[u].z || v[u].w != v[u].w) {
           sm = NAN;
@@ -72,45 +89,91 @@ __global__ void __launch_bounds__(NT) xent_kernel(const float* s, int64_t lds, i
     j0 = m4;
   }
   for (int j = j0 + tid; j < m; j += NT) take(sr[j]);
-  // NaN anywhere in the row: fmaxf drops NaN from the max but expf(NaN) poisons the sum
+  // NaN anywhere in the row: fmaxf drops NaN from the max but exp(NaN) poisons the sum
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) {
     const float m2 = __shfl_xor(mx, off, 64), s2 = __shfl_xor(sm, off, 64);
     lse_merge(mx, sm, m2, s2);
+    rs += __shfl_xor(rs, off, 64);
+    ps += __shfl_xor(ps, off, 64);
   }
   if ((tid & 63) == 0) {
-    red_m[tid >> 6] = mx;
-    red_s[tid >> 6] = sm;
+    red[0][tid >> 6] = mx;
+    red[1][tid >> 6] = sm;
+    red[2][tid >> 6] = rs;
   }
   __syncthreads();
-  mx = red_m[0];
-  sm = red_s[0];
+  mx = red[0][0];
+  sm = red[1][0];
+  rs = red[2][0];
 #pragma unroll
-  for (int w = 1; w < NT / 64; ++w) lse_merge(mx, sm, red_m[w], red_s[w]);
-  const float lse = mx + logf(sm);
-  if (tid == 0) loss[row] = lab_ok ? lse - s_lab : NAN;
+  for (int w = 1; w < NT / 64; ++w) {
+    lse_merge(mx, sm, red[0][w], red[1][w]);
+    rs += red[2][w];
+  }
+  __syncthreads();
+  if ((tid & 63) == 0) red[0][tid >> 6] = ps;
+  __syncthreads();
+  ps = red[0][0];
+#pragma unroll
+  for (int w = 1; w < NT / 64; ++w) ps += red[0][w];
+
+  const float lse = mx + __logf(sm);
+  const int64_t np = p1 - p0;
+  const float u = eps > 0.f ? 1.f / (float)m : 0.f;
+  const float z = (1.f - eps) * (float)np + (eps > 0.f ? 1.f : 0.f);
+  const float zi = z > 1e-12f ? 1.f / z : 0.f;  // F.normalize: x / max(|x|_1, 1e-12)
+  const float t0 = u * zi, t1 = ((1.f - eps) + u) * zi;
+  const float T = z > 0.f ? 1.f : 0.f;
+  if (tid == 0) {
+    if (!l_ptr) {  // index label: exactly lse - S[label] (no 0 * inf from the general form)
+      loss[row] = lse - ps;
+    } else {
+      const float H = (float)(m - np) * xlogx(t0) + (float)np * xlogx(t1);
+      loss[row] = H - t0 * rs - (t1 - t0) * ps + (T > 0.f ? lse : 0.f);
+    }
+  }
   if (!g) return;
 
-  // pass 2: G = scale * (exp(x - lse) - onehot)
+  // pass 2: G = scale * (T softmax - t0), then positives -= scale * (t1 - t0)
   float* gr = g + row * ldg;
+  const float a = scale * T, b = scale * t0;
   if (VEC) {
     const int m4 = m & ~3;
     for (int base = 0; base < m4; base += NT * 4 * U) {
       float4 v[U];
 #pragma unroll
-      for (int u = 0; u < U; ++u) v[u] = *reinterpret_cast<const float4*>(sr + min(base + (u * NT + tid) * 4, m4 - 4));
+      for (int q = 0; q < U; ++q) v[q] = *reinterpret_cast<const float4*>(sr + min(base + (q * NT + tid) * 4, m4 - 4));
 #pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const int j = base + (u * NT + tid) * 4;
+      for (int q = 0; q < U; ++q) {
+        const int j = base + (q * NT + tid) * 4;
         if (j < m4)
-          *reinterpret_cast<float4*>(gr + j) = make_float4(scale * expf(v[u].x - lse), scale * expf(v[u].y - lse),
-                                                           scale * expf(v[u].z - lse), scale * expf(v[u].w - lse));
+          *reinterpret_cast<float4*>(gr + j) =
+              make_float4(a * __expf(v[q].x - lse) - b, a * __expf(v[q].y - lse) - b, a * __expf(v[q].z - lse) - b,
+                          a * __expf(v[q].w - lse) - b);
       }
     }
   }
-  for (int j = j0 + tid; j < m; j += NT) gr[j] = scale * expf(sr[j] - lse);
-  __syncthreads();  // every write of the row is ordered before the label fix-up
-  if (tid == 0 && lab_ok) gr[lab] = scale * (expf(s_lab - lse) - 1.f);
+  for (int j = j0 + tid; j < m; j += NT) gr[j] = a * __expf(sr[j] - lse) - b;
+  __syncthreads();  // every write of the row is ordered before the positives' fix-up
+  const float d = scale * (t1 - t0);
+  for (int64_t k = p0 + tid; k < p1; k += NT) {
+    const int64_t c = l_col[k];
+    if (c >= 0 && c < m) gr[c] -= d;
+  }
+}
+
+int launch(const float* s, int64_t lds, int64_t n, int64_t m, const int64_t* l_ptr, const int64_t* l_col, float eps,
+           float scale, float* loss, float* g, int64_t ldg, hipStream_t st) {
+  const bool vec = lds % 4 == 0 && aligned16(s) && (!g || (ldg % 4 == 0 && aligned16(g)));
+  if (vec)
+    softmax_kl_kernel<true><<<dim3((unsigned)n), dim3(NT), 0, st>>>(s, lds, (int)m, l_ptr, l_col, eps, scale, loss,
+                                                                    g, ldg);
+  else
+    softmax_kl_kernel<false><<<dim3((unsigned)n), dim3(NT), 0, st>>>(s, lds, (int)m, l_ptr, l_col, eps, scale, loss,
+                                                                     g, ldg);
+  KGE_CHECK_LAUNCH();
+  return 0;
 }
 
 }  // namespace
@@ -121,12 +184,16 @@ extern "C" int kge_softmax_xent(const float* s, int64_t lds, int64_t n, int64_t 
   KGE_REQUIRE(s && labels && loss && lds >= m && (!g || ldg >= m));
   KGE_REQUIRE(!g || g != s || ldg == lds);  // in place only row-for-row
   if (n == 0) return 0;
-  hipStream_t st = as_stream(stream);
-  const bool vec = lds % 4 == 0 && aligned16(s) && (!g || (ldg % 4 == 0 && aligned16(g)));
-  if (vec)
-    xent_kernel<true><<<dim3((unsigned)n), dim3(NT), 0, st>>>(s, lds, (int)m, labels, scale, loss, g, ldg);
-  else
-    xent_kernel<false><<<dim3((unsigned)n), dim3(NT), 0, st>>>(s, lds, (int)m, labels, scale, loss, g, ldg);
-  KGE_CHECK_LAUNCH();
-  return 0;
+  return launch(s, lds, n, m, nullptr, labels, 0.f, scale, loss, g, ldg, as_stream(stream));
+}
+
+extern "C" int kge_softmax_kl(const float* s, int64_t lds, int64_t n, int64_t m, const int64_t* l_ptr,
+                              const int64_t* l_col, float smoothing, float scale, float* loss, float* g, int64_t ldg,
+                              void* stream) {
+  KGE_REQUIRE(n >= 0 && m > 0 && m < (1LL << 31) && n < (1LL << 31));
+  KGE_REQUIRE(s && l_ptr && l_col && loss && lds >= m && (!g || ldg >= m));
+  KGE_REQUIRE(!g || g != s || ldg == lds);
+  KGE_REQUIRE(smoothing >= 0.f && smoothing < 1.f);
+  if (n == 0) return 0;
+  return launch(s, lds, n, m, l_ptr, l_col, smoothing, scale, loss, g, ldg, as_stream(stream));
 }

@@ -49,6 +49,7 @@ SIGNATURES = {
     "kge_rank_counts": ([_P, _I64, _I64, _I64, _I64, _P, _P, _P, _P, _P, _P, _P, _P, _P], _I),
     "kge_rank_hist": ([_P, _P, _I64, _I, _P, _P, _I64, _P], _I),
     "kge_softmax_xent": ([_P, _I64, _I64, _I64, _P, _F, _P, _P, _I64, _P], _I),
+    "kge_softmax_kl": ([_P, _I64, _I64, _I64, _P, _P, _F, _F, _P, _P, _I64, _P], _I),
 }
 
 _lib: Optional[ctypes.CDLL] = None
@@ -314,4 +315,21 @@ def softmax_xent(s, labels, scale, g=None, loss=None):
         loss = torch.empty(n, device=s.device, dtype=torch.float32)
     _check(lib().kge_softmax_xent(ptr(s), rows(s), n, m, ptr(labels), float(scale), ptr(loss), ptr(g),
                                   rows(g) if g is not None else 0, stream()), "kge_softmax_xent")
+    return loss
+
+
+def softmax_kl(s, l_ptr, l_col, smoothing, scale, g=None, loss=None):
+    """Per-row KL(t || softmax(S[:, :m])) for CSR positive lists (l_ptr [n+1], l_col) with
+    label smoothing; optionally G = scale * (T softmax - t) into g (g may be s).  Returns the
+    per-row losses [n] (unscaled)."""
+    require_device(s)
+    l_ptr, l_col = idx64(l_ptr), idx64(l_col)
+    n, m = s.shape
+    if l_ptr.numel() != n + 1:
+        raise ValueError(f"l_ptr has {l_ptr.numel()} entries, expected {n + 1}")
+    check_index(l_col, m, "label column")
+    if loss is None:
+        loss = torch.empty(n, device=s.device, dtype=torch.float32)
+    _check(lib().kge_softmax_kl(ptr(s), rows(s), n, m, ptr(l_ptr), ptr(l_col), float(smoothing), float(scale),
+                                ptr(loss), ptr(g), rows(g) if g is not None else 0, stream()), "kge_softmax_kl")
     return loss

@@ -129,14 +129,18 @@ class _ScoreXent(torch.autograd.Function):
     contraction's backward GEMMs (whose loads vectorise on the padded rows)."""
 
     @staticmethod
-    def forward(ctx, kind, direction, precision, l_norm, ent, eidx, rel, ridx, tab, tidx, labels, scale):
+    def forward(ctx, kind, direction, precision, l_norm, ent, eidx, rel, ridx, tab, tidx, labels, l_ptr, smoothing,
+                scale):
         ent, rel, tab = _rows(ent), _rows(rel), _rows(tab)
         n = eidx.numel() if eidx is not None else ent.shape[0]
         m = tidx.numel() if tidx is not None else tab.shape[0]
         buf = torch.empty(n, (m + 3) // 4 * 4, device=tab.device, dtype=torch.float32)
         s, q = _scores_forward(ctx, kind, direction, precision, l_norm, ent, eidx, rel, ridx, tab, tidx,
                                out=buf[:, :m])
-        loss_rows = L.softmax_xent(s, labels, scale, g=s)
+        if l_ptr is None:  # index labels (1vsAll)
+            loss_rows = L.softmax_xent(s, labels, scale, g=s)
+        else:  # CSR positive lists (KvsAll)
+            loss_rows = L.softmax_kl(s, l_ptr, labels, smoothing, scale, g=s)
         ctx.save_for_backward(ent, eidx, rel, ridx, tab, tidx, q, s)
         return loss_rows.sum() * scale
 
@@ -144,19 +148,23 @@ class _ScoreXent(torch.autograd.Function):
     def backward(ctx, gl):
         ent, eidx, rel, ridx, tab, tidx, q, g = ctx.saved_tensors
         d_ent, d_rel, d_tab = _scores_backward(ctx, g, ent, eidx, rel, ridx, tab, tidx, q, gscale=gl)
-        return None, None, None, None, d_ent, None, d_rel, None, d_tab, None, None, None
+        return None, None, None, None, d_ent, None, d_rel, None, d_tab, None, None, None, None, None
 
 
 def score_all_xent(kind: int, direction: int, precision: int, l_norm: float, ent: torch.Tensor,
                    eidx: Optional[torch.Tensor], rel: torch.Tensor, ridx: Optional[torch.Tensor],
                    tab: torch.Tensor, tidx: Optional[torch.Tensor], labels: torch.Tensor,
-                   scale: float) -> torch.Tensor:
-    """scale * sum_i CrossEntropy(score_all(...)[i, :], labels[i]) -- the 1vsAll objective
-    (kge/util/loss.py:192-208 with index labels; kge/job/train.py:1042,1052) fused with its
-    gradient; returns a 0-dim tensor that backpropagates into ent / rel / tab."""
+                   scale: float, l_ptr: Optional[torch.Tensor] = None, smoothing: float = 0.0) -> torch.Tensor:
+    """scale * sum_i loss_i(score_all(...)[i, :]) fused with its gradient; a 0-dim tensor that
+    backpropagates into ent / rel / tab.
+      l_ptr None: labels[i] is the index of row i's target, loss_i = CrossEntropy -- the
+                  1vsAll objective (kge/util/loss.py:192-208; kge/job/train.py:1042,1052);
+      otherwise : labels[l_ptr[i]:l_ptr[i+1]] are row i's positives, loss_i = KL against
+                  the smoothed, L1-normalised label row -- the KvsAll objective
+                  (kge/util/loss.py:209-213; kge/job/train.py:715-721, 744-751)."""
     L.require_device(ent, rel, tab)
     return _ScoreXent.apply(kind, direction, precision, float(l_norm), ent, L.idx64(eidx), rel, L.idx64(ridx),
-                            tab, L.idx64(tidx), L.idx64(labels), float(scale))
+                            tab, L.idx64(tidx), L.idx64(labels), L.idx64(l_ptr), float(smoothing), float(scale))
 
 
 def score_all(kind: int, direction: int, precision: int, l_norm: float, ent: torch.Tensor,

@@ -234,18 +234,32 @@ class TrainingJobKvsAll(TrainingJob):
             rows = torch.repeat_interleave(torch.arange(len(sel), device=self.device), lens)
             pos = torch.arange(int(lens.sum().item()), device=self.device) - torch.repeat_interleave(
                 torch.cumsum(lens, 0) - lens, lens) + torch.repeat_interleave(lo, lens)
-            labels = torch.zeros(len(sel), E, device=self.device)
-            labels[rows, vals[pos]] = 1.0
-            if self.label_smoothing > 0.0:
-                labels = (1.0 - self.label_smoothing) * labels + 1.0 / E
-            t += time.time()
-            fwd -= time.time()
-            if qt == "sp_":
-                scores = self.model.score_sp(q[:, 0], q[:, 1])
+            loss = None
+            if self.config.get("engine.fused_loss") and isinstance(self.loss, KLDivWithSoftmaxKgeLoss):
+                # positives as a CSR (no dense label matrix); KL + gradient in the engine
+                l_ptr = torch.cat((lens.new_zeros(1), torch.cumsum(lens, 0)))
+                l_col = vals[pos]
+                t += time.time()
+                fwd -= time.time()
+                fn = self.model.score_sp_kl if qt == "sp_" else self.model.score_po_kl
+                loss = fn(q[:, 0], q[:, 1], l_ptr, l_col, self.label_smoothing, 1.0 / bs)
+                fwd += time.time()
+                t -= time.time()
+            if loss is None:
+                labels = torch.zeros(len(sel), E, device=self.device)
+                labels[rows, vals[pos]] = 1.0
+                if self.label_smoothing > 0.0:
+                    labels = (1.0 - self.label_smoothing) * labels + 1.0 / E
+                t += time.time()
+                fwd -= time.time()
+                if qt == "sp_":
+                    scores = self.model.score_sp(q[:, 0], q[:, 1])
+                else:
+                    scores = self.model.score_po(q[:, 0], q[:, 1])
+                loss = self.loss(scores, labels) / bs
+                fwd += time.time()
             else:
-                scores = self.model.score_po(q[:, 0], q[:, 1])
-            loss = self.loss(scores, labels) / bs
-            fwd += time.time()
+                t += time.time()
             bwd -= time.time()
             loss.backward()
             bwd += time.time()

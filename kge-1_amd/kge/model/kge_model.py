@@ -132,14 +132,15 @@ class RelationalScorer(KgeBase):
                                 ent, cand_idx)
 
     def score_lookup_xent(self, ent: Tensor, rel: Tensor, e_idx: Tensor, p_idx: Tensor, direction: str,
-                          labels: Tensor, scale: float) -> Tensor:
+                          labels: Tensor, scale: float, l_ptr: Optional[Tensor] = None,
+                          smoothing: float = 0.0) -> Tensor:
         """scale * sum_i CE(score_lookup(...)[i, :], labels[i]) in one engine pass (the
         1vsAll loss of kge/job/train.py:1042,1052 fused into the scorer)."""
         from .. import engine, _lib
 
         d = _lib.DIR_SP if direction == "sp_" else _lib.DIR_PO
         return engine.score_all_xent(self.engine_kind, d, self.precision(), self.l_norm(), ent, e_idx, rel, p_idx,
-                                     ent, None, labels, scale)
+                                     ent, None, labels, scale, l_ptr, smoothing)
 
     def score_lookup_spo(self, ent: Tensor, rel: Tensor, s: Tensor, p: Tensor, o: Tensor) -> Tensor:
         from .. import engine
@@ -340,6 +341,23 @@ class KgeModel(KgeBase):
         if tabs is None:
             return None
         return self._scorer.score_lookup_xent(tabs[0], tabs[1], o, p, "_po", s, scale)
+
+    def score_sp_kl(self, s: Tensor, p: Tensor, l_ptr: Tensor, l_col: Tensor, smoothing: float,
+                    scale: float) -> Optional[Tensor]:
+        """KvsAll: scale * sum_i KL(label row i || softmax(score_sp(s, p)[i, :])) fused into the
+        engine; row i's positives are l_col[l_ptr[i]:l_ptr[i+1]].  None when not fusable."""
+        tabs = self._lookup_tables()
+        if tabs is None:
+            return None
+        return self._scorer.score_lookup_xent(tabs[0], tabs[1], s, p, "sp_", l_col, scale, l_ptr, smoothing)
+
+    def score_po_kl(self, p: Tensor, o: Tensor, l_ptr: Tensor, l_col: Tensor, smoothing: float,
+                    scale: float) -> Optional[Tensor]:
+        """KvsAll (?, p, o) queries; see score_sp_kl."""
+        tabs = self._lookup_tables()
+        if tabs is None:
+            return None
+        return self._scorer.score_lookup_xent(tabs[0], tabs[1], o, p, "_po", l_col, scale, l_ptr, smoothing)
 
     def score_so(self, s: Tensor, o: Tensor, p: Tensor = None) -> Tensor:
         """[n, R] (or [n, |p|]) scores of (s_i, r_j, o_i) (kge_model.py:684-704)."""

@@ -53,6 +53,13 @@ class ReciprocalRelationsModel(KgeModel):
         return self._scorer.score_lookup_xent(tabs[0], tabs[1], o, p + self.dataset.num_relations(), "sp_", s,
                                               scale)
 
+    def score_po_kl(self, p: Tensor, o: Tensor, l_ptr: Tensor, l_col: Tensor, smoothing: float, scale: float):
+        tabs = self._lookup_tables()
+        if tabs is None:
+            return None
+        return self._scorer.score_lookup_xent(tabs[0], tabs[1], o, p + self.dataset.num_relations(), "sp_", l_col,
+                                              scale, l_ptr, smoothing)
+
     def score_so(self, s, o, p=None):
         raise Exception("The reciprocal relations model cannot score relations.")
 

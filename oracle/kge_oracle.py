@@ -472,6 +472,29 @@ def softmax_xent(logits: np.ndarray, labels: np.ndarray, scale: float = 1.0):
     return loss, G * scale
 
 
+def softmax_kl(logits: np.ndarray, positives: Sequence[np.ndarray], smoothing: float = 0.0, scale: float = 1.0):
+    """KvsAll loss per row: KLDivLoss(reduction="sum")(log_softmax(S), normalize(labels, p=1))
+    (loss.py:209-213) with labels = 0/1 rows of the positive lists, label-smoothed as
+    (1 - eps) * labels + 1 / m when eps > 0 (train.py:715-721).  Returns (loss [n], G) with
+    G the gradient of scale * sum_i loss_i w.r.t. the scores."""
+    x = logits.astype(np.float64)
+    n, m = x.shape
+    y = np.zeros((n, m))
+    for i, cols in enumerate(positives):
+        y[i, np.asarray(cols, np.int64)] = 1.0
+    if smoothing > 0.0:
+        y = (1.0 - smoothing) * y + 1.0 / m
+    t = y / np.maximum(np.abs(y).sum(1, keepdims=True), 1e-12)
+    mx = x.max(1, keepdims=True)
+    lse = np.log(np.exp(x - mx).sum(1, keepdims=True)) + mx
+    logsm = x - lse
+    with np.errstate(divide="ignore", invalid="ignore"):
+        tlogt = np.where(t > 0, t * np.log(np.where(t > 0, t, 1.0)), 0.0)
+    loss = (tlogt - t * logsm).sum(1)
+    G = np.exp(logsm) * t.sum(1, keepdims=True) - t
+    return loss, G * scale
+
+
 def train_1vsall(model, ent, rel, batches: Sequence[np.ndarray], lr=0.2, eps=1e-10):
     """TrainingJob1vsAll._process_batch (train.py:1032-1062) + Adagrad step.
 
