@@ -177,6 +177,29 @@ int kge_softmax_kl(const float* s, int64_t lds, int64_t n, int64_t m, const int6
                    const int64_t* l_col, float smoothing, float scale, float* loss, float* g,
                    int64_t ldg, void* stream);
 
+/* ---- per-row candidate lists (negative sampling) -------------------------------------
+ * out[i, c] = score(Q[i, :], ent[cand[i, c], :])  i in [0, n), c in [0, k), with the
+ * semantics of KgeModel.score_spo on the triple the candidate completes (kge_model.py:620-637):
+ *   ComplEx / DistMult / RESCAL: <q, e>   (Q from kge_prep_query, either direction)
+ *   TransE : -|| sigma (q - e) + 1e-6 ||_p, sigma = +1 (dir SP: s+p-o') / -1 (dir PO: s'+p-o)
+ *            (F.pairwise_distance, transe.py:221)
+ *   RotatE : sum_k |q_k - e_k|_C (p = 1) or its L2 form; (s o rot(p)) - o' / s' o rot(p) - o
+ *            via |s' - o conj(rot(p))| = |s' o rot(p) - o|  (rotate.py:18-50)
+ * Replaces the B x (1 + N) triple construction + score_spo of TrainingJobNegativeSampling's
+ * "triple" implementation (kge/job/train.py:868-892).  d <= 4096. */
+int kge_score_cand(int model, float l_norm, int dir, const float* q, int64_t ldq, const float* ent,
+                   int64_t ld_ent, const int64_t* cand, int64_t ldc, int64_t n, int64_t k, int d,
+                   float* out, int64_t ldo, void* stream);
+
+/* backward: dq[i, :] = sum_c g[i, c] d out[i, c] / d q (written; dq may be NULL) and
+ * d_ent[cand[i, c], :] += g[i, c] d out[i, c] / d e (atomic; may be NULL).  s = the forward
+ * scores (needed by TransE / RotatE, whose L2 norms it holds).  d <= 3584. */
+int kge_score_cand_bwd(int model, float l_norm, int dir, const float* q, int64_t ldq,
+                       const float* ent, int64_t ld_ent, const int64_t* cand, int64_t ldc,
+                       int64_t n, int64_t k, int d, const float* s, int64_t lds, const float* g,
+                       int64_t ldg, float* dq, int64_t lddq, float* d_ent, int64_t ld_dent,
+                       void* stream);
+
 /* ---- entity-ranking counts (eval) --------------------------------------------------
  * For row i of a score chunk S[n, m] covering entities [c0, c0 + m):
  *   v_j = S[i, j], with v_{true_i - c0} := true_score[i] when true_i is in the chunk;

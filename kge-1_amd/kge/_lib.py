@@ -50,6 +50,9 @@ SIGNATURES = {
     "kge_rank_hist": ([_P, _P, _I64, _I, _P, _P, _I64, _P], _I),
     "kge_softmax_xent": ([_P, _I64, _I64, _I64, _P, _F, _P, _P, _I64, _P], _I),
     "kge_softmax_kl": ([_P, _I64, _I64, _I64, _P, _P, _F, _F, _P, _P, _I64, _P], _I),
+    "kge_score_cand": ([_I, _F, _I, _P, _I64, _P, _I64, _P, _I64, _I64, _I64, _I, _P, _I64, _P], _I),
+    "kge_score_cand_bwd": ([_I, _F, _I, _P, _I64, _P, _I64, _P, _I64, _I64, _I64, _I, _P, _I64, _P, _I64, _P,
+                            _I64, _P, _I64, _P], _I),
 }
 
 _lib: Optional[ctypes.CDLL] = None
@@ -316,6 +319,31 @@ def softmax_xent(s, labels, scale, g=None, loss=None):
     _check(lib().kge_softmax_xent(ptr(s), rows(s), n, m, ptr(labels), float(scale), ptr(loss), ptr(g),
                                   rows(g) if g is not None else 0, stream()), "kge_softmax_xent")
     return loss
+
+
+def score_cand(model, l_norm, direction, q, ent, cand, out=None):
+    """out[i, c] = score(q_i, ent[cand[i, c]]) with score_spo semantics (kge_score_cand)."""
+    require_device(q, ent, cand)
+    cand = cand if (cand.dtype == torch.int64 and cand.dim() == 2 and cand.stride(1) == 1) else \
+        cand.long().contiguous()
+    check_index(cand, ent.shape[0], "candidate index")
+    n, k = cand.shape
+    d = q.shape[1]
+    o = out if out is not None else torch.empty(n, k, device=q.device, dtype=torch.float32)
+    _check(lib().kge_score_cand(model, float(l_norm), direction, ptr(q), rows(q), ptr(ent), rows(ent), ptr(cand),
+                                cand.stride(0), n, k, d, ptr(o), rows(o), stream()), "kge_score_cand")
+    return o
+
+
+def score_cand_bwd(model, l_norm, direction, q, ent, cand, s, g, dq, d_ent):
+    cand = cand if (cand.dtype == torch.int64 and cand.dim() == 2 and cand.stride(1) == 1) else \
+        cand.long().contiguous()
+    n, k = cand.shape
+    d = q.shape[1]
+    _check(lib().kge_score_cand_bwd(model, float(l_norm), direction, ptr(q), rows(q), ptr(ent), rows(ent),
+                                    ptr(cand), cand.stride(0), n, k, d, ptr(s), rows(s) if s is not None else 0,
+                                    ptr(g), rows(g), ptr(dq), rows(dq) if dq is not None else 0, ptr(d_ent),
+                                    rows(d_ent) if d_ent is not None else 0, stream()), "kge_score_cand_bwd")
 
 
 def softmax_kl(s, l_ptr, l_col, smoothing, scale, g=None, loss=None):

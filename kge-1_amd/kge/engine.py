@@ -203,6 +203,43 @@ def score_spo(kind: int, l_norm: float, ent, sidx, rel, pidx, oidx) -> torch.Ten
     return _ScoreSpo.apply(kind, float(l_norm), ent, L.idx64(sidx), rel, L.idx64(pidx), L.idx64(oidx))
 
 
+class _ScoreCand(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, kind, direction, l_norm, ent, eidx, rel, ridx, cand):
+        ent, rel = _rows(ent), _rows(rel)
+        n = eidx.numel()
+        d_e, d_r = ent.shape[1], rel.shape[1]
+        q = L.prep_query(kind, direction, ent, eidx, rel, ridx, n, d_e, d_r)
+        s = L.score_cand(kind, l_norm, direction, q, ent, cand)
+        ctx.meta = (kind, direction, l_norm, n, d_e, d_r)
+        ctx.save_for_backward(ent, eidx, rel, ridx, cand, q, s)
+        return s
+
+    @staticmethod
+    def backward(ctx, g):
+        kind, direction, l_norm, n, d_e, d_r = ctx.meta
+        ent, eidx, rel, ridx, cand, q, s = ctx.saved_tensors
+        need_ent, need_rel = ctx.needs_input_grad[3], ctx.needs_input_grad[5]
+        d_ent = torch.zeros_like(ent) if need_ent else None
+        d_rel = torch.zeros_like(rel) if need_rel else None
+        dq = torch.empty_like(q) if (need_ent or need_rel) else None
+        L.score_cand_bwd(kind, l_norm, direction, q, ent, cand, s, _rows(g.float()), dq, d_ent)
+        if dq is not None:
+            L.prep_query_bwd(kind, direction, ent, eidx, rel, ridx, n, d_e, d_r, dq, d_ent, d_rel)
+        return None, None, None, d_ent, None, d_rel, None, None
+
+
+def score_cand(kind: int, direction: int, l_norm: float, ent: torch.Tensor, eidx: torch.Tensor, rel: torch.Tensor,
+               ridx: torch.Tensor, cand: torch.Tensor) -> torch.Tensor:
+    """[n, k] scores of query i = prep(ent[eidx[i]], rel[ridx[i]]) against its own candidates
+    ent[cand[i, :]] -- KgeModel.score_spo of the n * k triples that complete each query with
+    a candidate (the negative-sampling "triple" scoring, kge/job/train.py:868-892) without
+    materialising them."""
+    L.require_device(ent, rel, cand)
+    return _ScoreCand.apply(kind, direction, float(l_norm), ent, L.idx64(eidx), rel, L.idx64(ridx),
+                            cand.long() if cand.dtype != torch.int64 else cand)
+
+
 def score_spo_emb(kind: int, l_norm: float, s_emb, p_emb, o_emb) -> torch.Tensor:
     """combine="spo" on embedding rows: s, o stacked into one table."""
     n = p_emb.shape[0]

@@ -1,0 +1,113 @@
+"""TrainingJobNegativeSampling (kge/job/train.py:759-999) on the engine.
+
+Per batch and corrupted slot, each positive (s, p, o) is scored together with its N
+negatives -- a [B, 1 + N] score matrix whose column 0 is the positive -- and the configured
+loss is applied with labels[:, 0] = 1.  Implementations (negative_sampling.implementation):
+
+* ``triple`` -- the reference scores B * (1 + N) materialised triples with score_spo
+  (train.py:868-892).  Here the s / o slots go through KgeModel.score_sp_cand /
+  score_po_cand: the fused candidate-gather kernel kge_score_cand, same per-triple
+  semantics, no triple tensor.  The p slot (and models without the fused path) fall back to
+  score_spo on expanded triples -- itself an engine kernel (kge_score_spo).
+* ``all``   -- score_sp / score_po against every entity, then pick (train.py:893-930).
+* ``batch`` -- score against the chunk's unique targets, then pick (train.py:931-968).
+
+Negatives are drawn on the device (kge/util/sampler.py), so the step has no host work
+beyond its one loss read-back.
+"""
+from __future__ import annotations
+
+import math
+import time
+
+import torch
+
+from ..util.sampler import KgeSampler, O, P, S
+from .train import TrainingJob
+
+
+class TrainingJobNegativeSampling(TrainingJob):
+    def __init__(self, config, dataset, parent_job=None, model=None):
+        super().__init__(config, dataset, parent_job, model=model)
+        self._sampler = KgeSampler.create(config, "negative_sampling", dataset, self.device)
+        impl = config.get("negative_sampling.implementation")
+        if impl not in ("triple", "all", "batch", "auto"):
+            raise ValueError(f"negative_sampling.implementation={impl}")
+        if impl == "auto":  # train.py:762-771
+            impl = "batch" if (self._sampler.shared or max(self._sampler.num_samples) > 30) else "triple"
+        self._implementation = impl
+        self._max_chunk_size = config.get("negative_sampling.chunk_size")
+        self.type_str = "negative_sampling"
+
+    def _prepare(self):
+        super()._prepare()
+        self.num_examples = self.dataset.split(self.train_split).size(0)
+
+    def _collate(self, example_ids):
+        return {"triples": self.dataset.split(self.train_split)[example_ids, :].long()}
+
+    # --------------------------------------------------------------------- scoring
+    def _scores(self, triples: torch.Tensor, slot: int, neg: torch.Tensor) -> torch.Tensor:
+        """[chunk, 1 + N] scores, column 0 the positive."""
+        cand = torch.cat((triples[:, [slot]], neg), 1)
+        n, k = cand.shape
+        if self._implementation == "triple":
+            out = None
+            if slot == O:
+                out = self.model.score_sp_cand(triples[:, S], triples[:, P], cand)
+            elif slot == S:
+                out = self.model.score_po_cand(triples[:, P], triples[:, O], cand)
+            if out is not None:
+                return out
+            t = triples.repeat(1, k).view(-1, 3)
+            t[:, slot] = cand.reshape(-1)
+            direction = "s" if slot == S else ("o" if slot == O else "p")
+            return self.model.score_spo(t[:, S], t[:, P], t[:, O], direction=direction).view(n, k)
+        if self._implementation == "all":
+            if slot == S:
+                allsc = self.model.score_po(triples[:, P], triples[:, O])
+            elif slot == P:
+                allsc = self.model.score_so(triples[:, S], triples[:, O])
+            else:
+                allsc = self.model.score_sp(triples[:, S], triples[:, P])
+            return torch.gather(allsc, 1, cand)
+        # batch
+        uniq, col = torch.unique(cand.reshape(-1), return_inverse=True)
+        if slot == S:
+            allsc = self.model.score_po(triples[:, P], triples[:, O], uniq)
+        elif slot == P:
+            allsc = self.model.score_so(triples[:, S], triples[:, O], uniq)
+        else:
+            allsc = self.model.score_sp(triples[:, S], triples[:, P], uniq)
+        return torch.gather(allsc, 1, col.view(n, k))
+
+    def _process_batch(self, batch_index, batch) -> TrainingJob._ProcessBatchResult:
+        prepare = -time.time()
+        triples = batch["triples"].to(self.device, non_blocking=True)
+        bs = len(triples)
+        negs = [self._sampler.sample(triples, slot) if self._sampler.num_samples[slot] > 0 else None
+                for slot in (S, P, O)]
+        prepare += time.time()
+        fwd = bwd = 0.0
+        total = torch.zeros((), device=self.device)
+        chunk = self._max_chunk_size if self._max_chunk_size > 0 else bs
+        labels = None
+        for c in range(math.ceil(bs / chunk)):
+            lo, hi = c * chunk, min(bs, (c + 1) * chunk)
+            tr = triples[lo:hi]
+            for slot in (S, P, O):
+                ns = self._sampler.num_samples[slot]
+                if ns <= 0:
+                    continue
+                if labels is None or labels.shape != (hi - lo, 1 + ns):
+                    labels = torch.zeros(hi - lo, 1 + ns, device=self.device)
+                    labels[:, 0] = 1.0
+                fwd -= time.time()
+                scores = self._scores(tr, slot, negs[slot][lo:hi])
+                loss = self.loss(scores, labels, num_negatives=ns) / bs
+                fwd += time.time()
+                bwd -= time.time()
+                loss.backward()
+                bwd += time.time()
+                total = total + loss.detach()
+        return TrainingJob._ProcessBatchResult(float(total.item()), bs, prepare, fwd, bwd)

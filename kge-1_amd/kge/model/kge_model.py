@@ -142,6 +142,15 @@ class RelationalScorer(KgeBase):
         return engine.score_all_xent(self.engine_kind, d, self.precision(), self.l_norm(), ent, e_idx, rel, p_idx,
                                      ent, None, labels, scale, l_ptr, smoothing)
 
+    def score_lookup_cand(self, ent: Tensor, rel: Tensor, e_idx: Tensor, p_idx: Tensor, direction: str,
+                          cand: Tensor) -> Tensor:
+        """[n, k]: query (ent[e_idx[i]], rel[p_idx[i]]) in direction "sp_" / "_po" against its
+        own candidates ent[cand[i, :]] (score_spo semantics; negative sampling)."""
+        from .. import engine, _lib
+
+        d = _lib.DIR_SP if direction == "sp_" else _lib.DIR_PO
+        return engine.score_cand(self.engine_kind, d, self.l_norm(), ent, e_idx, rel, p_idx, cand)
+
     def score_lookup_spo(self, ent: Tensor, rel: Tensor, s: Tensor, p: Tensor, o: Tensor) -> Tensor:
         from .. import engine
 
@@ -341,6 +350,22 @@ class KgeModel(KgeBase):
         if tabs is None:
             return None
         return self._scorer.score_lookup_xent(tabs[0], tabs[1], o, p, "_po", s, scale)
+
+    def score_sp_cand(self, s: Tensor, p: Tensor, cand: Tensor) -> Optional[Tensor]:
+        """[n, k] = score_spo(s_i, p_i, cand[i, c]) for every candidate object, without
+        building the n * k triples (negative sampling, train.py:868-892); None when the
+        fused path does not apply (the caller then expands triples for score_spo)."""
+        tabs = self._lookup_tables()
+        if tabs is None:
+            return None
+        return self._scorer.score_lookup_cand(tabs[0], tabs[1], s, p, "sp_", cand)
+
+    def score_po_cand(self, p: Tensor, o: Tensor, cand: Tensor) -> Optional[Tensor]:
+        """[n, k] = score_spo(cand[i, c], p_i, o_i) for every candidate subject."""
+        tabs = self._lookup_tables()
+        if tabs is None:
+            return None
+        return self._scorer.score_lookup_cand(tabs[0], tabs[1], o, p, "_po", cand)
 
     def score_sp_kl(self, s: Tensor, p: Tensor, l_ptr: Tensor, l_col: Tensor, smoothing: float,
                     scale: float) -> Optional[Tensor]:

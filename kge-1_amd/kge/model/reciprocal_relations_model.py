@@ -53,6 +53,14 @@ class ReciprocalRelationsModel(KgeModel):
         return self._scorer.score_lookup_xent(tabs[0], tabs[1], o, p + self.dataset.num_relations(), "sp_", s,
                                               scale)
 
+    def score_po_cand(self, p: Tensor, o: Tensor, cand: Tensor):
+        """score_spo(cand, p, o, direction="s") == score of (o, p + R, cand) as "sp_"
+        (reciprocal_relations_model.py:57-65)."""
+        tabs = self._lookup_tables()
+        if tabs is None:
+            return None
+        return self._scorer.score_lookup_cand(tabs[0], tabs[1], o, p + self.dataset.num_relations(), "sp_", cand)
+
     def score_po_kl(self, p: Tensor, o: Tensor, l_ptr: Tensor, l_col: Tensor, smoothing: float, scale: float):
         tabs = self._lookup_tables()
         if tabs is None:
