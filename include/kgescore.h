@@ -200,6 +200,24 @@ int kge_score_cand_bwd(int model, float l_norm, int dir, const float* q, int64_t
                        int64_t ldg, float* dq, int64_t lddq, float* d_ent, int64_t ld_dent,
                        void* stream);
 
+/* d_ent part of kge_score_cand_bwd without atomics, for candidate lists with many repeats:
+ * the caller groups the n*k pairs by entity -- order[] = the flattened pair indexes
+ * (i*k + c; cand contiguous [n][k]) sorted by cand value, seg_ptr[nseg+1] the group
+ * boundaries -- and each entity row is accumulated once (d_ent[e] += ..., plain RMW).
+ * Requires (d or d/2 for RotatE) % 4 == 0 and 16-B aligned rows (else KGE_ERR_ALIGN). */
+int kge_score_cand_bwd_ent(int model, float l_norm, int dir, const float* q, int64_t ldq,
+                           const float* ent, int64_t ld_ent, const int64_t* cand, int64_t n,
+                           int64_t k, int d, const int64_t* order, const int64_t* seg_ptr,
+                           int64_t nseg, const float* s, int64_t lds, const float* g, int64_t ldg,
+                           float* d_ent, int64_t ld_dent, void* stream);
+
+/* Counting-sort scatter: order[cursor[idx[t]]++] = t for t in [0, n) (int64 atomics on
+ * cursor; order within a bucket unspecified).  With cursor = the exclusive prefix sum of the
+ * bucket counts this groups t by idx[t] -- the order / seg_ptr input of
+ * kge_score_cand_bwd_ent. */
+int kge_bucket_scatter(const int64_t* idx, int64_t n, int64_t* cursor, int64_t* order,
+                       void* stream);
+
 /* ---- entity-ranking counts (eval) --------------------------------------------------
  * For row i of a score chunk S[n, m] covering entities [c0, c0 + m):
  *   v_j = S[i, j], with v_{true_i - c0} := true_score[i] when true_i is in the chunk;

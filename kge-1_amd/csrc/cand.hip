@@ -12,8 +12,14 @@
 // rows in flight) and reduces across the wave.  4*d bytes per scored triple; the FB15K-237
 // table (14,541 x 1024 x 4 = 59.6 MB) stays resident in the 256 MB MALL across rows.
 //
-// Backward: dq_i = sum_c g_ic d score / d q (per-wave partials in LDS, no atomics), and
-// d_ent[cand[i, c]] += g_ic d score / d e (fp32 atomics: candidates repeat across rows).
+// Backward (same gather shape, no atomics on the fast path):
+//   dq_i  = sum_c g_ic d score / d q   -- one workgroup per query row, each lane keeping
+//           its slice of the row in registers (all of a candidate row's loads in flight),
+//           waves reduced through LDS;
+//   d_ent = per entity e: sum over the (i, c) with cand[i, c] = e -- the caller groups the
+//           pairs by entity (kge_bucket_scatter), one wave per entity accumulates its row
+//           in registers and writes it once.
+// A scalar fallback (any d / alignment) scatters d_ent with fp32 atomics.
 #include <type_traits>
 
 #include "common.h"
@@ -24,6 +30,7 @@ constexpr int NT = 512, NW = NT / 64;
 enum { K_DOT = 0, K_TRANSE = 1, K_ROTATE = 2 };
 
 __device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
+__device__ __forceinline__ float4 f4(float v) { return make_float4(v, v, v, v); }
 
 // Per-element contribution to the reduction for (q, e) components.  For RotatE (re, im)
 // pairs are handled by the caller.
@@ -105,18 +112,191 @@ __global__ void __launch_bounds__(NT) cand_kernel(bool l1, float sigma, const fl
 }
 
 // ---------------------------------------------------------------------------- backward
+// g * d score / d q for one element (re part / both parts for RotatE); d score / d e is
+// its negative for the distance models and g * q for the dot models.
 template <int KIND>
-__global__ void __launch_bounds__(NT) cand_bwd_kernel(bool l1, float sigma, const float* __restrict__ q, int64_t ldq,
-                                                      const float* __restrict__ ent, int64_t ld_ent,
-                                                      const int64_t* __restrict__ cand, int64_t ldc, int k, int d,
-                                                      const float* __restrict__ s, int64_t lds,
-                                                      const float* __restrict__ g, int64_t ldg, float* dq,
-                                                      int64_t lddq, float* d_ent, int64_t ld_dent) {
-  extern __shared__ __attribute__((aligned(16))) float sh[];
-  float* qs = sh;               // d
-  float* part = sh + d;         // NW x d per-wave dq partials
+__device__ __forceinline__ void grad_q(bool l1, float sigma, float inv, float gc, float qr, float qi, float er,
+                                       float ei, float& gr, float& gi) {
+  if (KIND == K_DOT) {
+    gr = gc * er;
+  } else if (KIND == K_TRANSE) {  // score = -||diff||, diff = sigma (q - e) + eps
+    const float df = sigma * (qr - er) + 1e-6f;
+    const float dn = l1 ? (df > 0.f ? 1.f : (df < 0.f ? -1.f : 0.f)) : df * inv;
+    gr = -gc * sigma * dn;
+  } else {  // score = sum |q - e|_C or its L2 form
+    const float dr = qr - er, di = qi - ei;
+    float f = inv;
+    if (l1) {
+      const float a = sqrtf(fmaf(di, di, dr * dr));
+      f = a > 0.f ? 1.f / a : 0.f;
+    }
+    gr = gc * dr * f;
+    gi = gc * di * f;
+  }
+}
+
+// 1 / (L2 norm) of pair (i, c) from its forward score (TransE: -||.||, RotatE: +||.||)
+template <int KIND>
+__device__ __forceinline__ float inv_norm(bool l1, const float* s, int64_t idx) {
+  if (KIND == K_DOT || l1) return 0.f;
+  const float nrm = KIND == K_TRANSE ? -s[idx] : s[idx];
+  return nrm > 0.f ? 1.f / nrm : 0.f;
+}
+
+// dq, vectorised: lane owns elements ch*256 + lane*4 .. +3 (and the RotatE im parts)
+template <int KIND, int NCH>
+__global__ void __launch_bounds__(NT) cand_bwd_q_kernel(bool l1, float sigma, const float* __restrict__ q,
+                                                        int64_t ldq, const float* __restrict__ ent, int64_t ld_ent,
+                                                        const int64_t* __restrict__ cand, int64_t ldc, int k, int d,
+                                                        const float* __restrict__ s, int64_t lds,
+                                                        const float* __restrict__ g, int64_t ldg, float* __restrict__ dq,
+                                                        int64_t lddq) {
+  constexpr int P = KIND == K_ROTATE ? 2 : 1;  // float4 planes per chunk
+  extern __shared__ __attribute__((aligned(16))) float red[];  // NW x d
   const int64_t i = blockIdx.x;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int unit = KIND == K_ROTATE ? d / 2 : d;
+  const float* qi = q + i * ldq;
+  float4 qv[NCH][P], acc[NCH][P];
+#pragma unroll
+  for (int ch = 0; ch < NCH; ++ch) {
+    const int kk = min(ch * 256 + lane * 4, unit - 4);
+#pragma unroll
+    for (int pl = 0; pl < P; ++pl) {
+      qv[ch][pl] = ld4(qi + kk + pl * unit);
+      acc[ch][pl] = f4(0.f);
+    }
+  }
+  const int64_t* ci = cand + i * ldc;
+  for (int c = w; c < k; c += NW) {
+    const float gc = g[i * ldg + c];
+    if (gc == 0.f) continue;
+    const float inv = inv_norm<KIND>(l1, s, i * lds + c);
+    const float* e = ent + ci[c] * ld_ent;
+    float4 ev[NCH][P];
+#pragma unroll
+    for (int ch = 0; ch < NCH; ++ch)
+#pragma unroll
+      for (int pl = 0; pl < P; ++pl) ev[ch][pl] = ld4(e + min(ch * 256 + lane * 4, unit - 4) + pl * unit);
+#pragma unroll
+    for (int ch = 0; ch < NCH; ++ch) {
+      const float4 a = qv[ch][0], b = ev[ch][0];
+      const float4 ai = P > 1 ? qv[ch][P - 1] : a, bi = P > 1 ? ev[ch][P - 1] : b;
+      float gr[4], gi[4];
+      grad_q<KIND>(l1, sigma, inv, gc, a.x, ai.x, b.x, bi.x, gr[0], gi[0]);
+      grad_q<KIND>(l1, sigma, inv, gc, a.y, ai.y, b.y, bi.y, gr[1], gi[1]);
+      grad_q<KIND>(l1, sigma, inv, gc, a.z, ai.z, b.z, bi.z, gr[2], gi[2]);
+      grad_q<KIND>(l1, sigma, inv, gc, a.w, ai.w, b.w, bi.w, gr[3], gi[3]);
+      acc[ch][0].x += gr[0]; acc[ch][0].y += gr[1]; acc[ch][0].z += gr[2]; acc[ch][0].w += gr[3];
+      if (P > 1) {
+        acc[ch][P - 1].x += gi[0]; acc[ch][P - 1].y += gi[1]; acc[ch][P - 1].z += gi[2]; acc[ch][P - 1].w += gi[3];
+      }
+    }
+  }
+  // cross-wave reduction through LDS (each wave's partial row), then one store of dq_i
+#pragma unroll
+  for (int ch = 0; ch < NCH; ++ch) {
+    const int kk = ch * 256 + lane * 4;
+    if (kk < unit)
+#pragma unroll
+      for (int pl = 0; pl < P; ++pl) *reinterpret_cast<float4*>(red + w * d + kk + pl * unit) = acc[ch][pl];
+  }
+  __syncthreads();
+  for (int t = threadIdx.x; t < d; t += NT) {
+    float v = 0.f;
+#pragma unroll
+    for (int u = 0; u < NW; ++u) v += red[u * d + t];
+    dq[i * lddq + t] = v;
+  }
+}
+
+// d_ent, vectorised, one wave per entity group (pairs of order[seg_ptr[u] .. seg_ptr[u+1]))
+template <int KIND, int NCH>
+__global__ void __launch_bounds__(256) cand_bwd_ent_kernel(bool l1, float sigma, const float* __restrict__ q,
+                                                           int64_t ldq, const float* __restrict__ ent,
+                                                           int64_t ld_ent, const int64_t* __restrict__ cand, int k,
+                                                           const int64_t* __restrict__ order,
+                                                           const int64_t* __restrict__ seg_ptr, int64_t nseg, int d,
+                                                           const float* __restrict__ s, int64_t lds,
+                                                           const float* __restrict__ g, int64_t ldg, float* d_ent,
+                                                           int64_t ld_dent) {
+  constexpr int P = KIND == K_ROTATE ? 2 : 1;
+  const int lane = threadIdx.x & 63;
+  const int64_t u = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (u >= nseg) return;
+  const int64_t p0 = seg_ptr[u], p1 = seg_ptr[u + 1];
+  if (p0 >= p1) return;  // entity without pairs (seg_ptr may have one slot per entity)
+  const int64_t row = cand[order[p0]];  // order indexes the flattened [n, k] candidate matrix
+  const int unit = KIND == K_ROTATE ? d / 2 : d;
+  const float* e = ent + row * ld_ent;
+  float4 ev[NCH][P], acc[NCH][P];
+#pragma unroll
+  for (int ch = 0; ch < NCH; ++ch)
+#pragma unroll
+    for (int pl = 0; pl < P; ++pl) {
+      ev[ch][pl] = ld4(e + min(ch * 256 + lane * 4, unit - 4) + pl * unit);
+      acc[ch][pl] = f4(0.f);
+    }
+  for (int64_t t = p0; t < p1; ++t) {
+    const int64_t pair = order[t];
+    const int64_t i = pair / k, c = pair - i * k;
+    const float gc = g[i * ldg + c];
+    if (gc == 0.f) continue;
+    const float inv = inv_norm<KIND>(l1, s, i * lds + c);
+    const float* qi = q + i * ldq;
+    float4 qv[NCH][P];
+#pragma unroll
+    for (int ch = 0; ch < NCH; ++ch)
+#pragma unroll
+      for (int pl = 0; pl < P; ++pl) qv[ch][pl] = ld4(qi + min(ch * 256 + lane * 4, unit - 4) + pl * unit);
+#pragma unroll
+    for (int ch = 0; ch < NCH; ++ch) {
+      const float4 a = qv[ch][0], b = ev[ch][0];
+      const float4 ai = P > 1 ? qv[ch][P - 1] : a, bi = P > 1 ? ev[ch][P - 1] : b;
+      if (KIND == K_DOT) {  // d score / d e = q
+        acc[ch][0].x += gc * a.x; acc[ch][0].y += gc * a.y; acc[ch][0].z += gc * a.z; acc[ch][0].w += gc * a.w;
+      } else {  // d score / d e = -(d score / d q)
+        float gr[4], gi[4];
+        grad_q<KIND>(l1, sigma, inv, gc, a.x, ai.x, b.x, bi.x, gr[0], gi[0]);
+        grad_q<KIND>(l1, sigma, inv, gc, a.y, ai.y, b.y, bi.y, gr[1], gi[1]);
+        grad_q<KIND>(l1, sigma, inv, gc, a.z, ai.z, b.z, bi.z, gr[2], gi[2]);
+        grad_q<KIND>(l1, sigma, inv, gc, a.w, ai.w, b.w, bi.w, gr[3], gi[3]);
+        acc[ch][0].x -= gr[0]; acc[ch][0].y -= gr[1]; acc[ch][0].z -= gr[2]; acc[ch][0].w -= gr[3];
+        if (P > 1) {
+          acc[ch][P - 1].x -= gi[0]; acc[ch][P - 1].y -= gi[1]; acc[ch][P - 1].z -= gi[2]; acc[ch][P - 1].w -= gi[3];
+        }
+      }
+    }
+  }
+  float* de = d_ent + row * ld_dent;
+#pragma unroll
+  for (int ch = 0; ch < NCH; ++ch) {
+    const int kk = ch * 256 + lane * 4;
+    if (kk >= unit) continue;
+#pragma unroll
+    for (int pl = 0; pl < P; ++pl) {
+      float4* p = reinterpret_cast<float4*>(de + kk + pl * unit);
+      float4 v = *p;
+      v.x += acc[ch][pl].x; v.y += acc[ch][pl].y; v.z += acc[ch][pl].z; v.w += acc[ch][pl].w;
+      *p = v;
+    }
+  }
+}
+
+// scalar fallback (any d, any alignment): dq through per-wave LDS partials, d_ent atomics
+template <int KIND>
+__global__ void __launch_bounds__(NT) cand_bwd_scalar_kernel(bool l1, float sigma, const float* __restrict__ q,
+                                                             int64_t ldq, const float* __restrict__ ent,
+                                                             int64_t ld_ent, const int64_t* __restrict__ cand,
+                                                             int64_t ldc, int k, int d, const float* __restrict__ s,
+                                                             int64_t lds, const float* __restrict__ g, int64_t ldg,
+                                                             float* dq, int64_t lddq, float* d_ent, int64_t ld_dent) {
+  extern __shared__ __attribute__((aligned(16))) float sh[];
+  float* qs = sh;        // d
+  float* part = sh + d;  // NW x d per-wave dq partials
+  const int64_t i = blockIdx.x;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int unit = KIND == K_ROTATE ? d / 2 : d;
   for (int t = threadIdx.x; t < d; t += NT) qs[t] = q[i * ldq + t];
   for (int t = threadIdx.x; t < NW * d; t += NT) part[t] = 0.f;
   __syncthreads();
@@ -125,47 +305,19 @@ __global__ void __launch_bounds__(NT) cand_bwd_kernel(bool l1, float sigma, cons
   for (int c = w; c < k; c += NW) {
     const float gc = g[i * ldg + c];
     if (gc == 0.f) continue;
+    const float inv = inv_norm<KIND>(l1, s, i * lds + c);
     const int64_t row = ci[c];
     const float* e = ent + row * ld_ent;
     float* de = d_ent ? d_ent + row * ld_dent : nullptr;
-    if (KIND == K_DOT) {
-      for (int t = lane; t < d; t += 64) {
-        pw[t] += gc * e[t];
-        if (de) atomicAdd(de + t, gc * qs[t]);
-      }
-    } else if (KIND == K_TRANSE) {
-      // score = -||diff||, diff = sigma (q - e) + eps;  d/dq = -sigma * dnorm/ddiff
-      const float nrm = -s[i * lds + c];  // L2 norm from the forward score
-      const float inv = (!l1 && nrm > 0.f) ? 1.f / nrm : 0.f;
-      for (int t = lane; t < d; t += 64) {
-        const float df = sigma * (qs[t] - e[t]) + 1e-6f;
-        const float dn = l1 ? (df > 0.f ? 1.f : (df < 0.f ? -1.f : 0.f)) : df * inv;
-        const float gq = -gc * sigma * dn;
-        pw[t] += gq;
-        if (de) atomicAdd(de + t, -gq);
-      }
-    } else {  // RotatE: score = sum |q - e|_C (L1) or sqrt(sum |q - e|^2) (L2)
-      const int h = d / 2;
-      const float nrm = s[i * lds + c];
-      const float inv = (!l1 && nrm > 0.f) ? 1.f / nrm : 0.f;
-      for (int t = lane; t < h; t += 64) {
-        const float dr = qs[t] - e[t], di = qs[t + h] - e[t + h];
-        float sr, si;
-        if (l1) {
-          const float a = sqrtf(fmaf(di, di, dr * dr));
-          const float ia = a > 0.f ? 1.f / a : 0.f;
-          sr = dr * ia;
-          si = di * ia;
-        } else {
-          sr = dr * inv;
-          si = di * inv;
-        }
-        pw[t] += gc * sr;
-        pw[t + h] += gc * si;
-        if (de) {
-          atomicAdd(de + t, -gc * sr);
-          atomicAdd(de + t + h, -gc * si);
-        }
+    for (int t = lane; t < unit; t += 64) {
+      const float qi = KIND == K_ROTATE ? qs[t + unit] : 0.f, ei = KIND == K_ROTATE ? e[t + unit] : 0.f;
+      float gr = 0.f, gi = 0.f;
+      grad_q<KIND>(l1, sigma, inv, gc, qs[t], qi, e[t], ei, gr, gi);
+      pw[t] += gr;
+      if (KIND == K_ROTATE) pw[t + unit] += gi;
+      if (de) {
+        atomicAdd(de + t, KIND == K_DOT ? gc * qs[t] : -gr);
+        if (KIND == K_ROTATE) atomicAdd(de + t + unit, -gi);
       }
     }
   }
@@ -180,6 +332,13 @@ __global__ void __launch_bounds__(NT) cand_bwd_kernel(bool l1, float sigma, cons
   }
 }
 
+__global__ void bucket_scatter_kernel(const int64_t* __restrict__ idx, int64_t n, int64_t* cursor,
+                                      int64_t* __restrict__ order) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= n) return;
+  order[atomicAdd(reinterpret_cast<unsigned long long*>(cursor + idx[t]), 1ull)] = t;
+}
+
 int kind_of(int model) {
   switch (model) {
     case KGE_COMPLEX:
@@ -190,6 +349,43 @@ int kind_of(int model) {
     default: return -1;
   }
 }
+
+// chunks of 256 elements per lane row slice: 1, 2, 4 or 8 (unit <= 2048); 0 = unsupported
+int nch_of(int unit) {
+  const int c = (unit + 255) / 256;
+  return c <= 1 ? 1 : c <= 2 ? 2 : c <= 4 ? 4 : c <= 8 ? 8 : 0;
+}
+
+template <template <int, int> class F, int KIND, typename... A>
+void dispatch_nch(int nch, A&&... a) {
+  switch (nch) {
+    case 1: F<KIND, 1>::run(a...); break;
+    case 2: F<KIND, 2>::run(a...); break;
+    case 4: F<KIND, 4>::run(a...); break;
+    default: F<KIND, 8>::run(a...); break;
+  }
+}
+
+template <int KIND, int NCH>
+struct LaunchQ {
+  static void run(dim3 grid, size_t sh, hipStream_t st, bool l1, float sigma, const float* q, int64_t ldq,
+                  const float* ent, int64_t ld_ent, const int64_t* cand, int64_t ldc, int k, int d, const float* s,
+                  int64_t lds, const float* g, int64_t ldg, float* dq, int64_t lddq) {
+    cand_bwd_q_kernel<KIND, NCH><<<grid, dim3(NT), sh, st>>>(l1, sigma, q, ldq, ent, ld_ent, cand, ldc, k, d, s, lds,
+                                                             g, ldg, dq, lddq);
+  }
+};
+
+template <int KIND, int NCH>
+struct LaunchE {
+  static void run(dim3 grid, hipStream_t st, bool l1, float sigma, const float* q, int64_t ldq, const float* ent,
+                  int64_t ld_ent, const int64_t* cand, int k, const int64_t* order, const int64_t* seg_ptr,
+                  int64_t nseg, int d, const float* s, int64_t lds, const float* g, int64_t ldg, float* d_ent,
+                  int64_t ld_dent) {
+    cand_bwd_ent_kernel<KIND, NCH><<<grid, dim3(256), 0, st>>>(l1, sigma, q, ldq, ent, ld_ent, cand, k, order,
+                                                               seg_ptr, nseg, d, s, lds, g, ldg, d_ent, ld_dent);
+  }
+};
 
 }  // namespace
 
@@ -238,30 +434,89 @@ extern "C" int kge_score_cand_bwd(int model, float l_norm, int dir, const float*
   KGE_REQUIRE(!d_ent || ld_dent >= d);
   KGE_REQUIRE(kind == K_DOT || (s && lds >= k));
   KGE_REQUIRE(kind != K_ROTATE || d % 2 == 0);
-  if (n == 0) return 0;
+  if (n == 0 || (!dq && !d_ent)) return 0;
   hipStream_t st = as_stream(stream);
   const bool l1 = l_norm == 1.f;
   const float sigma = dir == KGE_DIR_SP ? 1.f : -1.f;
+  const int unit = kind == K_ROTATE ? d / 2 : d;
+  const int nch = nch_of(unit);
+  const dim3 grid((unsigned)n);
+  if (!d_ent && nch && unit % 4 == 0 && ldq % 4 == 0 && ld_ent % 4 == 0 && aligned16(q) && aligned16(ent)) {
+    const size_t sh = (size_t)NW * d * sizeof(float);
+    if (kind == K_DOT)
+      dispatch_nch<LaunchQ, K_DOT>(nch, grid, sh, st, l1, sigma, q, ldq, ent, ld_ent, cand, ldc, (int)k, d, s, lds, g,
+                                   ldg, dq, lddq);
+    else if (kind == K_TRANSE)
+      dispatch_nch<LaunchQ, K_TRANSE>(nch, grid, sh, st, l1, sigma, q, ldq, ent, ld_ent, cand, ldc, (int)k, d, s, lds,
+                                      g, ldg, dq, lddq);
+    else
+      dispatch_nch<LaunchQ, K_ROTATE>(nch, grid, sh, st, l1, sigma, q, ldq, ent, ld_ent, cand, ldc, (int)k, d, s, lds,
+                                      g, ldg, dq, lddq);
+    KGE_CHECK_LAUNCH();
+    return 0;
+  }
   const size_t sh = (size_t)(1 + NW) * d * sizeof(float);
   static bool attr = false;
   if (!attr) {
-    for (const void* f : {(const void*)cand_bwd_kernel<K_DOT>, (const void*)cand_bwd_kernel<K_TRANSE>,
-                          (const void*)cand_bwd_kernel<K_ROTATE>}) {
+    for (const void* f : {(const void*)cand_bwd_scalar_kernel<K_DOT>, (const void*)cand_bwd_scalar_kernel<K_TRANSE>,
+                          (const void*)cand_bwd_scalar_kernel<K_ROTATE>}) {
       hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (1 + NW) * 3584 * 4);
       if (e != hipSuccess) return (int)e;
     }
     attr = true;
   }
-  const dim3 grid((unsigned)n), block(NT);
   if (kind == K_DOT)
-    cand_bwd_kernel<K_DOT><<<grid, block, sh, st>>>(l1, sigma, q, ldq, ent, ld_ent, cand, ldc, (int)k, d, s, lds, g,
-                                                    ldg, dq, lddq, d_ent, ld_dent);
+    cand_bwd_scalar_kernel<K_DOT><<<grid, dim3(NT), sh, st>>>(l1, sigma, q, ldq, ent, ld_ent, cand, ldc, (int)k, d, s,
+                                                              lds, g, ldg, dq, lddq, d_ent, ld_dent);
   else if (kind == K_TRANSE)
-    cand_bwd_kernel<K_TRANSE><<<grid, block, sh, st>>>(l1, sigma, q, ldq, ent, ld_ent, cand, ldc, (int)k, d, s, lds,
-                                                       g, ldg, dq, lddq, d_ent, ld_dent);
+    cand_bwd_scalar_kernel<K_TRANSE><<<grid, dim3(NT), sh, st>>>(l1, sigma, q, ldq, ent, ld_ent, cand, ldc, (int)k, d,
+                                                                 s, lds, g, ldg, dq, lddq, d_ent, ld_dent);
   else
-    cand_bwd_kernel<K_ROTATE><<<grid, block, sh, st>>>(l1, sigma, q, ldq, ent, ld_ent, cand, ldc, (int)k, d, s, lds,
-                                                       g, ldg, dq, lddq, d_ent, ld_dent);
+    cand_bwd_scalar_kernel<K_ROTATE><<<grid, dim3(NT), sh, st>>>(l1, sigma, q, ldq, ent, ld_ent, cand, ldc, (int)k, d,
+                                                                 s, lds, g, ldg, dq, lddq, d_ent, ld_dent);
+  KGE_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int kge_score_cand_bwd_ent(int model, float l_norm, int dir, const float* q, int64_t ldq,
+                                      const float* ent, int64_t ld_ent, const int64_t* cand, int64_t n, int64_t k,
+                                      int d, const int64_t* order, const int64_t* seg_ptr, int64_t nseg,
+                                      const float* s, int64_t lds, const float* g, int64_t ldg, float* d_ent,
+                                      int64_t ld_dent, void* stream) {
+  const int kind = kind_of(model);
+  KGE_REQUIRE(kind >= 0 && (dir == KGE_DIR_SP || dir == KGE_DIR_PO) && (l_norm == 1.f || l_norm == 2.f));
+  KGE_REQUIRE(n >= 0 && k > 0 && d > 0 && nseg >= 0 && n * k < (1LL << 62));
+  KGE_REQUIRE(q && ent && cand && order && seg_ptr && g && d_ent && ldq >= d && ld_ent >= d && ldg >= k &&
+              ld_dent >= d);
+  KGE_REQUIRE(kind == K_DOT || (s && lds >= k));
+  KGE_REQUIRE(kind != K_ROTATE || d % 2 == 0);
+  const int unit = kind == K_ROTATE ? d / 2 : d;
+  const int nch = nch_of(unit);
+  if (!nch || unit % 4 != 0 || ldq % 4 != 0 || ld_ent % 4 != 0 || ld_dent % 4 != 0 || !aligned16(q) ||
+      !aligned16(ent) || !aligned16(d_ent))
+    return KGE_ERR_ALIGN;
+  if (nseg == 0) return 0;
+  hipStream_t st = as_stream(stream);
+  const bool l1 = l_norm == 1.f;
+  const float sigma = dir == KGE_DIR_SP ? 1.f : -1.f;
+  const dim3 grid((unsigned)((nseg + 3) / 4));
+  if (kind == K_DOT)
+    dispatch_nch<LaunchE, K_DOT>(nch, grid, st, l1, sigma, q, ldq, ent, ld_ent, cand, (int)k, order, seg_ptr, nseg, d,
+                                 s, lds, g, ldg, d_ent, ld_dent);
+  else if (kind == K_TRANSE)
+    dispatch_nch<LaunchE, K_TRANSE>(nch, grid, st, l1, sigma, q, ldq, ent, ld_ent, cand, (int)k, order, seg_ptr, nseg,
+                                    d, s, lds, g, ldg, d_ent, ld_dent);
+  else
+    dispatch_nch<LaunchE, K_ROTATE>(nch, grid, st, l1, sigma, q, ldq, ent, ld_ent, cand, (int)k, order, seg_ptr, nseg,
+                                    d, s, lds, g, ldg, d_ent, ld_dent);
+  KGE_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int kge_bucket_scatter(const int64_t* idx, int64_t n, int64_t* cursor, int64_t* order, void* stream) {
+  KGE_REQUIRE(n >= 0 && (n == 0 || (idx && cursor && order)));
+  if (n == 0) return 0;
+  bucket_scatter_kernel<<<dim3((unsigned)((n + 255) / 256)), dim3(256), 0, as_stream(stream)>>>(idx, n, cursor, order);
   KGE_CHECK_LAUNCH();
   return 0;
 }

@@ -53,6 +53,9 @@ SIGNATURES = {
     "kge_score_cand": ([_I, _F, _I, _P, _I64, _P, _I64, _P, _I64, _I64, _I64, _I, _P, _I64, _P], _I),
     "kge_score_cand_bwd": ([_I, _F, _I, _P, _I64, _P, _I64, _P, _I64, _I64, _I64, _I, _P, _I64, _P, _I64, _P,
                             _I64, _P, _I64, _P], _I),
+    "kge_score_cand_bwd_ent": ([_I, _F, _I, _P, _I64, _P, _I64, _P, _I64, _I64, _I, _P, _P, _I64, _P, _I64, _P,
+                                _I64, _P, _I64, _P], _I),
+    "kge_bucket_scatter": ([_P, _I64, _P, _P, _P], _I),
 }
 
 _lib: Optional[ctypes.CDLL] = None
@@ -344,6 +347,31 @@ def score_cand_bwd(model, l_norm, direction, q, ent, cand, s, g, dq, d_ent):
                                     ptr(cand), cand.stride(0), n, k, d, ptr(s), rows(s) if s is not None else 0,
                                     ptr(g), rows(g), ptr(dq), rows(dq) if dq is not None else 0, ptr(d_ent),
                                     rows(d_ent) if d_ent is not None else 0, stream()), "kge_score_cand_bwd")
+
+
+def score_cand_bwd_ent(model, l_norm, direction, q, ent, cand, s, g, d_ent) -> bool:
+    """d_ent += d(sum g * scores)/d ent without fp32 atomics: the n*k pairs are grouped by
+    entity with a counting sort (bincount, exclusive scan, kge_bucket_scatter) -- one group
+    slot per entity, fixed size, no host sync -- and each entity row is reduced once.
+    Returns False (nothing done) when the layout is not supported."""
+    unit = q.shape[1] // 2 if model == ROTATE else q.shape[1]
+    if unit % 4 or unit > 2048 or rows(q) % 4 or rows(ent) % 4 or rows(d_ent) % 4 or q.data_ptr() % 16 \
+            or ent.data_ptr() % 16 or d_ent.data_ptr() % 16:
+        return False
+    cand = cand.long().contiguous()
+    n, k = cand.shape
+    flat = cand.reshape(-1)
+    E = ent.shape[0]
+    seg_ptr = torch.zeros(E + 1, dtype=torch.int64, device=cand.device)
+    torch.cumsum(torch.bincount(flat, minlength=E), 0, out=seg_ptr[1:])
+    cursor = seg_ptr[:-1].clone()
+    order = torch.empty_like(flat)
+    _check(lib().kge_bucket_scatter(ptr(flat), flat.numel(), ptr(cursor), ptr(order), stream()), "kge_bucket_scatter")
+    _check(lib().kge_score_cand_bwd_ent(model, float(l_norm), direction, ptr(q), rows(q), ptr(ent), rows(ent),
+                                        ptr(cand), n, k, q.shape[1], ptr(order), ptr(seg_ptr), ent.shape[0], ptr(s),
+                                        rows(s) if s is not None else 0, ptr(g), rows(g), ptr(d_ent), rows(d_ent),
+                                        stream()), "kge_score_cand_bwd_ent")
+    return True
 
 
 def softmax_kl(s, l_ptr, l_col, smoothing, scale, g=None, loss=None):

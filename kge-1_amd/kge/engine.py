@@ -223,7 +223,10 @@ class _ScoreCand(torch.autograd.Function):
         d_ent = torch.zeros_like(ent) if need_ent else None
         d_rel = torch.zeros_like(rel) if need_rel else None
         dq = torch.empty_like(q) if (need_ent or need_rel) else None
-        L.score_cand_bwd(kind, l_norm, direction, q, ent, cand, s, _rows(g.float()), dq, d_ent)
+        g = _rows(g.float())
+        # candidate rows repeat across queries: grouped per entity (sort) instead of atomics
+        ent_done = d_ent is not None and L.score_cand_bwd_ent(kind, l_norm, direction, q, ent, cand, s, g, d_ent)
+        L.score_cand_bwd(kind, l_norm, direction, q, ent, cand, s, g, dq, None if ent_done else d_ent)
         if dq is not None:
             L.prep_query_bwd(kind, direction, ent, eidx, rel, ridx, n, d_e, d_r, dq, d_ent, d_rel)
         return None, None, None, d_ent, None, d_rel, None, None
