@@ -177,6 +177,21 @@ int kge_softmax_kl(const float* s, int64_t lds, int64_t n, int64_t m, const int6
                    const int64_t* l_col, float smoothing, float scale, float* loss, float* g,
                    int64_t ldg, void* stream);
 
+/* Vocab-parallel 1vsAll (entity table row-sharded): S holds columns
+ * [c0, c0 + m) of the full score rows, labels are global column ids.
+ * row_stats: row_max[i], row_sumexp[i] = sum_j exp(S[i, j] - row_max[i]) over the slice, and
+ *            target[i] = S[i, labels[i] - c0] when the label is in the slice, else 0
+ *            (target may be NULL) -- reduce across shards (MAX; rescaled SUM; SUM) to get
+ *            lse_i and the target score.
+ * grad     : g[i, j] = scale * (exp(S[i, j] - lse[i]) - [j + c0 == labels[i]])  (labels may
+ *            be NULL: no one-hot term; g may alias s with ldg == lds). */
+int kge_softmax_row_stats(const float* s, int64_t lds, int64_t n, int64_t m, int64_t c0,
+                          const int64_t* labels, float* row_max, float* row_sumexp, float* target,
+                          void* stream);
+int kge_softmax_grad(const float* s, int64_t lds, int64_t n, int64_t m, int64_t c0,
+                     const int64_t* labels, const float* lse, float scale, float* g, int64_t ldg,
+                     void* stream);
+
 /* ---- per-row candidate lists (negative sampling) -------------------------------------
  * out[i, c] = score(Q[i, :], ent[cand[i, c], :])  i in [0, n), c in [0, k), with the
  * semantics of KgeModel.score_spo on the triple the candidate completes (kge_model.py:620-637):

@@ -13,6 +13,10 @@
 // Index labels (1vsAll, KLDivWithSoftmaxKgeLoss -> CrossEntropyLoss, loss.py:198-208) are
 // the case |P_i| = 1, eps = 0: loss_i = lse_i - S_i,label, G = scale (softmax - onehot).
 //
+// Column-sharded rows (vocab-parallel 1vsAll over the row-sharded entity table):
+// kge_softmax_row_stats gives each shard's (max, sum exp(x - max), target score) for the
+// cross-shard reduction, kge_softmax_grad the shard's slice of G from the global lse.
+//
 // HBM-bound: one workgroup per row reads the row once for the online (max, sum-exp, sum),
 // then again (L2 / MALL-resident: 4m bytes just touched) to write G, which may alias S.
 // exp is v_exp_f32 (__expf): relative error ~|x| * 6e-8 for exp(x), x = score - max <= 0,
@@ -34,34 +38,15 @@ __device__ __forceinline__ void lse_merge(float& m, float& s, float m2, float s2
 
 __device__ __forceinline__ float xlogx(float x) { return x > 0.f ? x * logf(x) : 0.f; }
 
-// l_ptr == NULL: index labels, P_i = {l_col[i]}
+// Block-wide online (max, sum exp(x - max), sum x) of row sr[0, m); every thread returns
+// the block totals.  red: 3 x (NT / 64) floats of LDS.
 template <bool VEC>
-__global__ void __launch_bounds__(NT) softmax_kl_kernel(const float* s, int64_t lds, int m,
-                                                        const int64_t* __restrict__ l_ptr,
-                                                        const int64_t* __restrict__ l_col, float eps, float scale,
-                                                        float* __restrict__ loss, float* g, int64_t ldg) {
-  __shared__ float red[3][NT / 64];
-  const int64_t row = blockIdx.x;
-  const float* sr = s + row * lds;
+__device__ __forceinline__ void row_stats(const float* sr, int m, float (&red)[3][NT / 64], float& mx, float& sm,
+                                          float& rs) {
   const int tid = threadIdx.x;
-  const int64_t p0 = l_ptr ? l_ptr[row] : row, p1 = l_ptr ? l_ptr[row + 1] : row + 1;
-
-  // pass 1: online (max, sum exp(x - max)), row sum, and the positives' scores -- all read
-  // before the reduction barrier, i.e. before any thread overwrites the row (g may alias s)
-  float mx = -INFINITY, sm = 0.f, rs = 0.f, ps = 0.f;
-  for (int64_t k = p0 + tid; k < p1; k += NT) {
-    const int64_t c = l_col[k];
-    ps += (c >= 0 && c < m) ? sr[c] : NAN;  // a label outside the row poisons the loss
-  }
-  auto take = [&](float v) {
-    rs += v;
-    if (v > mx) {
-      sm = sm * __expf(mx - v) + 1.f;
-      mx = v;
-    } else if (v != -INFINITY) {  // -inf adds 0 (and would be NaN while mx is -inf)
-      sm += __expf(v - mx);
-    }
-  };
+  mx = -INFINITY;
+  sm = 0.f;
+  rs = 0.f;
   int j0 = 0;
   if (VEC) {
     // U float4 loads in flight per thread before any is consumed: the running (max, sum)
@@ -88,14 +73,22 @@ __global__ void __launch_bounds__(NT) softmax_kl_kernel(const float* s, int64_t 
     }
     j0 = m4;
   }
-  for (int j = j0 + tid; j < m; j += NT) take(sr[j]);
+  for (int j = j0 + tid; j < m; j += NT) {
+    const float v = sr[j];
+    rs += v;
+    if (v > mx) {
+      sm = sm * __expf(mx - v) + 1.f;
+      mx = v;
+    } else if (v != -INFINITY) {  // -inf adds 0 (and would be NaN while mx is -inf)
+      sm += __expf(v - mx);
+    }
+  }
   // NaN anywhere in the row: fmaxf drops NaN from the max but exp(NaN) poisons the sum
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) {
     const float m2 = __shfl_xor(mx, off, 64), s2 = __shfl_xor(sm, off, 64);
     lse_merge(mx, sm, m2, s2);
     rs += __shfl_xor(rs, off, 64);
-    ps += __shfl_xor(ps, off, 64);
   }
   if ((tid & 63) == 0) {
     red[0][tid >> 6] = mx;
@@ -111,12 +104,69 @@ __global__ void __launch_bounds__(NT) softmax_kl_kernel(const float* s, int64_t 
     lse_merge(mx, sm, red[0][w], red[1][w]);
     rs += red[2][w];
   }
-  __syncthreads();
-  if ((tid & 63) == 0) red[0][tid >> 6] = ps;
-  __syncthreads();
-  ps = red[0][0];
+  __syncthreads();  // red is reused by the caller
+}
+
+// gr[j] = a * exp(sr[j] - lse) - b for j in [0, m); gr may alias sr (read before write per element)
+template <bool VEC>
+__device__ __forceinline__ void row_grad(const float* sr, float* gr, int m, float lse, float a, float b) {
+  const int tid = threadIdx.x;
+  int j0 = 0;
+  if (VEC) {
+    const int m4 = m & ~3;
+    for (int base = 0; base < m4; base += NT * 4 * U) {
+      float4 v[U];
 #pragma unroll
-  for (int w = 1; w < NT / 64; ++w) ps += red[0][w];
+      for (int q = 0; q < U; ++q) v[q] = *reinterpret_cast<const float4*>(sr + min(base + (q * NT + tid) * 4, m4 - 4));
+#pragma unroll
+      for (int q = 0; q < U; ++q) {
+        const int j = base + (q * NT + tid) * 4;
+        if (j < m4)
+          *reinterpret_cast<float4*>(gr + j) =
+              make_float4(a * __expf(v[q].x - lse) - b, a * __expf(v[q].y - lse) - b, a * __expf(v[q].z - lse) - b,
+                          a * __expf(v[q].w - lse) - b);
+      }
+    }
+    j0 = m4;
+  }
+  for (int j = j0 + tid; j < m; j += NT) gr[j] = a * __expf(sr[j] - lse) - b;
+}
+
+__device__ __forceinline__ float block_sum(float v, float* red) {
+  const int tid = threadIdx.x;
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+  if ((tid & 63) == 0) red[tid >> 6] = v;
+  __syncthreads();
+  float t = red[0];
+#pragma unroll
+  for (int w = 1; w < NT / 64; ++w) t += red[w];
+  __syncthreads();
+  return t;
+}
+
+// l_ptr == NULL: index labels, P_i = {l_col[i]}
+template <bool VEC>
+__global__ void __launch_bounds__(NT) softmax_kl_kernel(const float* s, int64_t lds, int m,
+                                                        const int64_t* __restrict__ l_ptr,
+                                                        const int64_t* __restrict__ l_col, float eps, float scale,
+                                                        float* __restrict__ loss, float* g, int64_t ldg) {
+  __shared__ float red[3][NT / 64];
+  const int64_t row = blockIdx.x;
+  const float* sr = s + row * lds;
+  const int tid = threadIdx.x;
+  const int64_t p0 = l_ptr ? l_ptr[row] : row, p1 = l_ptr ? l_ptr[row + 1] : row + 1;
+
+  // positives' scores and the row statistics are read before the first barrier inside
+  // row_stats, i.e. before any thread overwrites the row (g may alias s)
+  float ps = 0.f;
+  for (int64_t k = p0 + tid; k < p1; k += NT) {
+    const int64_t c = l_col[k];
+    ps += (c >= 0 && c < m) ? sr[c] : NAN;  // a label outside the row poisons the loss
+  }
+  float mx, sm, rs;
+  row_stats<VEC>(sr, m, red, mx, sm, rs);
+  ps = block_sum(ps, red[0]);
 
   const float lse = mx + __logf(sm);
   const int64_t np = p1 - p0;
@@ -137,24 +187,7 @@ __global__ void __launch_bounds__(NT) softmax_kl_kernel(const float* s, int64_t 
 
   // pass 2: G = scale * (T softmax - t0), then positives -= scale * (t1 - t0)
   float* gr = g + row * ldg;
-  const float a = scale * T, b = scale * t0;
-  if (VEC) {
-    const int m4 = m & ~3;
-    for (int base = 0; base < m4; base += NT * 4 * U) {
-      float4 v[U];
-#pragma unroll
-      for (int q = 0; q < U; ++q) v[q] = *reinterpret_cast<const float4*>(sr + min(base + (q * NT + tid) * 4, m4 - 4));
-#pragma unroll
-      for (int q = 0; q < U; ++q) {
-        const int j = base + (q * NT + tid) * 4;
-        if (j < m4)
-          *reinterpret_cast<float4*>(gr + j) =
-              make_float4(a * __expf(v[q].x - lse) - b, a * __expf(v[q].y - lse) - b, a * __expf(v[q].z - lse) - b,
-                          a * __expf(v[q].w - lse) - b);
-      }
-    }
-  }
-  for (int j = j0 + tid; j < m; j += NT) gr[j] = a * __expf(sr[j] - lse) - b;
+  row_grad<VEC>(sr, gr, m, lse, scale * T, scale * t0);
   __syncthreads();  // every write of the row is ordered before the positives' fix-up
   const float d = scale * (t1 - t0);
   for (int64_t k = p0 + tid; k < p1; k += NT) {
@@ -163,10 +196,48 @@ __global__ void __launch_bounds__(NT) softmax_kl_kernel(const float* s, int64_t 
   }
 }
 
+// column slice [c0, c0 + m) of rows whose labels are global column ids
+template <bool VEC>
+__global__ void __launch_bounds__(NT) row_stats_kernel(const float* __restrict__ s, int64_t lds, int m, int64_t c0,
+                                                       const int64_t* __restrict__ labels, float* __restrict__ mx_out,
+                                                       float* __restrict__ sm_out, float* __restrict__ tg_out) {
+  __shared__ float red[3][NT / 64];
+  const int64_t row = blockIdx.x;
+  const float* sr = s + row * lds;
+  float mx, sm, rs;
+  row_stats<VEC>(sr, m, red, mx, sm, rs);
+  if (threadIdx.x == 0) {
+    mx_out[row] = mx;
+    sm_out[row] = sm;
+    if (tg_out) {
+      const int64_t c = labels[row] - c0;
+      tg_out[row] = (c >= 0 && c < m) ? sr[c] : 0.f;  // the owner contributes, others 0
+    }
+  }
+}
+
+template <bool VEC>
+__global__ void __launch_bounds__(NT) grad_kernel(const float* s, int64_t lds, int m, int64_t c0,
+                                                  const int64_t* __restrict__ labels, const float* __restrict__ lse,
+                                                  float scale, float* g, int64_t ldg) {
+  const int64_t row = blockIdx.x;
+  const float* sr = s + row * lds;
+  float* gr = g + row * ldg;
+  row_grad<VEC>(sr, gr, m, lse[row], scale, 0.f);
+  __syncthreads();
+  if (threadIdx.x == 0 && labels) {
+    const int64_t c = labels[row] - c0;
+    if (c >= 0 && c < m) gr[c] -= scale;
+  }
+}
+
+bool vec_ok(const float* s, int64_t lds, const float* g, int64_t ldg) {
+  return lds % 4 == 0 && aligned16(s) && (!g || (ldg % 4 == 0 && aligned16(g)));
+}
+
 int launch(const float* s, int64_t lds, int64_t n, int64_t m, const int64_t* l_ptr, const int64_t* l_col, float eps,
            float scale, float* loss, float* g, int64_t ldg, hipStream_t st) {
-  const bool vec = lds % 4 == 0 && aligned16(s) && (!g || (ldg % 4 == 0 && aligned16(g)));
-  if (vec)
+  if (vec_ok(s, lds, g, ldg))
     softmax_kl_kernel<true><<<dim3((unsigned)n), dim3(NT), 0, st>>>(s, lds, (int)m, l_ptr, l_col, eps, scale, loss,
                                                                     g, ldg);
   else
@@ -196,4 +267,35 @@ extern "C" int kge_softmax_kl(const float* s, int64_t lds, int64_t n, int64_t m,
   KGE_REQUIRE(smoothing >= 0.f && smoothing < 1.f);
   if (n == 0) return 0;
   return launch(s, lds, n, m, l_ptr, l_col, smoothing, scale, loss, g, ldg, as_stream(stream));
+}
+
+extern "C" int kge_softmax_row_stats(const float* s, int64_t lds, int64_t n, int64_t m, int64_t c0,
+                                     const int64_t* labels, float* row_max, float* row_sumexp, float* target,
+                                     void* stream) {
+  KGE_REQUIRE(n >= 0 && m > 0 && m < (1LL << 31) && n < (1LL << 31) && lds >= m);
+  KGE_REQUIRE(s && row_max && row_sumexp && (!target || labels));
+  if (n == 0) return 0;
+  hipStream_t st = as_stream(stream);
+  if (vec_ok(s, lds, nullptr, 0))
+    row_stats_kernel<true><<<dim3((unsigned)n), dim3(NT), 0, st>>>(s, lds, (int)m, c0, labels, row_max, row_sumexp,
+                                                                   target);
+  else
+    row_stats_kernel<false><<<dim3((unsigned)n), dim3(NT), 0, st>>>(s, lds, (int)m, c0, labels, row_max, row_sumexp,
+                                                                    target);
+  KGE_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int kge_softmax_grad(const float* s, int64_t lds, int64_t n, int64_t m, int64_t c0, const int64_t* labels,
+                                const float* lse, float scale, float* g, int64_t ldg, void* stream) {
+  KGE_REQUIRE(n >= 0 && m > 0 && m < (1LL << 31) && n < (1LL << 31) && lds >= m);
+  KGE_REQUIRE(s && lse && g && ldg >= m && (g != s || ldg == lds));
+  if (n == 0) return 0;
+  hipStream_t st = as_stream(stream);
+  if (vec_ok(s, lds, g, ldg))
+    grad_kernel<true><<<dim3((unsigned)n), dim3(NT), 0, st>>>(s, lds, (int)m, c0, labels, lse, scale, g, ldg);
+  else
+    grad_kernel<false><<<dim3((unsigned)n), dim3(NT), 0, st>>>(s, lds, (int)m, c0, labels, lse, scale, g, ldg);
+  KGE_CHECK_LAUNCH();
+  return 0;
 }

@@ -56,6 +56,8 @@ SIGNATURES = {
     "kge_score_cand_bwd_ent": ([_I, _F, _I, _P, _I64, _P, _I64, _P, _I64, _I64, _I, _P, _P, _I64, _P, _I64, _P,
                                 _I64, _P, _I64, _P], _I),
     "kge_bucket_scatter": ([_P, _I64, _P, _P, _P], _I),
+    "kge_softmax_row_stats": ([_P, _I64, _I64, _I64, _I64, _P, _P, _P, _P, _P], _I),
+    "kge_softmax_grad": ([_P, _I64, _I64, _I64, _I64, _P, _P, _F, _P, _I64, _P], _I),
 }
 
 _lib: Optional[ctypes.CDLL] = None
@@ -372,6 +374,30 @@ def score_cand_bwd_ent(model, l_norm, direction, q, ent, cand, s, g, d_ent) -> b
                                         rows(s) if s is not None else 0, ptr(g), rows(g), ptr(d_ent), rows(d_ent),
                                         stream()), "kge_score_cand_bwd_ent")
     return True
+
+
+def softmax_row_stats(s, c0, labels):
+    """(row max, row sum exp(x - max), target score or 0) over the column slice s = columns
+    [c0, c0 + m) of score rows; labels are global column ids."""
+    require_device(s)
+    labels = idx64(labels)
+    n, m = s.shape
+    mx = torch.empty(n, device=s.device, dtype=torch.float32)
+    sm = torch.empty_like(mx)
+    tg = torch.empty_like(mx) if labels is not None else None
+    _check(lib().kge_softmax_row_stats(ptr(s), rows(s), n, m, int(c0), ptr(labels), ptr(mx), ptr(sm), ptr(tg),
+                                       stream()), "kge_softmax_row_stats")
+    return mx, sm, tg
+
+
+def softmax_grad(s, c0, labels, lse, scale, g):
+    """g = scale * (exp(s - lse[:, None]) - onehot(labels - c0)) on the column slice."""
+    labels = idx64(labels)
+    lse = lse.contiguous()
+    n, m = s.shape
+    _check(lib().kge_softmax_grad(ptr(s), rows(s), n, m, int(c0), ptr(labels), ptr(lse), float(scale), ptr(g),
+                                  rows(g), stream()), "kge_softmax_grad")
+    return g
 
 
 def softmax_kl(s, l_ptr, l_col, smoothing, scale, g=None, loss=None):

@@ -44,13 +44,37 @@ class EngineOps:
         n = eidx.numel()
         return self.L.prep_query(self.kind, direction, ent, eidx, rel, ridx, n, ent.shape[1], rel.shape[1])
 
-    def score(self, q, tab):
+    def score(self, q, tab, out=None):
         from .engine import BILINEAR, dist_kind
 
         if self.kind in BILINEAR:
-            return self.L.contract(q, tab, None, self.precision)
+            return self.L.contract(q, tab, None, self.precision, out=out)
         dk, sign = dist_kind(self.kind, self.l_norm)
-        return self.L.score_dist(dk, sign, q, tab, None)
+        return self.L.score_dist(dk, sign, q, tab, None, out=out)
+
+    # ---- vocab-parallel 1vsAll training
+    def row_stats(self, s, c0, labels):
+        return self.L.softmax_row_stats(s, c0, labels)
+
+    def softmax_grad(self, s, c0, labels, lse, scale, g):
+        return self.L.softmax_grad(s, c0, labels, lse, scale, g)
+
+    def score_bwd(self, g, q, tab, dq, d_tab):
+        """dq = d/dq <g, S(q, tab)> (written), d_tab += d/dtab <g, S>."""
+        from .engine import BILINEAR, dist_kind
+
+        if self.kind in BILINEAR:
+            self.L.score_dot_bwd_q(g, tab, None, self.precision, dq=dq, accumulate=False)
+            self.L.score_dot_bwd_t(g, q, None, d_tab, self.precision)
+        else:
+            dq.zero_()
+            dk, sign = dist_kind(self.kind, self.l_norm)
+            self.L.score_dist_bwd(dk, sign, g, q, tab, None, dq, d_tab)
+
+    def prep_bwd(self, direction, ent, eidx, rel, ridx, dq, d_ent, d_rel):
+        n = eidx.numel()
+        self.L.prep_query_bwd(self.kind, direction, ent, eidx, rel, ridx, n, ent.shape[1], rel.shape[1], dq, d_ent,
+                              d_rel)
 
     def spo(self, ent_s, rel, p, ent_o):
         n = p.numel()
@@ -148,6 +172,52 @@ class RowShardedScorer:
         V, I = torch.cat(vs, 1), torch.cat(is_, 1)
         tv, ti = torch.topk(V, k, dim=1)
         return tv, torch.gather(I, 1, ti)
+
+    # ---------------------------------------------------------------- training
+    def train_1vsall_grads(self, s: torch.Tensor, p: torch.Tensor, o: torch.Tensor):
+        """Vocab-parallel 1vsAll (SURVEY.md 8e "training collectives"): every rank passes its
+        own B triples; the global batch is the W*B gathered triples and the objective is
+        the reference's  sum over (sp_, _po) of CE(scores, target) / (W*B)
+        (train.py:1032-1062 with batch W*B).  Per direction:
+          all_gather triples -> owner-computed Q (all_reduce) -> local logits [W*B, E_k]
+          -> local (max, sumexp, target) -> all_reduce MAX / SUM / SUM (3 x W*B floats)
+          -> lse -> local G_k = scale (softmax - onehot) in place of the logits
+          -> dQ = sum_k G_k E_k (all_reduce, W*B x d) ; dE_k = G_k^T Q stays local
+          -> prep backward for the queries this rank owns.
+        The relation gradient is all_reduced once (each query's at its owner).
+        Returns (loss, d_ent for this rank's shard, d_rel) -- identical loss on every rank."""
+        tr = torch.stack([s, p, o], 1)
+        tr_all = self._all_gather_1d(tr.reshape(-1)).view(-1, 3)
+        n = tr_all.shape[0]
+        scale = 1.0 / n
+        E_k = self.hi - self.lo
+        d_ent = torch.zeros_like(self.ent)
+        d_rel = torch.zeros_like(self.rel)
+        loss = torch.zeros((), device=self.ent.device, dtype=torch.float64)
+        for direction, e_col, lab_col in ((0, 0, 2), (1, 2, 0)):
+            e_all, p_all, labels = tr_all[:, e_col], tr_all[:, 1], tr_all[:, lab_col]
+            owned, local = self._owned_rows(e_all)
+            q = self.ops.prep(direction, self.ent, local, self.rel, p_all)
+            q = torch.where(owned[:, None], q, torch.zeros_like(q))
+            dist.all_reduce(q, group=self.group)
+            buf = torch.empty(n, (E_k + 3) // 4 * 4, device=q.device, dtype=torch.float32)
+            logits = self.ops.score(q, self.ent, out=buf[:, :E_k])
+            mx, sm, tg = self.ops.row_stats(logits, self.lo, labels)
+            M = mx.clone()
+            dist.all_reduce(M, op=dist.ReduceOp.MAX, group=self.group)
+            z = torch.where(mx == -math.inf, torch.zeros_like(sm), sm * torch.exp(mx - M))
+            dist.all_reduce(z, group=self.group)
+            dist.all_reduce(tg, group=self.group)
+            lse = M + torch.log(z)
+            loss += ((lse - tg).double().sum() * scale)
+            g = self.ops.softmax_grad(logits, self.lo, labels, lse, scale, logits)
+            dq = torch.empty_like(q)
+            self.ops.score_bwd(g, q, self.ent, dq, d_ent)
+            dist.all_reduce(dq, group=self.group)
+            dq = torch.where(owned[:, None], dq, torch.zeros_like(dq))
+            self.ops.prep_bwd(direction, self.ent, local, self.rel, p_all, dq, d_ent, d_rel)
+        dist.all_reduce(d_rel, group=self.group)
+        return float(loss), d_ent, d_rel
 
     # ---------------------------------------------------------------- eval
     def rank_counts(self, s, p, o, f_sp, f_po, t_sp=None, t_po=None):

@@ -1,0 +1,88 @@
+"""GPU: the vocab-parallel pieces on the engine -- kge_softmax_row_stats / kge_softmax_grad
+against torch on column slices, and RowShardedScorer.train_1vsall_grads with EngineOps at
+world size 1 (RCCL, in-process) against the fused single-GPU 1vsAll gradients."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def L():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from kge import _lib
+    _lib.lib()
+    return _lib
+
+
+@pytest.mark.parametrize("m,ld", [(1001, 1004), (777, 777), (4096, 4096)])
+def test_row_stats_and_grad_on_slice(L, m, ld):
+    rng = np.random.default_rng(m)
+    n, c0 = 19, 300
+    buf = torch.zeros(n, ld, device="cuda")
+    s = buf[:, :m]
+    s.copy_(torch.from_numpy((rng.standard_normal((n, m)) * 4).astype(np.float32)))
+    labels = torch.from_numpy(rng.integers(0, c0 + m + 200, size=n)).cuda()  # some outside the slice
+    mx, sm, tg = L.softmax_row_stats(s, c0, labels)
+    ref_mx = s.max(1).values
+    assert torch.equal(mx, ref_mx)
+    torch.testing.assert_close(sm, torch.exp(s - ref_mx[:, None]).sum(1), rtol=2e-6, atol=0)
+    c = labels - c0
+    inside = (c >= 0) & (c < m)
+    ref_tg = torch.where(inside, s[torch.arange(n), c.clamp(0, m - 1)], torch.zeros_like(mx))
+    assert torch.equal(tg, ref_tg)
+    lse = ref_mx + torch.log(torch.exp(s - ref_mx[:, None]).sum(1)) + 0.25  # any global lse
+    g = torch.empty_like(s)
+    L.softmax_grad(s, c0, labels, lse, 0.5, g)
+    ref = 0.5 * torch.exp(s - lse[:, None])
+    rows = torch.nonzero(inside).view(-1)
+    ref[rows, c[rows]] -= 0.5
+    torch.testing.assert_close(g, ref, rtol=0, atol=2e-6 * 0.5)
+
+
+def _free_port():
+    with socket.socket() as s_:
+        s_.bind(("127.0.0.1", 0))
+        return s_.getsockname()[1]
+
+
+@pytest.mark.parametrize("prec", ["bf16x3", "fp32"])
+def test_train_1vsall_grads_world1_matches_fused(L, prec):
+    from kge import Config, Dataset, KgeModel
+    from kge.sharded import EngineOps, RowShardedScorer
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()))
+    dist.init_process_group("nccl", rank=0, world_size=1)
+    try:
+        torch.manual_seed(0)
+        c = Config()
+        c.set("model", "complex")
+        c._import("complex")
+        c.set("job.device", "cuda")
+        c.set("lookup_embedder.dim", 128)
+        c.set("lookup_embedder.initialize_args", {"mean": 0.0, "std": 0.1})
+        c.set("engine.precision", prec)
+        c.set("dataset.num_entities", 3001)
+        c.set("dataset.num_relations", 17)
+        m = KgeModel.create(c, Dataset(c, None))
+        ent = m._entity_embedder._embeddings.weight
+        rel = m._relation_embedder._embeddings.weight
+        g = torch.Generator().manual_seed(3)
+        B = 300
+        s, p, o = (torch.randint(0, n, (B,), generator=g).cuda() for n in (3001, 17, 3001))
+        loss = m.score_sp_xent(s, p, o, 1.0 / B) + m.score_po_xent(p, o, s, 1.0 / B)
+        loss.backward()
+        sc = RowShardedScorer(ent.detach(), 0, 3001, 3001, rel.detach(), EngineOps(0, L.PRECISIONS[prec]))
+        l2, d_ent, d_rel = sc.train_1vsall_grads(s, p, o)
+        assert abs(l2 - loss.item()) <= 1e-5 * abs(loss.item())
+        tol = 1e-4 if prec == "bf16x3" else 1e-5
+        assert (d_ent - ent.grad).abs().max() <= tol * ent.grad.abs().max()
+        assert (d_rel - rel.grad).abs().max() <= tol * rel.grad.abs().max()
+    finally:
+        dist.destroy_process_group()
