@@ -230,8 +230,18 @@ def main():
         peak = FP32_MFMA_TFLOPS
         note = "fp32-input MFMA (v_mfma_f32_32x32x2_f32); peak = 157.3 TF"
     achieved = alg_flops / k_s / 1e12
+    # HBM bytes per launch from the PMC passes of scripts/pmc_traffic.sh (same kernel, same
+    # shape at N=1), committed under profiles/; null when absent or for another shape.
+    traffic, traffic_src = None, None
+    pmc = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r01", "pmc_traffic.json")
+    if world == 1 and args.precision == "bf16x3" and os.path.exists(pmc):
+        with open(pmc) as f:
+            t = json.load(f)
+        traffic = int(t["traffic_bytes"])
+        traffic_src = ("profiles/r01/pmc_traffic.json: 2 x FETCH_SIZE + WRITE_SIZE per dispatch "
+                       f"(read {t['read_bytes'] / 1e6:.1f} MB, write {t['write_bytes'] / 1e6:.1f} MB)")
     roofline = {"bound": "mfma", "achieved": round(achieved, 1), "peak": round(peak, 1), "unit": "TFLOP/s",
-                "frac": round(achieved / peak, 4), "traffic": None,
+                "frac": round(achieved / peak, 4), "traffic": traffic, "traffic_source": traffic_src,
                 "kernel": "score_dot_persist_kernel" if args.precision == "bf16x3" else "score_dot_kernel", "kernel_us": round(kern_ms * 1e3, 2),
                 "kernel_us_per_launch_events": round(launch_ms * 1e3, 2),
                 "hbm_achieved_GBs": round(alg_bytes / k_s / 1e9, 1),
@@ -312,6 +322,65 @@ def extras(args, model, c, E, R, device):
     res["eval_seconds"] = round(time.perf_counter() - t0, 4)
     res["eval_mrr_filtered"] = tr["mean_reciprocal_rank_filtered"]
     res["eval_hits_at_10_filtered"] = tr["hits_at_10_filtered"]
+    res.update(other_configs(device))
+    return res
+
+
+def _job_step_time(cfg, dataset, batch, steps=10, warmup=3):
+    from kge import Dataset
+    from kge.job import TrainingJob
+
+    ds = Dataset.synthetic(cfg, dataset, seed=0)
+    job = TrainingJob.create(cfg, ds)
+    job._prepare()
+    perm = torch.randperm(job.num_examples, generator=torch.Generator().manual_seed(0))
+
+    def step(i):
+        job.optimizer.zero_grad()
+        job._process_batch(i, job._collate(perm[i * batch:(i + 1) * batch]))
+        job.optimizer.step()
+    return timed_loop(step, steps, warmup, 1), ds
+
+
+def other_configs(device):
+    """BASELINE configs C3 (DistMult-512 KvsAll WN18RR, B=512) and C4 (RotatE-1024 negative
+    sampling, 1024 negatives per corrupted slot, FB15K-237, B=512): full training steps
+    (fwd + bwd + loss + Adagrad) on synthetic data of the dataset shape."""
+    from kge import Config
+
+    res = {}
+    c = Config()
+    c.set("model", "distmult")
+    c._import("distmult")
+    c.set("job.device", str(device))
+    c.set("lookup_embedder.dim", 512)
+    c.set("lookup_embedder.initialize_args", {"mean": 0.0, "std": 0.1})
+    c.set("train.type", "KvsAll")
+    c.set("train.optimizer", "Adagrad")
+    c.set("train.optimizer_args", {"lr": 0.2})
+    c.set("train.batch_size", 512)
+    c.set("verbose", False)
+    sec, ds = _job_step_time(c, "wn18rr", 512)
+    E = ds.num_entities()
+    res["c3_kvsall_distmult512_wn18rr_b512_step_ms"] = round(sec * 1e3, 3)
+    res["c3_scored_triples_per_s"] = 512 * E / sec  # one query type per batch slice; B queries x E
+    torch.manual_seed(0)
+    c = Config()
+    c.set("model", "rotate")
+    c._import("rotate")
+    c.set("job.device", str(device))
+    c.set("lookup_embedder.dim", 1024)
+    c.set("train.type", "negative_sampling")
+    c.set("train.loss", "kl")
+    c.set("negative_sampling.num_samples.s", 1024)
+    c.set("negative_sampling.implementation", "triple")
+    c.set("train.optimizer", "Adagrad")
+    c.set("train.optimizer_args", {"lr": 0.1})
+    c.set("train.batch_size", 512)
+    c.set("verbose", False)
+    sec, _ = _job_step_time(c, "fb15k-237", 512)
+    res["c4_ns_rotate1024_fb15k237_b512_n1024_step_ms"] = round(sec * 1e3, 3)
+    res["c4_scored_triples_per_s"] = 2 * 512 * 1025 / sec  # s and o slots, positive + 1024 negatives
     return res
 
 

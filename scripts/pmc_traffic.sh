@@ -1,0 +1,42 @@
+#!/bin/bash
+# HBM traffic of the headline contraction kernel per launch, as MI355X_MICROARCH.md §HBM
+# prescribes: separate --pmc passes for FETCH_SIZE and WRITE_SIZE (kernel-trace only, no
+# sys/runtime trace), FETCH_SIZE doubled for the 16-B-per-lane streaming reads on gfx950.
+# Writes gpurun_out/pmc_traffic/pmc_traffic.json (copy it to profiles/r01/, which bench.py
+# reports as roofline.traffic) and also refreshes profiles/r01/ in the box's copy of the repo.
+set -o pipefail
+export TMPDIR=/tmp
+OUT=$GRAFT_REPO_ROOT/gpurun_out/pmc_traffic
+mkdir -p $OUT
+cd /tmp
+i=0
+for ctr in FETCH_SIZE WRITE_SIZE; do
+  i=$((i+1))
+  timeout -k 10 240 rocprofv3 --pmc $ctr --kernel-trace --output-format csv -d $OUT/p$i -o run -- \
+    python3 $GRAFT_REPO_ROOT/bench.py --no-cpu --no-extras --steps 10 --warmup 3 > $OUT/bench$i.json 2> $OUT/err$i.txt \
+    || { echo "pmc pass $ctr failed"; tail -5 $OUT/err$i.txt; exit 1; }
+done
+python3 - "$OUT" "$OUT/pmc_traffic.json" <<'EOF'
+import csv, glob, json, sys, collections
+root, dst = sys.argv[1], sys.argv[2]
+vals = collections.defaultdict(list)
+name = None
+for fn in sorted(glob.glob(f"{root}/p*/**/*counter_collection.csv", recursive=True)):
+    for row in csv.DictReader(open(fn)):
+        if "score_dot_persist_kernel" in row.get("Kernel_Name", ""):
+            vals[row["Counter_Name"]].append(float(row["Counter_Value"]))
+            name = row["Kernel_Name"]
+fetch_kb = sum(vals["FETCH_SIZE"]) / len(vals["FETCH_SIZE"])
+write_kb = sum(vals["WRITE_SIZE"]) / len(vals["WRITE_SIZE"])
+out = {"kernel": name, "dispatches": {k: len(v) for k, v in vals.items()},
+       "fetch_size_kb": fetch_kb, "write_size_kb": write_kb,
+       "read_bytes": 2 * fetch_kb * 1024, "write_bytes": write_kb * 1024,
+       "traffic_bytes": 2 * fetch_kb * 1024 + write_kb * 1024,
+       "method": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes, kernel-trace only) over "
+                 "bench.py --no-cpu --no-extras; per-dispatch mean; FETCH_SIZE x2 (gfx950: 16-B/lane "
+                 "streaming reads tallied at half, MI355X_MICROARCH.md §HBM); WRITE_SIZE as reported "
+                 "(4-B/lane score stores: width not calibrated by the guide)"}
+json.dump(out, open(dst, "w"), indent=1)
+print(json.dumps(out))
+EOF
+cp $OUT/pmc_traffic.json $GRAFT_REPO_ROOT/profiles/r01/pmc_traffic.json
