@@ -85,6 +85,74 @@ __global__ void __launch_bounds__(256) prep_elementwise(const float* __restrict_
   }
 }
 
+// Vectorised elementwise prep: one wave per query row, 4 consecutive elements (complex
+// positions for ComplEx / RotatE) per lane per step, float4 loads, float4 / bf16x4 stores.
+// Needs d_e % 8 == 0 (complex halves % 4) and 16-B aligned rows (checked by the launcher).
+template <int MODEL, int DIR>
+__global__ void __launch_bounds__(256) prep_elementwise_vec(const float* __restrict__ ent, int64_t ld_ent,
+                                                             const int64_t* __restrict__ eidx,
+                                                             const float* __restrict__ rel, int64_t ld_rel,
+                                                             const int64_t* __restrict__ ridx, int64_t n, int d_e,
+                                                             QOut out) {
+  const int64_t i = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (i >= n) return;
+  const int lane = threadIdx.x & 63;
+  Rows rw = fetch_rows(ent, ld_ent, eidx, rel, ld_rel, ridx, i);
+  auto put4 = [&](int k, float4 v) {
+    if (out.q) *reinterpret_cast<float4*>(out.q + i * out.ldq + k) = v;
+    if (out.hi) {
+      bf16x4 h, l;
+      split_bf16x4(v, h, l);
+      *reinterpret_cast<bf16x4*>(out.hi + i * out.ldp + k) = h;
+      *reinterpret_cast<bf16x4*>(out.lo + i * out.ldp + k) = l;
+    }
+  };
+  if (out.hi)
+    for (int k = d_e + lane * 4; k < out.ldp; k += 256) {  // zero padding to ldp (ldp % 8 == 0)
+      *reinterpret_cast<bf16x4*>(out.hi + i * out.ldp + k) = bf16x4{};
+      *reinterpret_cast<bf16x4*>(out.lo + i * out.ldp + k) = bf16x4{};
+    }
+  if (MODEL == KGE_COMPLEX || MODEL == KGE_ROTATE) {
+    const int h = d_e / 2;
+    for (int k = lane * 4; k < h; k += 256) {
+      const float4 ar = *reinterpret_cast<const float4*>(rw.e + k), ai = *reinterpret_cast<const float4*>(rw.e + k + h);
+      float4 c, s;
+      if (MODEL == KGE_COMPLEX) {
+        c = *reinterpret_cast<const float4*>(rw.r + k);
+        s = *reinterpret_cast<const float4*>(rw.r + k + h);
+      } else {
+        const float4 ph = *reinterpret_cast<const float4*>(rw.r + k);  // rotate.py:273
+        sincosf(ph.x, &s.x, &c.x);
+        sincosf(ph.y, &s.y, &c.y);
+        sincosf(ph.z, &s.z, &c.z);
+        sincosf(ph.w, &s.w, &c.w);
+      }
+      float4 re, im;
+      if (DIR == KGE_DIR_SP) {  // a * (c + i s)
+        re = make_float4(ar.x * c.x - ai.x * s.x, ar.y * c.y - ai.y * s.y, ar.z * c.z - ai.z * s.z, ar.w * c.w - ai.w * s.w);
+        im = make_float4(ar.x * s.x + ai.x * c.x, ar.y * s.y + ai.y * c.y, ar.z * s.z + ai.z * c.z, ar.w * s.w + ai.w * c.w);
+      } else {  // conj(c + i s) * a
+        re = make_float4(c.x * ar.x + s.x * ai.x, c.y * ar.y + s.y * ai.y, c.z * ar.z + s.z * ai.z, c.w * ar.w + s.w * ai.w);
+        im = make_float4(c.x * ai.x - s.x * ar.x, c.y * ai.y - s.y * ar.y, c.z * ai.z - s.z * ar.z, c.w * ai.w - s.w * ar.w);
+      }
+      put4(k, re);
+      put4(k + h, im);
+    }
+  } else {
+    for (int k = lane * 4; k < d_e; k += 256) {
+      const float4 a = *reinterpret_cast<const float4*>(rw.e + k), b = *reinterpret_cast<const float4*>(rw.r + k);
+      float4 v;
+      if (MODEL == KGE_DISTMULT)
+        v = make_float4(a.x * b.x, a.y * b.y, a.z * b.z, a.w * b.w);
+      else if (DIR == KGE_DIR_SP)  // TRANSE
+        v = make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w);
+      else
+        v = make_float4(a.x - b.x, a.y - b.y, a.z - b.z, a.w - b.w);
+      put4(k, v);
+    }
+  }
+}
+
 // RESCAL: Q = s^T M (sp) or M o (po), M = rel row viewed as [d, d] row-major.
 template <int DIR>
 __global__ void __launch_bounds__(256) prep_rescal(const float* __restrict__ ent, int64_t ld_ent,
@@ -228,6 +296,30 @@ template <int DIR>
 int launch_prep(int model, const float* ent, int64_t ld_ent, const int64_t* eidx, const float* rel,
                 int64_t ld_rel, const int64_t* ridx, int64_t n, int d_e, QOut q, hipStream_t st) {
   dim3 grid((unsigned)n), block(256);
+  const int unit = (model == KGE_COMPLEX || model == KGE_ROTATE) ? d_e / 2 : d_e;
+  const bool vec = model != KGE_RESCAL && (model == KGE_DISTMULT || model == KGE_TRANSE || d_e % 2 == 0) &&
+                   unit % 4 == 0 && ld_ent % 4 == 0 && ld_rel % 4 == 0 && aligned16(ent) && aligned16(rel) &&
+                   (!q.q || (q.ldq % 4 == 0 && aligned16(q.q))) &&
+                   (!q.hi || (q.ldp % 8 == 0 && aligned16(q.hi) && aligned16(q.lo)));
+  if (vec) {
+    const dim3 g4((unsigned)((n + 3) / 4));
+    switch (model) {
+      case KGE_COMPLEX:
+        prep_elementwise_vec<KGE_COMPLEX, DIR><<<g4, block, 0, st>>>(ent, ld_ent, eidx, rel, ld_rel, ridx, n, d_e, q);
+        break;
+      case KGE_DISTMULT:
+        prep_elementwise_vec<KGE_DISTMULT, DIR><<<g4, block, 0, st>>>(ent, ld_ent, eidx, rel, ld_rel, ridx, n, d_e, q);
+        break;
+      case KGE_TRANSE:
+        prep_elementwise_vec<KGE_TRANSE, DIR><<<g4, block, 0, st>>>(ent, ld_ent, eidx, rel, ld_rel, ridx, n, d_e, q);
+        break;
+      default:
+        prep_elementwise_vec<KGE_ROTATE, DIR><<<g4, block, 0, st>>>(ent, ld_ent, eidx, rel, ld_rel, ridx, n, d_e, q);
+        break;
+    }
+    KGE_CHECK_LAUNCH();
+    return 0;
+  }
   switch (model) {
     case KGE_COMPLEX:
       prep_elementwise<KGE_COMPLEX, DIR><<<grid, block, 0, st>>>(ent, ld_ent, eidx, rel, ld_rel, ridx, d_e, q);

@@ -31,7 +31,9 @@ struct PCfg {
   static_assert(BM % (32 * WM) == 0 && BN % (32 * WN) == 0, "tile");
 };
 
-template <int BM, int BN, int WM, int WN>
+typedef float f32x4u __attribute__((ext_vector_type(4), aligned(4)));  // 4-B-aligned float4
+
+template <int BM, int BN, int WM, int WN, bool EPI = false>
 __global__ void __launch_bounds__(64 * WM * WN, 1)
     score_dot_persist_kernel(const __bf16* __restrict__ qhi, const __bf16* __restrict__ qlo, int64_t ldq,
                              const float* __restrict__ t, int64_t ldt, const int64_t* __restrict__ tidx, int n,
@@ -173,22 +175,57 @@ __global__ void __launch_bounds__(64 * WM * WN, 1)
     compute(smem + (st & 1) * C::STAGE);
 
     const int col_l = lane & 31, rh = lane >> 5;
+    if (EPI) {
+      // Row-vector epilogue: each 32x32 accumulator tile (a column per lane) is transposed
+      // through a wave-private 4 KB LDS scratch and stored as whole-row float4s -- 4
+      // global_store_dwordx4 per lane instead of 16 dword stores; the tail of the kernel is
+      // store-issue-bound.  Score rows (leading dim m, odd in general) are only 4-B aligned:
+      // gfx950 / HSA declares unaligned global access (the compiler emits dwordx4 for an
+      // align-4 float4), so no per-row realignment is needed.
+      __syncthreads();  // every wave is done with the stage buffers: reuse as scratch
+      float* scr = reinterpret_cast<float*>(smem) + wave * 32 * 32;
+      const int rr = lane >> 3, cc = (lane & 7) * 4;
 #pragma unroll
-    for (int x = 0; x < C::TM; ++x)
+      for (int x = 0; x < C::TM; ++x)
 #pragma unroll
-      for (int y = 0; y < C::TN; ++y) {
-        const int j = n0 + wc * (BN / WN) + y * 32 + col_l;
+        for (int y = 0; y < C::TN; ++y) {
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int i = m0 + wr * (BM / WM) + x * 32 + (r & 3) + 8 * (r >> 2) + 4 * rh;
-          if (i < n && j < m) s[(int64_t)i * lds + j] = acc[x][y][r];
+          for (int r = 0; r < 16; ++r) scr[((r & 3) + 8 * (r >> 2) + 4 * rh) * 32 + col_l] = acc[x][y][r];
+          const int i0 = m0 + wr * (BM / WM) + x * 32, j = n0 + wc * (BN / WN) + y * 32 + cc;
+#pragma unroll
+          for (int pass = 0; pass < 4; ++pass) {
+            const int row = pass * 8 + rr;
+            const float4 v = *reinterpret_cast<const float4*>(scr + row * 32 + cc);
+            const int i = i0 + row;
+            if (i >= n) continue;
+            float* dst = s + (int64_t)i * lds + j;
+            if (j + 3 < m) {
+              *reinterpret_cast<f32x4u*>(dst) = f32x4u{v.x, v.y, v.z, v.w};
+            } else {
+              if (j < m) dst[0] = v.x;
+              if (j + 1 < m) dst[1] = v.y;
+              if (j + 2 < m) dst[2] = v.z;
+            }
+          }
         }
-      }
+    } else {
+#pragma unroll
+      for (int x = 0; x < C::TM; ++x)
+#pragma unroll
+        for (int y = 0; y < C::TN; ++y) {
+          const int j = n0 + wc * (BN / WN) + y * 32 + col_l;
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int i = m0 + wr * (BM / WM) + x * 32 + (r & 3) + 8 * (r >> 2) + 4 * rh;
+            if (i < n && j < m) s[(int64_t)i * lds + j] = acc[x][y][r];
+          }
+        }
+    }
     __syncthreads();  // LDS of this tile is free for the next tile's prologue
   }
 }
 
-template <int BM, int BN, int WM, int WN>
+template <int BM, int BN, int WM, int WN, bool EPI = false>
 int launch_persist(const __bf16* qhi, const __bf16* qlo, int64_t ldq, const float* t, int64_t ldt,
                    const int64_t* tidx, int64_t n, int64_t m, int d, float* s, int64_t lds, int per_cu,
                    hipStream_t st) {
@@ -199,7 +236,7 @@ int launch_persist(const __bf16* qhi, const __bf16* qlo, int64_t ldq, const floa
   const size_t shmem = 2 * C::STAGE;
   static bool attr_set = false;
   if (!attr_set) {
-    hipError_t e = hipFuncSetAttribute((const void*)score_dot_persist_kernel<BM, BN, WM, WN>,
+    hipError_t e = hipFuncSetAttribute((const void*)score_dot_persist_kernel<BM, BN, WM, WN, EPI>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)shmem);
     if (e != hipSuccess) return (int)e;
     attr_set = true;
@@ -207,7 +244,7 @@ int launch_persist(const __bf16* qhi, const __bf16* qlo, int64_t ldq, const floa
   int grid = kge_num_cus() * per_cu;
   grid = (int)std::min<int64_t>(grid, (ntiles + 7) / 8 * 8);
   grid = std::max(8, grid / 8 * 8);
-  score_dot_persist_kernel<BM, BN, WM, WN><<<dim3(grid), dim3(C::NT), shmem, st>>>(
+  score_dot_persist_kernel<BM, BN, WM, WN, EPI><<<dim3(grid), dim3(C::NT), shmem, st>>>(
       qhi, qlo, ldq, t, ldt, tidx, (int)n, (int)m, d, s, lds, nrt, (int)ntiles);
   KGE_CHECK_LAUNCH();
   return 0;
@@ -250,8 +287,8 @@ extern "C" int kge_score_dot_split(const void* qhi, const void* qlo, int64_t ldq
   hipStream_t st = as_stream(stream);
   const __bf16* h = (const __bf16*)qhi;
   const __bf16* l = (const __bf16*)qlo;
-  if (n > 128) return launch_persist<256, 256, 2, 4>(h, l, ldq, t, ldt, tidx, n, m, d, s, lds, 1, st);
-  return launch_persist<128, 256, 2, 4>(h, l, ldq, t, ldt, tidx, n, m, d, s, lds, 1, st);
+  if (n > 128) return launch_persist<256, 256, 2, 4, true>(h, l, ldq, t, ldt, tidx, n, m, d, s, lds, 1, st);
+  return launch_persist<128, 256, 2, 4, true>(h, l, ldq, t, ldt, tidx, n, m, d, s, lds, 1, st);
 }
 
 extern "C" int kge_dev_score_dot_persist(int variant, const void* qhi, const void* qlo, int64_t ldq,
@@ -270,6 +307,8 @@ extern "C" int kge_dev_score_dot_persist(int variant, const void* qhi, const voi
     case 4: return launch_persist<256, 256, 2, 4>(h, l, ldq, t, ldt, tidx, n, m, d, s, lds, 1, st);
     case 5: return launch_persist<256, 128, 4, 2>(h, l, ldq, t, ldt, tidx, n, m, d, s, lds, 2, st);
     case 6: return launch_persist<128, 128, 2, 2>(h, l, ldq, t, ldt, tidx, n, m, d, s, lds, 3, st);
+    case 7: return launch_persist<256, 256, 2, 4, true>(h, l, ldq, t, ldt, tidx, n, m, d, s, lds, 1, st);
+    case 8: return launch_persist<128, 256, 2, 4, true>(h, l, ldq, t, ldt, tidx, n, m, d, s, lds, 1, st);
     default: return KGE_ERR_ARG;
   }
 }

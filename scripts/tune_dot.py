@@ -4,12 +4,9 @@ sys.path.insert(0, '.'); sys.path.insert(0, 'kge-1_amd')
 import numpy as np, torch
 from kge import _lib as L
 lib = L.lib()
-lib.kge_dev_score_dot_x3.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p,
-                                     ctypes.c_int64, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64, ctypes.c_int,
-                                     ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p]
-lib.kge_dev_score_dot_persist.argtypes = lib.kge_dev_score_dot_x3.argtypes
-lib.kge_dev_split_rows.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64, ctypes.c_int, ctypes.c_void_p,
-                                   ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p]
+lib.kge_dev_score_dot_persist.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64,
+                                          ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_int64,
+                                          ctypes.c_int64, ctypes.c_int, ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p]
 E, R, B, d = 14541, 237, 1024, 512
 if len(sys.argv) > 1: B = int(sys.argv[1])
 torch.manual_seed(0)
@@ -19,7 +16,7 @@ q = L.prep_query(0, 0, ent, s, rel, p, B, d, d)
 ldo = ((d + 31) // 32) * 32
 qh = torch.empty(B, ldo, dtype=torch.bfloat16, device='cuda'); ql = torch.empty_like(qh)
 st = L.stream()
-assert lib.kge_dev_split_rows(q.data_ptr(), d, B, d, qh.data_ptr(), ql.data_ptr(), ldo, st) == 0
+assert lib.kge_split_rows(q.data_ptr(), d, B, d, qh.data_ptr(), ql.data_ptr(), ldo, st) == 0
 ref = (q.double() @ ent.double().T)
 out = torch.empty(B, E, device='cuda')
 def run(v):
@@ -29,9 +26,8 @@ def run(v):
         assert lib.kge_dev_score_dot_persist(int(v[1:]), qh.data_ptr(), ql.data_ptr(), ldo, ent.data_ptr(), d, None, B, E, d,
                                         out.data_ptr(), E, st) == 0
     else:
-        assert lib.kge_dev_score_dot_x3(v, qh.data_ptr(), ql.data_ptr(), ldo, ent.data_ptr(), d, None, B, E, d,
-                                        out.data_ptr(), E, st) == 0
-variants = [3, 'p0', 'p1', 'p2', 'p3', 'p4', 'p5', 'p6']
+        raise ValueError(v)
+variants = sys.argv[2].split(',') if len(sys.argv) > 2 else ['p4', 'p7', 'p1', 'p8']
 res = {v: [] for v in variants}
 for v in variants:
     out.zero_(); run(v); torch.cuda.synchronize()
