@@ -23,7 +23,7 @@ vals = collections.defaultdict(list)
 name = None
 for fn in sorted(glob.glob(f"{root}/p*/**/*counter_collection.csv", recursive=True)):
     for row in csv.DictReader(open(fn)):
-        if "score_dot_persist_kernel" in row.get("Kernel_Name", ""):
+        if "score_dot_persist" in row.get("Kernel_Name", ""):
             vals[row["Counter_Name"]].append(float(row["Counter_Value"]))
             name = row["Kernel_Name"]
 fetch_kb = sum(vals["FETCH_SIZE"]) / len(vals["FETCH_SIZE"])
