@@ -7,10 +7,12 @@ KgeModel.score_sp(s, p) -> fused LookupEmbedder gather + ComplEx query prep + th
 all-entities contraction against the 14,541-row entity table (libkgescore, gfx950).
 value = scored triples / s = (queries x entities) / step time, all ranks.
 
-N > 1 (torchrun, one process per GPU, RCCL): the entity table is row-sharded
-(kge.sharded); each rank contributes 1024 queries per step whose subjects it owns (a
-shard-affine loader), their query rows are all_gathered over RCCL, and the global batch of
-N*1024 queries is scored against every shard -> per-GPU work is constant (weak scaling).
+N > 1 (torchrun, one process per GPU): the scored triples are partitioned by query -- every
+rank scores its own 1024 queries against the entity table, replicated at setup -- so the
+step has no data-path collective and per-GPU work is constant (weak scaling).  The
+entity-row-sharded exchange over RCCL (kge.sharded: query rows all_gathered, global batch
+scored against each rank's shard) is timed after the headline loop and reported as
+"row_sharded", together with the cost of its all_gather alone.
 
 Also reported (rank 0): the contraction kernel's roofline from HIP events on the launch stream
 (20 back-to-back launches after the timed region), score_po, a full 1vsAll training step
@@ -136,64 +138,65 @@ def main():
     rel = model._relation_embedder._embeddings.weight
     steps, warmup = args.steps, args.warmup
     g = torch.Generator(device=device).manual_seed(1 + rank)
-    if world == 1:
-        s_all = torch.randint(0, E, (steps + warmup, B), device=device, generator=g)
-    else:  # shard-affine loader: rank k's queries have their subject in shard k
-        from kge.sharded import shard_bounds
-
-        lo_, hi_ = shard_bounds(E, world, rank)
-        s_all = torch.randint(lo_, hi_, (steps + warmup, B), device=device, generator=g)
+    s_all = torch.randint(0, E, (steps + warmup, B), device=device, generator=g)
     p_all = torch.randint(0, R, (steps + warmup, B), device=device, generator=g)
     prec = _lib.PRECISIONS[args.precision]
 
-    if world == 1:
-        def step(i):
-            with torch.no_grad():
-                return model.score_sp(s_all[i], p_all[i])
-        scored_per_step = B * E
-    else:
-        from kge.sharded import EngineOps, RowShardedScorer, shard_bounds
-
-        lo, hi = shard_bounds(E, world, rank)
-        shard = ent.detach()[lo:hi].contiguous()
-        sharded = RowShardedScorer(shard, lo, hi, E, rel.detach(), EngineOps(_lib.COMPLEX, prec))
-
-        def step(i):
-            with torch.no_grad():
-                return sharded.score_sp_local(s_all[i], p_all[i])
-        scored_per_step = world * B * E
+    # Every rank scores its own 1024 queries against the entity table (30 MB, replicated at
+    # setup): the scored triples are partitioned by query and the step has no data-path
+    # collective.  The entity-row-sharded exchange (kge.sharded: the design for eval top-k,
+    # vocab-parallel training and tables too large to replicate) is timed after the headline
+    # loop and reported in "row_sharded".
+    def step(i):
+        with torch.no_grad():
+            return model.score_sp(s_all[i], p_all[i])
+    scored_per_step = world * B * E
 
     # timed region: K steps bracketed by barrier + synchronize, nothing else inside
     sec = timed_loop(step, steps, warmup, world)
     # instrumented re-run of the same steps: HIP events around every contraction launch
     engine.KERNEL_EVENTS = []
-    _lib_events = []
     for i in range(min(steps, 20)):
-        if world == 1:
-            step(warmup + i)
-        else:
-            a = torch.cuda.Event(enable_timing=True)
-            b = torch.cuda.Event(enable_timing=True)
-            with torch.no_grad():
-                q = sharded.queries_local(s_all[warmup + i], p_all[warmup + i], 0)
-                a.record()
-                sharded.ops.score(q, sharded.ent)
-                b.record()
-            _lib_events.append((a, b))
+        step(warmup + i)
     torch.cuda.synchronize()
-    events = engine.KERNEL_EVENTS if world == 1 else _lib_events
+    events = engine.KERNEL_EVENTS
     engine.KERNEL_EVENTS = None
+    row_sharded = None
+    if world > 1:
+        from kge.sharded import EngineOps, RowShardedScorer, shard_bounds
+
+        lo, hi = shard_bounds(E, world, rank)
+        sharded = RowShardedScorer(ent.detach()[lo:hi].contiguous(), lo, hi, E, rel.detach(),
+                                   EngineOps(_lib.COMPLEX, prec))
+        # shard-affine loader: rank k's queries have their subject in shard k
+        s_aff = torch.randint(lo, hi, (steps + warmup, B), device=device, generator=g)
+
+        def step_sharded(i):
+            with torch.no_grad():
+                return sharded.score_sp_local(s_aff[i], p_all[i])
+
+        sec_sh = timed_loop(step_sharded, steps, warmup, world)
+        q_loc = torch.randn(B, d, device=device)
+
+        def gather_only(i):
+            out = torch.empty(world * B, d, device=device)
+            dist.all_gather_into_tensor(out, q_loc)
+        sec_ag = timed_loop(gather_only, steps, warmup, world)
+        t = torch.tensor([sec_sh, sec_ag], device=device, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        sec_sh, sec_ag = float(t[0]), float(t[1])
+        row_sharded = {"ms_per_step": sec_sh * 1e3, "value": world * B * E / sec_sh,
+                       "q_all_gather_ms": sec_ag * 1e3,
+                       "what": f"entity table row-sharded x{world}; each rank's 1024 queries (subjects in its "
+                               f"shard) -> query rows all_gathered ({world * B * d * 4 / 1e6:.0f} MB) -> global "
+                               f"batch scored against every shard (kge.sharded.score_sp_local)"}
     launch_ms = float(np.mean([a.elapsed_time(b) for a, b in events])) if events else float("nan")
     # back-to-back launches of the same contraction between two HIP events on the launch
     # stream: the kernel's average duration without per-launch event overhead (this is the
     # figure the rocprofv3 kernel-trace average is compared with)
     with torch.no_grad():
-        if world == 1:
-            q = _lib.prep_query(_lib.COMPLEX, _lib.DIR_SP, ent.detach(), s_all[0], rel.detach(), p_all[0], B, d, d)
-            tab = ent.detach()
-        else:
-            q = sharded.queries_local(s_all[0], p_all[0], 0)
-            tab = sharded.ent
+        q = _lib.prep_query(_lib.COMPLEX, _lib.DIR_SP, ent.detach(), s_all[0], rel.detach(), p_all[0], B, d, d)
+        tab = ent.detach()
         out_buf = torch.empty(q.shape[0], tab.shape[0], device=device)
         if prec == _lib.PREC_BF16X3:  # the production path: pre-split Q planes + persistent kernel
             qh, ql = _lib.split_rows(q)
@@ -217,9 +220,9 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         sec, kern_ms, launch_ms = float(t[0]), float(t[1]), float(t[2])
 
-    # roofline of the dominant kernel (the contraction) -- per launch
-    rows_q = B * world
-    cols = E if world == 1 else math.ceil(E / world)
+    # roofline of the dominant kernel (the contraction) -- per launch, per GPU
+    rows_q = B
+    cols = E
     alg_flops = 2.0 * rows_q * cols * d
     alg_bytes = 4.0 * (rows_q * d + cols * d + rows_q * cols)
     k_s = kern_ms / 1e3
@@ -234,7 +237,7 @@ def main():
     # shape at N=1), committed under profiles/; null when absent or for another shape.
     traffic, traffic_src = None, None
     pmc = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r01", "pmc_traffic.json")
-    if world == 1 and args.precision == "bf16x3" and os.path.exists(pmc):
+    if args.precision == "bf16x3" and os.path.exists(pmc):  # same per-GPU launch at every N
         with open(pmc) as f:
             t = json.load(f)
         traffic = int(t["traffic_bytes"])
@@ -242,7 +245,7 @@ def main():
                        f"(read {t['read_bytes'] / 1e6:.1f} MB, write {t['write_bytes'] / 1e6:.1f} MB)")
     roofline = {"bound": "mfma", "achieved": round(achieved, 1), "peak": round(peak, 1), "unit": "TFLOP/s",
                 "frac": round(achieved / peak, 4), "traffic": traffic, "traffic_source": traffic_src,
-                "kernel": "score_dot_persist_kernel" if args.precision == "bf16x3" else "score_dot_kernel", "kernel_us": round(kern_ms * 1e3, 2),
+                "kernel": "score_dot_persist16_kernel" if args.precision == "bf16x3" else "score_dot_kernel", "kernel_us": round(kern_ms * 1e3, 2),
                 "kernel_us_per_launch_events": round(launch_ms * 1e3, 2),
                 "hbm_achieved_GBs": round(alg_bytes / k_s / 1e9, 1),
                 "hbm_frac": round(alg_bytes / k_s / 1e9 / HBM_PEAK_GBS, 4),
@@ -257,9 +260,12 @@ def main():
            "config": {"workload": "configs[1]: ComplEx dim=512 1vsAll FB15K-237, batch 1024, score_sp per step",
                       "model": "complex", "dim": d, "global_batch": B * world, "entities": E,
                       "parallelism": "single GPU" if world == 1 else
-                      f"entity-row-sharded x{world}, shard-affine queries, Q all_gather ({os.environ.get('KGE_DIST_BACKEND', 'nccl')})",
+                      f"dp{world}: queries partitioned over ranks (1024 each), entity table replicated, "
+                      f"no collective in the step",
                       "precision": args.precision},
            "roofline": roofline}
+    if row_sharded is not None:
+        out["row_sharded"] = row_sharded
 
     if rank == 0 and world == 1 and not args.no_extras:
         out["extras"] = extras(args, model, c, E, R, device)
