@@ -1,11 +1,12 @@
 // Persistent bf16x3 contraction S = Q . T^T (the production score_sp / score_po kernel):
 // workgroups loop over output tiles (one tile per CU at the C2 shape).
 //
-// Per tile: Q arrives pre-split as bf16 hi / lo planes, the entity rows are split on the
-// fly; K is staged 32 fp32 columns at a time into a double-buffered, XOR-swizzled LDS
-// image; one barrier per stage; 16x16x32 bf16 MFMA, hi*hi + hi*lo + lo*hi (measured 7 %
-// faster than the 32x32x16 form of the same kernel: the chip holds a higher clock on the
-// 16x16 shape, MI355X_MICROARCH 'DVFS give-back' item 7).  Row-vector epilogue through LDS.
+// Per tile: Q arrives pre-split as bf16 hi / lo planes and is staged by LDS-DMA
+// (global_load_lds_dwordx4); the entity rows are loaded into registers and split on the
+// fly.  K is staged 32 columns at a time into a double-buffered, XOR-swizzled LDS image;
+// one barrier per stage; 16x16x32 bf16 MFMA, hi*hi + hi*lo + lo*hi (measured 7 % faster
+// than the 32x32x16 form of the same kernel: the chip holds a higher clock on the 16x16
+// shape, MI355X_MICROARCH 'DVFS give-back' item 7).  Row-vector epilogue through LDS.
 // Tile order is XCD-grouped: the workgroups that share an XCD take consecutive tiles, i.e.
 // the query tiles of one entity panel, so each panel is read from HBM once per XCD.
 #include "common.h"
@@ -39,86 +40,111 @@ __device__ __forceinline__ int sw16_off(int row, int slot) {
   return row * 64 + ((slot ^ ((0x78 >> (2 * ((row >> 2) & 3))) & 3)) << 4);
 }
 
-template <int BM, int BN, int WM, int WN>
+// VMEM issued from inline asm: hipcc neither counts nor waits for these, the kernel does
+// (mixing LDS-DMA with compiler-visible register loads makes hipcc drain vmcnt to 0 at
+// every use of a loaded register, cdna_hip_programming.md 'Projection GEMM' item 4(b)).
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void glds16_asm(const void* gsrc, unsigned lds_dst) {
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(gsrc), "s"(lds_dst)
+               : "memory");
+}
+__device__ __forceinline__ u32x4 gload16_asm(const void* gsrc) {
+  u32x4 r;
+  asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(r) : "v"(gsrc) : "memory");
+  return r;
+}
+__device__ __forceinline__ unsigned lds_addr(const void* p) {
+  return (unsigned)(uintptr_t)(const __attribute__((address_space(3))) void*)p;
+}
+
+// ABL: dev-only ablation / probe switches (kge_dev_score_dot_persist): 1 = no score stores,
+// 2 = no staging after the prologue, 4 = per-workgroup clock probe written to row n of s.
+template <int BM, int BN, int WM, int WN, int ABL = 0>
 __global__ void __launch_bounds__(64 * WM * WN, 1)
     score_dot_persist16_kernel(const __bf16* __restrict__ qhi, const __bf16* __restrict__ qlo, int64_t ldq,
                                const float* __restrict__ t, int64_t ldt, const int64_t* __restrict__ tidx, int n,
                                int m, int d, float* __restrict__ s, int64_t lds, int nrt, int ntiles) {
   using C = PCfg<BM, BN, WM, WN>;
+  constexpr int NW = C::NT / 64;
   constexpr int TM = BM / WM / 16, TN = BN / WN / 16;  // 16 x 16 tiles per wave
   constexpr int WCOLS = BN / WN;                         // wave tile width
   constexpr int SCR_LD = WCOLS + 4;                      // padded scratch row (floats)
+  constexpr int A_G = BM / 16 / NW;                      // 1-KB A chunks per plane per wave
+  constexpr int XS = TM / 4 > 0 ? TM / 4 : 1;            // bands computed before the staging block
+  static_assert((BM / 16) % NW == 0, "A chunks");
+  static_assert(C::B_PER_T == 4, "KGE_WAIT_VM names 4 registers");
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wr = wave / WN, wc = wave % WN;
   const int fr = lane & 15, fs = lane >> 4;
   const int G = gridDim.x;
   const int xcd = blockIdx.x & 7, per_xcd = G >> 3, local = blockIdx.x >> 3;
   const int nst = (d + BK - 1) / BK;
+  const unsigned smem_base = lds_addr(smem);
+  const int64_t lo_off = qlo - qhi;
+  const uint64_t t_clk0 = (ABL & 4) ? __builtin_amdgcn_s_memtime() : 0;
+  const uint64_t t_rt0 = (ABL & 4) ? __builtin_amdgcn_s_memrealtime() : 0;
 
   for (int it = 0;; ++it) {
     const int tile = it * G + xcd * per_xcd + local;
     if (tile >= ntiles) break;
     const int m0 = (tile % nrt) * BM, n0 = (tile / nrt) * BN;
 
-    const __bf16* a_hi[C::A_PER_T];
-    const __bf16* a_lo[C::A_PER_T];
-    int a_off[C::A_PER_T];
-    unsigned a_mk[C::A_PER_T];
+    // A planes by LDS-DMA: wave-instruction c fills rows 16c .. 16c+15 of a plane (64 B
+    // each, lane-linear destination), so the 16x16x32 read swizzle goes on the source
+    // address.  Rows past n read row n-1: their scores are never stored.
+    const __bf16* ga[A_G];
 #pragma unroll
-    for (int i = 0; i < C::A_PER_T; ++i) {
-      const int c = tid + i * C::NT;
-      const int row = c >> 2, slot = c & 3;
-      const int qi = m0 + row;
-      a_mk[i] = qi < n ? 0xffffffffu : 0u;
-      const int64_t base = (int64_t)(qi < n ? qi : 0) * ldq + slot * 8;
-      a_hi[i] = qhi + base;
-      a_lo[i] = qlo + base;
-      a_off[i] = sw16_off(row, slot);
+    for (int i = 0; i < A_G; ++i) {
+      const int row = (wave * A_G + i) * 16 + (lane >> 2);
+      const int slot = (lane & 3) ^ ((0x78 >> (2 * ((row >> 2) & 3))) & 3);
+      ga[i] = qhi + (int64_t)min(m0 + row, n - 1) * ldq + slot * 8;
     }
+    // B (entity rows, fp32) through registers: float4 f of the stage = row f / 8, cols 4 (f % 8)
     const float* b_src[C::B_PER_T];
     int b_off[C::B_PER_T], b_col[C::B_PER_T];
-    bool b_ok[C::B_PER_T];
 #pragma unroll
     for (int i = 0; i < C::B_PER_T; ++i) {
       const int f = tid + i * C::NT;
       const int row = f >> 3, col = (f & 7) * 4;
-      const int ej = n0 + row;
-      b_ok[i] = ej < m;
-      const int64_t er = b_ok[i] ? (tidx ? tidx[ej] : (int64_t)ej) : 0;
+      const int ej = n0 + row;  // rows past m read row 0: their scores are never stored
+      const int64_t er = ej < m ? (tidx ? tidx[ej] : (int64_t)ej) : 0;
       b_src[i] = t + er * ldt + col;
       b_col[i] = col;
       b_off[i] = sw16_off(row, col >> 3) + ((col >> 2) & 1) * 8;
     }
-    uint4 ra_hi[C::A_PER_T], ra_lo[C::A_PER_T], rb[C::B_PER_T];
-    auto load = [&](int k0) {
+    u32x4 rv[C::B_PER_T];
+
+    // Every VMEM operation of the K loop is inline asm, counted by hand: per stage a wave
+    // issues 2 A_G DMAs (stage st + 1), then B_PER_T register loads (stage st + 2).
+#define KGE_WAIT_VM(N) \
+  asm volatile("s_waitcnt vmcnt(%4)" : "+v"(rv[0]), "+v"(rv[1]), "+v"(rv[2]), "+v"(rv[3]) : "i"(N) : "memory")
+    auto glds_a = [&](int buf, int k0) {
+      const unsigned base = smem_base + buf * C::STAGE;
 #pragma unroll
-      for (int i = 0; i < C::A_PER_T; ++i) {
-        ra_hi[i] = *reinterpret_cast<const uint4*>(a_hi[i] + k0);
-        ra_lo[i] = *reinterpret_cast<const uint4*>(a_lo[i] + k0);
+      for (int i = 0; i < A_G; ++i) {
+        const unsigned c = (unsigned)(wave * A_G + i) * 1024u;
+        glds16_asm(ga[i] + k0, base + c);
+        glds16_asm(ga[i] + lo_off + k0, base + C::PLANE_A + c);
       }
-#pragma unroll
-      for (int i = 0; i < C::B_PER_T; ++i)
-        rb[i] = *reinterpret_cast<const uint4*>(b_src[i] + min(k0, d - 4 - b_col[i]));
     };
-    auto store = [&](unsigned char* st, int k0) {
-      unsigned char* ahi = st;
-      unsigned char* alo = st + C::PLANE_A;
-      unsigned char* bhi = st + 2 * C::PLANE_A;
-      unsigned char* blo = bhi + C::PLANE_B;
+    auto load_b = [&](int k0) {
 #pragma unroll
-      for (int i = 0; i < C::A_PER_T; ++i) {
-        const unsigned mk = a_mk[i];
-        *reinterpret_cast<uint4*>(ahi + a_off[i]) =
-            make_uint4(ra_hi[i].x & mk, ra_hi[i].y & mk, ra_hi[i].z & mk, ra_hi[i].w & mk);
-        *reinterpret_cast<uint4*>(alo + a_off[i]) =
-            make_uint4(ra_lo[i].x & mk, ra_lo[i].y & mk, ra_lo[i].z & mk, ra_lo[i].w & mk);
-      }
+      for (int i = 0; i < C::B_PER_T; ++i) rv[i] = gload16_asm(b_src[i] + min(k0, d - 4 - b_col[i]));
+    };
+    auto store_b = [&](unsigned char* stg, int k0) {  // split fp32 -> bf16 hi / lo, LDS image
+      unsigned char* bhi = stg + 2 * C::PLANE_A;
+      unsigned char* blo = bhi + C::PLANE_B;
+      const bool tail = k0 + BK > d;  // only the K tail needs zeros
 #pragma unroll
       for (int i = 0; i < C::B_PER_T; ++i) {
-        const unsigned mk = (b_ok[i] && k0 + b_col[i] < d) ? 0xffffffffu : 0u;
-        const float4 v = make_float4(__uint_as_float(rb[i].x & mk), __uint_as_float(rb[i].y & mk),
-                                     __uint_as_float(rb[i].z & mk), __uint_as_float(rb[i].w & mk));
+        const unsigned mk = (!tail || k0 + b_col[i] < d) ? 0xffffffffu : 0u;
+        const float4 v = make_float4(__uint_as_float(rv[i].x & mk), __uint_as_float(rv[i].y & mk),
+                                     __uint_as_float(rv[i].z & mk), __uint_as_float(rv[i].w & mk));
         bf16x4 h, l;
         split_bf16x4(v, h, l);
         *reinterpret_cast<bf16x4*>(bhi + b_off[i]) = h;
@@ -132,20 +158,22 @@ __global__ void __launch_bounds__(64 * WM * WN, 1)
 #pragma unroll
       for (int y = 0; y < TN; ++y) acc[x][y] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-    auto compute = [&](const unsigned char* cur) {
-      const unsigned char* ahi = cur;
-      const unsigned char* alo = cur + C::PLANE_A;
+    bf16x8 b_h[TN], b_l[TN];
+    auto compute_b = [&](const unsigned char* cur) {
       const unsigned char* bhi = cur + 2 * C::PLANE_A;
       const unsigned char* blo = bhi + C::PLANE_B;
-      bf16x8 b_h[TN], b_l[TN];
 #pragma unroll
       for (int y = 0; y < TN; ++y) {
         const int rb_ = wc * WCOLS + y * 16 + fr;
         b_h[y] = *reinterpret_cast<const bf16x8*>(bhi + sw16_off(rb_, fs));
         b_l[y] = *reinterpret_cast<const bf16x8*>(blo + sw16_off(rb_, fs));
       }
+    };
+    auto compute_x = [&](const unsigned char* cur, int x0, int x1) {
+      const unsigned char* ahi = cur;
+      const unsigned char* alo = cur + C::PLANE_A;
 #pragma unroll
-      for (int x = 0; x < TM; ++x) {
+      for (int x = x0; x < x1; ++x) {
         const int ra = wr * (BM / WM) + x * 16 + fr;
         const bf16x8 a_h = *reinterpret_cast<const bf16x8*>(ahi + sw16_off(ra, fs));
         const bf16x8 a_l = *reinterpret_cast<const bf16x8*>(alo + sw16_off(ra, fs));
@@ -158,24 +186,36 @@ __global__ void __launch_bounds__(64 * WM * WN, 1)
       }
     };
 
-    load(0);
-    store(smem, 0);
-    if (nst > 1) load(BK);
-    __syncthreads();
-    int st = 0;
-    for (; st + 2 < nst; ++st) {
-      store(smem + ((st + 1) & 1) * C::STAGE, (st + 1) * BK);
-      load((st + 2) * BK);
-      compute(smem + (st & 1) * C::STAGE);
-      __syncthreads();
+    glds_a(0, 0);
+    load_b(0);
+    KGE_WAIT_VM(0);
+    store_b(smem, 0);
+    load_b(nst > 1 ? BK : 0);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    // One barrier per stage.  Stage st + 1 is staged into the other buffer between the first
+    // XS bands of stage st's MFMAs and the rest (measured: 8 % over staging ahead of them).
+    for (int st = 0; st < nst; ++st) {
+      const int nb = (st + 1) & 1;
+      const unsigned char* cur = smem + (st & 1) * C::STAGE;
+      const bool more = !(ABL & 2) && st + 1 < nst;
+      if (more) glds_a(nb, (st + 1) * BK);
+      compute_b(cur);
+      compute_x(cur, 0, XS);
+      if (more) {
+        KGE_WAIT_VM(2 * A_G);  // B(st + 1) has landed
+        store_b(smem + nb * C::STAGE, (st + 1) * BK);
+      }
+      if (!(ABL & 2)) load_b(min(st + 2, nst - 1) * BK);
+      compute_x(cur, XS, TM);
+      KGE_WAIT_VM(C::B_PER_T);  // A(st + 1) has landed
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
     }
-    if (st + 1 < nst) {
-      store(smem + ((st + 1) & 1) * C::STAGE, (st + 1) * BK);
-      compute(smem + (st & 1) * C::STAGE);
-      __syncthreads();
-      ++st;
-    }
-    compute(smem + (st & 1) * C::STAGE);
+    KGE_WAIT_VM(0);
+#undef KGE_WAIT_VM
 
     // epilogue: C/D of 16x16 -- lane holds column (lane & 15), rows 4 (lane >> 4) + r
     __syncthreads();  // stage buffers free: per-wave scratch of 16 rows x WCOLS (+4) floats
@@ -196,7 +236,9 @@ __global__ void __launch_bounds__(64 * WM * WN, 1)
         const int i = i0 + row;
         if (i >= n) continue;
         float* dst = s + (int64_t)i * lds + j;
-        if (j + 3 < m) {
+        if (ABL & 1) {
+          if (v.x == 1234.5f) dst[0] = v.y;  // keep the values live, store (almost) nothing
+        } else if (j + 3 < m) {
           *reinterpret_cast<f32x4u*>(dst) = f32x4u{v.x, v.y, v.z, v.w};
         } else {
           if (j < m) dst[0] = v.x;
@@ -207,9 +249,14 @@ __global__ void __launch_bounds__(64 * WM * WN, 1)
     }
     __syncthreads();  // LDS of this tile is free for the next tile's prologue
   }
+  if ((ABL & 4) && tid == 0) {  // dev: shader clocks and 100-MHz ticks spent by this workgroup
+    const uint64_t c = __builtin_amdgcn_s_memtime() - t_clk0, r = __builtin_amdgcn_s_memrealtime() - t_rt0;
+    s[(int64_t)n * lds + 2 * blockIdx.x] = (float)c;  // the caller allocates row n
+    s[(int64_t)n * lds + 2 * blockIdx.x + 1] = (float)r;
+  }
 }
 
-template <int BM, int BN, int WM, int WN>
+template <int BM, int BN, int WM, int WN, int ABL = 0>
 int launch_persist16(const __bf16* qhi, const __bf16* qlo, int64_t ldq, const float* t, int64_t ldt,
                      const int64_t* tidx, int64_t n, int64_t m, int d, float* s, int64_t lds, hipStream_t st) {
   using C = PCfg<BM, BN, WM, WN>;
@@ -219,7 +266,7 @@ int launch_persist16(const __bf16* qhi, const __bf16* qlo, int64_t ldq, const fl
   const size_t shmem = 2 * C::STAGE;
   static bool attr_set = false;
   if (!attr_set) {
-    hipError_t e = hipFuncSetAttribute((const void*)score_dot_persist16_kernel<BM, BN, WM, WN>,
+    hipError_t e = hipFuncSetAttribute((const void*)score_dot_persist16_kernel<BM, BN, WM, WN, ABL>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)shmem);
     if (e != hipSuccess) return (int)e;
     attr_set = true;
@@ -227,7 +274,7 @@ int launch_persist16(const __bf16* qhi, const __bf16* qlo, int64_t ldq, const fl
   int grid = kge_num_cus();
   grid = (int)std::min<int64_t>(grid, (ntiles + 7) / 8 * 8);
   grid = std::max(8, grid / 8 * 8);
-  score_dot_persist16_kernel<BM, BN, WM, WN><<<dim3(grid), dim3(C::NT), shmem, st>>>(
+  score_dot_persist16_kernel<BM, BN, WM, WN, ABL><<<dim3(grid), dim3(C::NT), shmem, st>>>(
       qhi, qlo, ldq, t, ldt, tidx, (int)n, (int)m, d, s, lds, nrt, (int)ntiles);
   KGE_CHECK_LAUNCH();
   return 0;
@@ -285,7 +332,11 @@ extern "C" int kge_dev_score_dot_persist(int variant, const void* qhi, const voi
   switch (variant) {
     case 0: return launch_persist16<256, 256, 2, 4>(h, l, ldq, t, ldt, tidx, n, m, d, s, lds, st);
     case 1: return launch_persist16<128, 256, 2, 4>(h, l, ldq, t, ldt, tidx, n, m, d, s, lds, st);
-    case 2: return launch_persist16<256, 128, 4, 2>(h, l, ldq, t, ldt, tidx, n, m, d, s, lds, st);
+    case 11: return launch_persist16<256, 256, 2, 4, 1>(h, l, ldq, t, ldt, tidx, n, m, d, s, lds, st);
+    case 12: return launch_persist16<256, 256, 2, 4, 2>(h, l, ldq, t, ldt, tidx, n, m, d, s, lds, st);
+    case 13: return launch_persist16<256, 256, 2, 4, 3>(h, l, ldq, t, ldt, tidx, n, m, d, s, lds, st);
+    case 14: return launch_persist16<256, 256, 2, 4, 4>(h, l, ldq, t, ldt, tidx, n, m, d, s, lds, st);
+    case 17: return launch_persist16<256, 256, 2, 4, 7>(h, l, ldq, t, ldt, tidx, n, m, d, s, lds, st);
     default: return KGE_ERR_ARG;
   }
 }
