@@ -15,7 +15,7 @@ scored against each rank's shard) is timed after the headline loop and reported 
 "row_sharded", together with the cost of its all_gather alone.
 
 Also reported (rank 0): the contraction kernel's roofline from HIP events on the launch stream
-(20 back-to-back launches after the timed region), score_po, a full 1vsAll training step
+(100 back-to-back launches after the timed region), score_po, a full 1vsAll training step
 (sp + po forward/backward + CE + Adagrad), the filtered eval MRR on the synthetic test
 split, and the reference CPU path (oracle/refseq.py: the reference's exact ATen op
 sequence, verified bit-exact against it) timed on this host's cores.
@@ -203,11 +203,11 @@ def main():
             kern = lambda: _lib.score_dot_split(qh, ql, tab, None, d, out=out_buf)  # noqa: E731
         else:
             kern = lambda: _lib.score_dot(q, tab, None, prec, out=out_buf)  # noqa: E731
-        for _ in range(3):
+        for _ in range(20):  # the clock settles under sustained MFMA load
             kern()
         a = torch.cuda.Event(enable_timing=True)
         b = torch.cuda.Event(enable_timing=True)
-        reps = 20
+        reps = 100
         a.record()
         for _ in range(reps):
             kern()
