@@ -31,6 +31,9 @@ extern "C" {
 #define KGE_RESCAL 2   /* kge/model/rescal.py             */
 #define KGE_TRANSE 3   /* kge/model/transe.py             */
 #define KGE_ROTATE 4   /* kge/model/rotate.py             */
+#define KGE_CP 5       /* kge/model/cp.py: query width d_e/2; sp_ contracts with the
+                          entity rows' second half, _po with their first half       */
+#define KGE_SIMPLE 6   /* kge/model/simple.py                                       */
 
 #define KGE_DIR_SP 0 /* (s, p, ?): combine="sp_" */
 #define KGE_DIR_PO 1 /* (?, p, o): combine="_po" */
@@ -62,11 +65,16 @@ const char* kge_error_string(int status);
  *             rescal   s^T M_r              rescal.py:145-151
  *             transe   s + r                transe.py:223
  *             rotate   s * rot(r)           rotate.py:288-297
+ *             cp       s_h * r              cp.py:23  (Q has d_e/2 columns)
+ *             simple   [s_t*r_b | s_h*r_f]/2   simple.py:24-26,34
  *   dir = PO: complex conj(r)*o             complex.py:40
  *             distmult o*r                  distmult.py:85
  *             rescal   M_r o                rescal.py:152-157
  *             transe   o - r                transe.py:225
  *             rotate   o * conj(rot(r))     rotate.py:298-307 (|e*rot - o| = |e - o*conj(rot)|)
+ *             cp       o_t * r              cp.py:25  (Q has d_e/2 columns)
+ *             simple   [o_t*r_f | o_h*r_b]/2   simple.py:28-30,34
+ * (x_h / x_t: first / second half of an entity row; r_f / r_b: of a relation row.)
  * Replaces LookupEmbedder.embed (lookup_embedder.py:91-92) + the per-scorer prologue.
  */
 int kge_prep_query(int model, int dir, const float* ent, int64_t ld_ent,
@@ -195,7 +203,8 @@ int kge_softmax_grad(const float* s, int64_t lds, int64_t n, int64_t m, int64_t 
 /* ---- per-row candidate lists (negative sampling) -------------------------------------
  * out[i, c] = score(Q[i, :], ent[cand[i, c], :])  i in [0, n), c in [0, k), with the
  * semantics of KgeModel.score_spo on the triple the candidate completes (kge_model.py:620-637):
- *   ComplEx / DistMult / RESCAL: <q, e>   (Q from kge_prep_query, either direction)
+ *   ComplEx / DistMult / RESCAL / CP / SimplE: <q, e>   (Q from kge_prep_query, either
+ *            direction; for CP, ent / d are the entity-row window of width d_e/2)
  *   TransE : -|| sigma (q - e) + 1e-6 ||_p, sigma = +1 (dir SP: s+p-o') / -1 (dir PO: s'+p-o)
  *            (F.pairwise_distance, transe.py:221)
  *   RotatE : sum_k |q_k - e_k|_C (p = 1) or its L2 form; (s o rot(p)) - o' / s' o rot(p) - o

@@ -343,7 +343,9 @@ int kind_of(int model) {
   switch (model) {
     case KGE_COMPLEX:
     case KGE_DISTMULT:
-    case KGE_RESCAL: return K_DOT;
+    case KGE_RESCAL:
+    case KGE_CP:  // the caller passes the entity-row window (cp.py:17-19) as ent
+    case KGE_SIMPLE: return K_DOT;
     case KGE_TRANSE: return K_TRANSE;
     case KGE_ROTATE: return K_ROTATE;
     default: return -1;

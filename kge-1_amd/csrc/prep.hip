@@ -54,8 +54,18 @@ __global__ void __launch_bounds__(256) prep_elementwise(const float* __restrict_
                                                          const int64_t* __restrict__ ridx, int d_e, QOut out) {
   const int64_t i = blockIdx.x;
   Rows rw = fetch_rows(ent, ld_ent, eidx, rel, ld_rel, ridx, i);
-  out.pad(i, d_e);
-  if (MODEL == KGE_COMPLEX || MODEL == KGE_ROTATE) {
+  out.pad(i, MODEL == KGE_CP ? d_e / 2 : d_e);
+  if (MODEL == KGE_CP) {  // s_h * r (sp) / o_t * r (po), d_e / 2 columns
+    const int h = d_e / 2;
+    const float* e = rw.e + (DIR == KGE_DIR_SP ? 0 : h);
+    for (int k = threadIdx.x; k < h; k += blockDim.x) out.put(i, k, e[k] * rw.r[k]);
+  } else if (MODEL == KGE_SIMPLE) {  // q[j] = e[j'] r[j'] / 2 (sp), e[j'] r[j] / 2 (po), j' = other half
+    const int h = d_e / 2;
+    for (int j = threadIdx.x; j < d_e; j += blockDim.x) {
+      const int jp = j < h ? j + h : j - h;
+      out.put(i, j, 0.5f * rw.e[jp] * rw.r[DIR == KGE_DIR_SP ? jp : j]);
+    }
+  } else if (MODEL == KGE_COMPLEX || MODEL == KGE_ROTATE) {
     const int h = d_e / 2;
     for (int k = threadIdx.x; k < h; k += blockDim.x) {
       const float a_re = rw.e[k], a_im = rw.e[k + h];
@@ -107,12 +117,29 @@ __global__ void __launch_bounds__(256) prep_elementwise_vec(const float* __restr
       *reinterpret_cast<bf16x4*>(out.lo + i * out.ldp + k) = l;
     }
   };
+  const int qw = MODEL == KGE_CP ? d_e / 2 : d_e;
   if (out.hi)
-    for (int k = d_e + lane * 4; k < out.ldp; k += 256) {  // zero padding to ldp (ldp % 8 == 0)
+    for (int k = qw + lane * 4; k < out.ldp; k += 256) {  // zero padding to ldp (ldp % 8 == 0)
       *reinterpret_cast<bf16x4*>(out.hi + i * out.ldp + k) = bf16x4{};
       *reinterpret_cast<bf16x4*>(out.lo + i * out.ldp + k) = bf16x4{};
     }
-  if (MODEL == KGE_COMPLEX || MODEL == KGE_ROTATE) {
+  auto mul4 = [](float4 a, float4 b, float c) {
+    return make_float4(c * a.x * b.x, c * a.y * b.y, c * a.z * b.z, c * a.w * b.w);
+  };
+  if (MODEL == KGE_CP) {
+    const int h = d_e / 2;
+    const float* e = rw.e + (DIR == KGE_DIR_SP ? 0 : h);
+    for (int k = lane * 4; k < h; k += 256)
+      put4(k, mul4(*reinterpret_cast<const float4*>(e + k), *reinterpret_cast<const float4*>(rw.r + k), 1.f));
+  } else if (MODEL == KGE_SIMPLE) {
+    const int h = d_e / 2;
+    for (int k = lane * 4; k < h; k += 256) {
+      const float4 e0 = *reinterpret_cast<const float4*>(rw.e + k), e1 = *reinterpret_cast<const float4*>(rw.e + k + h);
+      const float4 r0 = *reinterpret_cast<const float4*>(rw.r + k), r1 = *reinterpret_cast<const float4*>(rw.r + k + h);
+      put4(k, mul4(e1, DIR == KGE_DIR_SP ? r1 : r0, 0.5f));
+      put4(k + h, mul4(e0, DIR == KGE_DIR_SP ? r0 : r1, 0.5f));
+    }
+  } else if (MODEL == KGE_COMPLEX || MODEL == KGE_ROTATE) {
     const int h = d_e / 2;
     for (int k = lane * 4; k < h; k += 256) {
       const float4 ar = *reinterpret_cast<const float4*>(rw.e + k), ai = *reinterpret_cast<const float4*>(rw.e + k + h);
@@ -198,7 +225,20 @@ __global__ void __launch_bounds__(256) prep_elementwise_bwd(
   const float* g = dq + i * lddq;
   float* ge = d_ent ? d_ent + (eidx ? eidx[i] : i) * ld_dent : nullptr;
   float* gr = d_rel ? d_rel + (ridx ? ridx[i] : i) * ld_drel : nullptr;
-  if (MODEL == KGE_COMPLEX) {
+  if (MODEL == KGE_CP) {
+    const int h = d_e / 2, off = DIR == KGE_DIR_SP ? 0 : h;
+    for (int k = threadIdx.x; k < h; k += blockDim.x) {
+      atomic_add_row(ge, k + off, g[k] * rw.r[k]);
+      atomic_add_row(gr, k, g[k] * rw.e[k + off]);
+    }
+  } else if (MODEL == KGE_SIMPLE) {
+    const int h = d_e / 2;
+    for (int j = threadIdx.x; j < d_e; j += blockDim.x) {
+      const int jp = j < h ? j + h : j - h, jr = DIR == KGE_DIR_SP ? jp : j;
+      atomic_add_row(ge, jp, 0.5f * g[j] * rw.r[jr]);
+      atomic_add_row(gr, jr, 0.5f * g[j] * rw.e[jp]);
+    }
+  } else if (MODEL == KGE_COMPLEX) {
     const int h = d_e / 2;
     for (int k = threadIdx.x; k < h; k += blockDim.x) {
       const float a_re = rw.e[k], a_im = rw.e[k + h], r_re = rw.r[k], r_im = rw.r[k + h];
@@ -296,8 +336,9 @@ template <int DIR>
 int launch_prep(int model, const float* ent, int64_t ld_ent, const int64_t* eidx, const float* rel,
                 int64_t ld_rel, const int64_t* ridx, int64_t n, int d_e, QOut q, hipStream_t st) {
   dim3 grid((unsigned)n), block(256);
-  const int unit = (model == KGE_COMPLEX || model == KGE_ROTATE) ? d_e / 2 : d_e;
-  const bool vec = model != KGE_RESCAL && (model == KGE_DISTMULT || model == KGE_TRANSE || d_e % 2 == 0) &&
+  const bool halves = model == KGE_COMPLEX || model == KGE_ROTATE || model == KGE_CP || model == KGE_SIMPLE;
+  const int unit = halves ? d_e / 2 : d_e;
+  const bool vec = model != KGE_RESCAL && (!halves || d_e % 2 == 0) &&
                    unit % 4 == 0 && ld_ent % 4 == 0 && ld_rel % 4 == 0 && aligned16(ent) && aligned16(rel) &&
                    (!q.q || (q.ldq % 4 == 0 && aligned16(q.q))) &&
                    (!q.hi || (q.ldp % 8 == 0 && aligned16(q.hi) && aligned16(q.lo)));
@@ -312,6 +353,12 @@ int launch_prep(int model, const float* ent, int64_t ld_ent, const int64_t* eidx
         break;
       case KGE_TRANSE:
         prep_elementwise_vec<KGE_TRANSE, DIR><<<g4, block, 0, st>>>(ent, ld_ent, eidx, rel, ld_rel, ridx, n, d_e, q);
+        break;
+      case KGE_CP:
+        prep_elementwise_vec<KGE_CP, DIR><<<g4, block, 0, st>>>(ent, ld_ent, eidx, rel, ld_rel, ridx, n, d_e, q);
+        break;
+      case KGE_SIMPLE:
+        prep_elementwise_vec<KGE_SIMPLE, DIR><<<g4, block, 0, st>>>(ent, ld_ent, eidx, rel, ld_rel, ridx, n, d_e, q);
         break;
       default:
         prep_elementwise_vec<KGE_ROTATE, DIR><<<g4, block, 0, st>>>(ent, ld_ent, eidx, rel, ld_rel, ridx, n, d_e, q);
@@ -332,6 +379,12 @@ int launch_prep(int model, const float* ent, int64_t ld_ent, const int64_t* eidx
       break;
     case KGE_ROTATE:
       prep_elementwise<KGE_ROTATE, DIR><<<grid, block, 0, st>>>(ent, ld_ent, eidx, rel, ld_rel, ridx, d_e, q);
+      break;
+    case KGE_CP:
+      prep_elementwise<KGE_CP, DIR><<<grid, block, 0, st>>>(ent, ld_ent, eidx, rel, ld_rel, ridx, d_e, q);
+      break;
+    case KGE_SIMPLE:
+      prep_elementwise<KGE_SIMPLE, DIR><<<grid, block, 0, st>>>(ent, ld_ent, eidx, rel, ld_rel, ridx, d_e, q);
       break;
     case KGE_RESCAL:
       prep_rescal<DIR><<<grid, block, d_e * sizeof(float), st>>>(ent, ld_ent, eidx, rel, ld_rel, ridx, d_e, q);
@@ -357,6 +410,8 @@ int launch_prep_bwd(int model, const float* ent, int64_t ld_ent, const int64_t* 
     case KGE_DISTMULT: KGE_PB(KGE_DISTMULT); break;
     case KGE_TRANSE: KGE_PB(KGE_TRANSE); break;
     case KGE_ROTATE: KGE_PB(KGE_ROTATE); break;
+    case KGE_CP: KGE_PB(KGE_CP); break;
+    case KGE_SIMPLE: KGE_PB(KGE_SIMPLE); break;
     case KGE_RESCAL:
       prep_rescal_bwd<DIR><<<grid, block, 2 * d_e * sizeof(float), st>>>(
           ent, ld_ent, eidx, rel, ld_rel, ridx, d_e, dq, lddq, d_ent, ld_dent, d_rel, ld_drel);
@@ -377,9 +432,13 @@ int check_dims(int model, int d_e, int d_r) {
     case KGE_TRANSE: return d_r == d_e ? 0 : KGE_ERR_ARG;
     case KGE_ROTATE: return (d_e % 2 == 0 && d_r == d_e / 2) ? 0 : KGE_ERR_ARG;
     case KGE_RESCAL: return (d_r == d_e * d_e && d_e <= 8192) ? 0 : KGE_ERR_ARG;
+    case KGE_CP: return (d_e % 2 == 0 && d_r == d_e / 2) ? 0 : KGE_ERR_ARG;
+    case KGE_SIMPLE: return (d_e % 2 == 0 && d_r == d_e) ? 0 : KGE_ERR_ARG;
     default: return KGE_ERR_ARG;
   }
 }
+
+int query_width(int model, int d_e) { return model == KGE_CP ? d_e / 2 : d_e; }
 
 }  // namespace
 
@@ -396,8 +455,8 @@ extern "C" int kge_prep_query_split(int model, int dir, const float* ent, int64_
                                     void* stream) {
   if (int e = check_dims(model, d_e, d_r)) return e;
   KGE_REQUIRE(n >= 0 && ent && rel && (q || q_hi));
-  KGE_REQUIRE(!q || ldq >= d_e);
-  KGE_REQUIRE(!q_hi || (q_lo && ldp >= d_e && ldp % 8 == 0));
+  KGE_REQUIRE(!q || ldq >= query_width(model, d_e));
+  KGE_REQUIRE(!q_hi || (q_lo && ldp >= query_width(model, d_e) && ldp % 8 == 0));
   if (n == 0) return 0;
   QOut out{q, ldq, (__bf16*)q_hi, (__bf16*)q_lo, ldp};
   hipStream_t st = as_stream(stream);

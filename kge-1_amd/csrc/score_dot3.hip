@@ -21,10 +21,8 @@ struct PCfg {
   static constexpr int PLANE_A = BM * BK * 2;
   static constexpr int PLANE_B = BN * BK * 2;
   static constexpr int STAGE = 2 * PLANE_A + 2 * PLANE_B;
-  static constexpr int A_PER_T = BM * 4 / NT;
-  static constexpr int B_PER_T = BN * 8 / NT;
-  static_assert(BM * 4 % NT == 0 && BN * 8 % NT == 0, "staging");
-  static_assert(BM % (32 * WM) == 0 && BN % (32 * WN) == 0, "tile");
+  static constexpr int B_PER_T = (BN * 8 + NT - 1) / NT;  // float4 slots per thread (last may idle)
+  static_assert(BM % (16 * WM) == 0 && BN % (16 * WN) == 0, "tile");
 };
 
 typedef float f32x4u __attribute__((ext_vector_type(4), aligned(4)));  // 4-B-aligned float4
@@ -105,17 +103,20 @@ __global__ void __launch_bounds__(64 * WM * WN, 1)
       ga[i] = qhi + (int64_t)min(m0 + row, n - 1) * ldq + slot * 8;
     }
     // B (entity rows, fp32) through registers: float4 f of the stage = row f / 8, cols 4 (f % 8)
+    // slot i of thread tid: row tid / 8 + i NT / 8, columns 4 (tid % 8) .. +3; NT / 8 is a
+    // multiple of 16 rows, so the swizzle term is the same for every slot
+    static_assert(C::NT % 128 == 0, "B slot stride");
     const float* b_src[C::B_PER_T];
-    int b_off[C::B_PER_T], b_col[C::B_PER_T];
+    constexpr bool B_RAGGED = BN * 8 % C::NT != 0;  // the last slot of some threads idles
+    const bool b_last = !B_RAGGED || tid + (C::B_PER_T - 1) * C::NT < BN * 8;
+    const int b_col = (tid & 7) * 4;
+    const int b_off0 = sw16_off(tid >> 3, b_col >> 3) + ((b_col >> 2) & 1) * 8;
 #pragma unroll
     for (int i = 0; i < C::B_PER_T; ++i) {
-      const int f = tid + i * C::NT;
-      const int row = f >> 3, col = (f & 7) * 4;
+      const int row = min((tid >> 3) + i * (C::NT / 8), BN - 1);
       const int ej = n0 + row;  // rows past m read row 0: their scores are never stored
       const int64_t er = ej < m ? (tidx ? tidx[ej] : (int64_t)ej) : 0;
-      b_src[i] = t + er * ldt + col;
-      b_col[i] = col;
-      b_off[i] = sw16_off(row, col >> 3) + ((col >> 2) & 1) * 8;
+      b_src[i] = t + er * ldt + b_col;
     }
     u32x4 rv[C::B_PER_T];
 
@@ -134,7 +135,7 @@ __global__ void __launch_bounds__(64 * WM * WN, 1)
     };
     auto load_b = [&](int k0) {
 #pragma unroll
-      for (int i = 0; i < C::B_PER_T; ++i) rv[i] = gload16_asm(b_src[i] + min(k0, d - 4 - b_col[i]));
+      for (int i = 0; i < C::B_PER_T; ++i) rv[i] = gload16_asm(b_src[i] + min(k0, d - 4 - b_col));
     };
     auto store_b = [&](unsigned char* stg, int k0) {  // split fp32 -> bf16 hi / lo, LDS image
       unsigned char* bhi = stg + 2 * C::PLANE_A;
@@ -142,13 +143,14 @@ __global__ void __launch_bounds__(64 * WM * WN, 1)
       const bool tail = k0 + BK > d;  // only the K tail needs zeros
 #pragma unroll
       for (int i = 0; i < C::B_PER_T; ++i) {
-        const unsigned mk = (!tail || k0 + b_col[i] < d) ? 0xffffffffu : 0u;
+        const unsigned mk = (!tail || k0 + b_col < d) ? 0xffffffffu : 0u;
         const float4 v = make_float4(__uint_as_float(rv[i].x & mk), __uint_as_float(rv[i].y & mk),
                                      __uint_as_float(rv[i].z & mk), __uint_as_float(rv[i].w & mk));
         bf16x4 h, l;
         split_bf16x4(v, h, l);
-        *reinterpret_cast<bf16x4*>(bhi + b_off[i]) = h;
-        *reinterpret_cast<bf16x4*>(blo + b_off[i]) = l;
+        if (i == C::B_PER_T - 1 && !b_last) continue;
+        *reinterpret_cast<bf16x4*>(bhi + b_off0 + i * (C::NT / 8) * 64) = h;
+        *reinterpret_cast<bf16x4*>(blo + b_off0 + i * (C::NT / 8) * 64) = l;
       }
     };
 
@@ -186,6 +188,35 @@ __global__ void __launch_bounds__(64 * WM * WN, 1)
       }
     };
 
+    // WN == 1 (a wave spans the tile's columns): A fragments of the wave's TM bands are read
+    // once per stage and the B fragments stream through, y-outer
+    bf16x8 a_hf[TM], a_lf[TM];
+    auto compute_a = [&](const unsigned char* cur) {
+#pragma unroll
+      for (int x = 0; x < TM; ++x) {
+        const int ra = wr * (BM / WM) + x * 16 + fr;
+        a_hf[x] = *reinterpret_cast<const bf16x8*>(cur + sw16_off(ra, fs));
+        a_lf[x] = *reinterpret_cast<const bf16x8*>(cur + C::PLANE_A + sw16_off(ra, fs));
+      }
+    };
+    auto compute_y = [&](const unsigned char* cur, int y0, int y1) {
+      const unsigned char* bhi = cur + 2 * C::PLANE_A;
+      const unsigned char* blo = bhi + C::PLANE_B;
+#pragma unroll
+      for (int y = y0; y < y1; ++y) {
+        const int rb_ = y * 16 + fr;
+        const bf16x8 bh = *reinterpret_cast<const bf16x8*>(bhi + sw16_off(rb_, fs));
+        const bf16x8 bl = *reinterpret_cast<const bf16x8*>(blo + sw16_off(rb_, fs));
+#pragma unroll
+        for (int x = 0; x < TM; ++x) {
+          acc[x][y] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a_lf[x], bh, acc[x][y], 0, 0, 0);
+          acc[x][y] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a_hf[x], bl, acc[x][y], 0, 0, 0);
+          acc[x][y] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a_hf[x], bh, acc[x][y], 0, 0, 0);
+        }
+      }
+    };
+    constexpr int YS = TN / 4 > 0 ? TN / 4 : 1;  // y-outer: columns before the staging block
+
     glds_a(0, 0);
     load_b(0);
     KGE_WAIT_VM(0);
@@ -201,14 +232,22 @@ __global__ void __launch_bounds__(64 * WM * WN, 1)
       const unsigned char* cur = smem + (st & 1) * C::STAGE;
       const bool more = !(ABL & 2) && st + 1 < nst;
       if (more) glds_a(nb, (st + 1) * BK);
-      compute_b(cur);
-      compute_x(cur, 0, XS);
+      if constexpr (WN == 1) {
+        compute_a(cur);
+        compute_y(cur, 0, YS);
+      } else {
+        compute_b(cur);
+        compute_x(cur, 0, XS);
+      }
       if (more) {
         KGE_WAIT_VM(2 * A_G);  // B(st + 1) has landed
         store_b(smem + nb * C::STAGE, (st + 1) * BK);
       }
       if (!(ABL & 2)) load_b(min(st + 2, nst - 1) * BK);
-      compute_x(cur, XS, TM);
+      if constexpr (WN == 1)
+        compute_y(cur, YS, TN);
+      else
+        compute_x(cur, XS, TM);
       KGE_WAIT_VM(C::B_PER_T);  // A(st + 1) has landed
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
@@ -228,12 +267,14 @@ __global__ void __launch_bounds__(64 * WM * WN, 1)
 #pragma unroll
         for (int r = 0; r < 4; ++r) scr[(4 * fs + r) * SCR_LD + y * 16 + fr] = acc[x][y][r];
       const int i0 = m0 + wr * (BM / WM) + x * 16;
-      const int j = n0 + wc * WCOLS + (lane % LPR) * 4;
 #pragma unroll
-      for (int pass = 0; pass < 16 * LPR / 64; ++pass) {
-        const int row = pass * (64 / LPR) + lane / LPR;
-        const float4 v = *reinterpret_cast<const float4*>(scr + row * SCR_LD + (lane % LPR) * 4);
+      for (int pass = 0; pass < (16 * LPR + 63) / 64; ++pass) {
+        const int g = pass * 64 + lane;  // float4 g of the band: row g / LPR, column 4 (g % LPR)
+        const int row = g / LPR, c4 = g % LPR;
         const int i = i0 + row;
+        if ((16 * LPR) % 64 != 0 && g >= 16 * LPR) continue;
+        const float4 v = *reinterpret_cast<const float4*>(scr + row * SCR_LD + c4 * 4);
+        const int j = n0 + wc * WCOLS + c4 * 4;
         if (i >= n) continue;
         float* dst = s + (int64_t)i * lds + j;
         if (ABL & 1) {
@@ -337,6 +378,10 @@ extern "C" int kge_dev_score_dot_persist(int variant, const void* qhi, const voi
     case 13: return launch_persist16<256, 256, 2, 4, 3>(h, l, ldq, t, ldt, tidx, n, m, d, s, lds, st);
     case 14: return launch_persist16<256, 256, 2, 4, 4>(h, l, ldq, t, ldt, tidx, n, m, d, s, lds, st);
     case 17: return launch_persist16<256, 256, 2, 4, 7>(h, l, ldq, t, ldt, tidx, n, m, d, s, lds, st);
+    case 20: return launch_persist16<256, 240, 8, 1>(h, l, ldq, t, ldt, tidx, n, m, d, s, lds, st);
+    case 21: return launch_persist16<256, 240, 8, 1, 1>(h, l, ldq, t, ldt, tidx, n, m, d, s, lds, st);
+    case 22: return launch_persist16<256, 256, 8, 1>(h, l, ldq, t, ldt, tidx, n, m, d, s, lds, st);
+    case 24: return launch_persist16<256, 240, 8, 1, 4>(h, l, ldq, t, ldt, tidx, n, m, d, s, lds, st);
     default: return KGE_ERR_ARG;
   }
 }

@@ -45,6 +45,15 @@ __global__ void __launch_bounds__(NT) spo_kernel(float l_norm, const float* __re
     }
   } else if (MODEL == KGE_DISTMULT) {
     for (int k = lane; k < d_e; k += 64) acc = fmaf(t.s[k] * t.p[k], t.o[k], acc);
+  } else if (MODEL == KGE_CP) {  // sum s_h p o_t (cp.py:21)
+    const int h = d_e / 2;
+    for (int k = lane; k < h; k += 64) acc = fmaf(t.s[k] * t.p[k], t.o[k + h], acc);
+  } else if (MODEL == KGE_SIMPLE) {  // (sum s_h p_f o_t + sum s_t p_b o_h) / 2 (simple.py:21-23,34)
+    const int h = d_e / 2;
+    for (int k = lane; k < h; k += 64) {
+      acc = fmaf(t.s[k] * t.p[k], t.o[k + h], acc);
+      acc = fmaf(t.s[k + h] * t.p[k + h], t.o[k], acc);
+    }
   } else if (MODEL == KGE_RESCAL) {  // s^T M o, M = p.view(d, d)
     for (int a = 0; a < d_e; ++a) {
       float row = 0.f;
@@ -72,6 +81,7 @@ __global__ void __launch_bounds__(NT) spo_kernel(float l_norm, const float* __re
   if (lane == 0) {
     if (MODEL == KGE_TRANSE) acc = -((l_norm == 1.f) ? acc : sqrtf(acc));
     if (MODEL == KGE_ROTATE && l_norm != 1.f) acc = sqrtf(acc);
+    if (MODEL == KGE_SIMPLE) acc *= 0.5f;
     out[i] = acc;
   }
 }
@@ -114,6 +124,26 @@ __global__ void __launch_bounds__(NT) spo_bwd_kernel(float l_norm, const float* 
       add(gs, k, gi * p * o);
       add(gp, k, gi * s * o);
       add(go, k, gi * s * p);
+    }
+  } else if (MODEL == KGE_CP) {
+    const int h = d_e / 2;
+    for (int k = lane; k < h; k += 64) {
+      const float s = t.s[k], p = t.p[k], o = t.o[k + h];
+      add(gs, k, gi * p * o);
+      add(gp, k, gi * s * o);
+      add(go, k + h, gi * s * p);
+    }
+  } else if (MODEL == KGE_SIMPLE) {
+    const int h = d_e / 2;
+    const float g2 = 0.5f * gi;
+    for (int k = lane; k < h; k += 64) {
+      const float sh = t.s[k], st = t.s[k + h], pf = t.p[k], pb = t.p[k + h], oh = t.o[k], ot = t.o[k + h];
+      add(gs, k, g2 * pf * ot);
+      add(gs, k + h, g2 * pb * oh);
+      add(gp, k, g2 * sh * ot);
+      add(gp, k + h, g2 * st * oh);
+      add(go, k, g2 * st * pb);
+      add(go, k + h, g2 * sh * pf);
     }
   } else if (MODEL == KGE_RESCAL) {
     for (int a = 0; a < d_e; ++a) {
@@ -190,6 +220,8 @@ int check(int model, int d_e, int d_r) {
     case KGE_TRANSE: return d_r == d_e ? 0 : KGE_ERR_ARG;
     case KGE_ROTATE: return (d_e % 2 == 0 && d_r == d_e / 2) ? 0 : KGE_ERR_ARG;
     case KGE_RESCAL: return d_r == d_e * d_e ? 0 : KGE_ERR_ARG;
+    case KGE_CP: return (d_e % 2 == 0 && d_r == d_e / 2) ? 0 : KGE_ERR_ARG;
+    case KGE_SIMPLE: return (d_e % 2 == 0 && d_r == d_e) ? 0 : KGE_ERR_ARG;
     default: return KGE_ERR_ARG;
   }
 }
@@ -211,6 +243,8 @@ extern "C" int kge_score_spo(int model, float l_norm, const float* ent, int64_t 
     case KGE_DISTMULT: KGE_S(KGE_DISTMULT); break;
     case KGE_RESCAL: KGE_S(KGE_RESCAL); break;
     case KGE_TRANSE: KGE_S(KGE_TRANSE); break;
+    case KGE_CP: KGE_S(KGE_CP); break;
+    case KGE_SIMPLE: KGE_S(KGE_SIMPLE); break;
     default: KGE_S(KGE_ROTATE); break;
   }
 #undef KGE_S
@@ -236,6 +270,8 @@ extern "C" int kge_score_spo_bwd(int model, float l_norm, const float* ent, int6
     case KGE_DISTMULT: KGE_S(KGE_DISTMULT); break;
     case KGE_RESCAL: KGE_S(KGE_RESCAL); break;
     case KGE_TRANSE: KGE_S(KGE_TRANSE); break;
+    case KGE_CP: KGE_S(KGE_CP); break;
+    case KGE_SIMPLE: KGE_S(KGE_SIMPLE); break;
     default: KGE_S(KGE_ROTATE); break;
   }
 #undef KGE_S

@@ -16,7 +16,12 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libkgescore.so")
 
 # enums (kgescore.h)
-COMPLEX, DISTMULT, RESCAL, TRANSE, ROTATE = range(5)
+COMPLEX, DISTMULT, RESCAL, TRANSE, ROTATE, CP, SIMPLE = range(7)
+
+
+def query_width(model: int, d_e: int) -> int:
+    """Columns of the prepared query rows: CP contracts half an entity row (cp.py:17-19)."""
+    return d_e // 2 if model == CP else d_e
 DIR_SP, DIR_PO = 0, 1
 PREC_FP32, PREC_BF16X3 = 0, 1
 DIST_L1, DIST_L2, DIST_ROT_L1, DIST_ROT_L2 = range(4)
@@ -149,20 +154,21 @@ def prep_query(model, direction, ent, eidx, rel, ridx, n, d_e, d_r, out=None):
     eidx, ridx = idx64(eidx), idx64(ridx)
     check_index(eidx, ent.shape[0], "entity index")
     check_index(ridx, rel.shape[0], "relation index")
-    q = out if out is not None else torch.empty(n, d_e, device=ent.device, dtype=torch.float32)
+    q = out if out is not None else torch.empty(n, query_width(model, d_e), device=ent.device, dtype=torch.float32)
     _check(lib().kge_prep_query(model, direction, ptr(ent), rows(ent), ptr(eidx), ptr(rel), rows(rel),
                                 ptr(ridx), n, d_e, d_r, ptr(q), rows(q), stream()), "kge_prep_query")
     return q
 
 
 def prep_query_split(model, direction, ent, eidx, rel, ridx, n, d_e, d_r, want_fp32=True):
-    """Query rows as fp32 (optional) plus bf16 hi / lo planes [n, round32(d_e)] in one pass."""
+    """Query rows as fp32 (optional) plus bf16 hi / lo planes [n, round32(width)] in one pass."""
     require_device(ent, rel)
     eidx, ridx = idx64(eidx), idx64(ridx)
     check_index(eidx, ent.shape[0], "entity index")
     check_index(ridx, rel.shape[0], "relation index")
-    ldp = (d_e + 31) // 32 * 32
-    q = torch.empty(n, d_e, device=ent.device, dtype=torch.float32) if want_fp32 else None
+    qw = query_width(model, d_e)
+    ldp = (qw + 31) // 32 * 32
+    q = torch.empty(n, qw, device=ent.device, dtype=torch.float32) if want_fp32 else None
     hi = torch.empty(n, ldp, device=ent.device, dtype=torch.bfloat16)
     lo = torch.empty_like(hi)
     _check(lib().kge_prep_query_split(model, direction, ptr(ent), rows(ent), ptr(eidx), ptr(rel), rows(rel),

@@ -20,7 +20,17 @@ import torch
 
 from . import _lib as L
 
-BILINEAR = (L.COMPLEX, L.DISTMULT, L.RESCAL)
+BILINEAR = (L.COMPLEX, L.DISTMULT, L.RESCAL, L.CP, L.SIMPLE)
+
+
+def window(kind: int, direction: int, t: torch.Tensor) -> torch.Tensor:
+    """The columns of the candidate rows a query contracts with (a view): CP scores
+    subjects with the first half of an entity row and objects with the second (cp.py:17-19),
+    so sp_ reads t[:, d/2:] and _po t[:, :d/2]; every other model the whole row."""
+    if kind == L.CP:
+        h = t.shape[1] // 2
+        return t[:, h:] if direction == L.DIR_SP else t[:, :h]
+    return t
 
 #: When set to a list, every all-entities contraction launch appends a pair of HIP events
 #: recorded on the launching stream right before / after it (bench.py's kernel timing).
@@ -64,17 +74,18 @@ def _scores_forward(ctx, kind, direction, precision, l_norm, ent, eidx, rel, rid
     d_e, d_r = ent.shape[1], rel.shape[1]
     if tab.shape[1] != d_e:
         raise ValueError(f"candidate dim {tab.shape[1]} != entity dim {d_e}")
-    if kind in BILINEAR and L.split_ok(d_e, tab, precision):
+    qw, tab_w = L.query_width(kind, d_e), window(kind, direction, tab)
+    if kind in BILINEAR and L.split_ok(qw, tab_w, precision):
         # one pass emits Q (kept for backward only when a gradient is needed) and its
         # bf16 hi / lo planes for the split contraction
         need_q = any(ctx.needs_input_grad[i] for i in (4, 6, 8))
         q, q_hi, q_lo = L.prep_query_split(kind, direction, ent, eidx, rel, ridx, n, d_e, d_r, need_q)
-        s = _timed(L.score_dot_split, q_hi, q_lo, tab, tidx, d_e, out=out)
+        s = _timed(L.score_dot_split, q_hi, q_lo, tab_w, tidx, qw, out=out)
         if q is None:
             q = q_hi.new_empty(0)
     elif kind in BILINEAR:
         q = L.prep_query(kind, direction, ent, eidx, rel, ridx, n, d_e, d_r)
-        s = _timed(L.contract, q, tab, tidx, precision, out=out)
+        s = _timed(L.contract, q, tab_w, tidx, precision, out=out)
     else:
         q = L.prep_query(kind, direction, ent, eidx, rel, ridx, n, d_e, d_r)
         dk, sign = dist_kind(kind, l_norm)
@@ -94,11 +105,12 @@ def _scores_backward(ctx, g, ent, eidx, rel, ridx, tab, tidx, q, gscale=None):
     dq = torch.zeros_like(q) if (need_ent or need_rel) else None
     if kind in BILINEAR:
         if dq is not None:
-            L.score_dot_bwd_q(g, tab, tidx, precision, dq=dq, accumulate=False)
+            L.score_dot_bwd_q(g, window(kind, direction, tab), tidx, precision, dq=dq, accumulate=False)
             if gscale is not None:
                 dq.mul_(gscale)
         if d_tab is not None:
-            L.score_dot_bwd_t(g, q if gscale is None else q * gscale, tidx, d_tab, precision)
+            L.score_dot_bwd_t(g, q if gscale is None else q * gscale, tidx, window(kind, direction, d_tab),
+                              precision)
     else:
         dk, sign = dist_kind(kind, l_norm)
         L.score_dist_bwd(dk, sign, g if gscale is None else g * gscale, q, tab, tidx, dq, d_tab)
@@ -210,7 +222,7 @@ class _ScoreCand(torch.autograd.Function):
         n = eidx.numel()
         d_e, d_r = ent.shape[1], rel.shape[1]
         q = L.prep_query(kind, direction, ent, eidx, rel, ridx, n, d_e, d_r)
-        s = L.score_cand(kind, l_norm, direction, q, ent, cand)
+        s = L.score_cand(kind, l_norm, direction, q, window(kind, direction, ent), cand)
         ctx.meta = (kind, direction, l_norm, n, d_e, d_r)
         ctx.save_for_backward(ent, eidx, rel, ridx, cand, q, s)
         return s
@@ -225,8 +237,11 @@ class _ScoreCand(torch.autograd.Function):
         dq = torch.empty_like(q) if (need_ent or need_rel) else None
         g = _rows(g.float())
         # candidate rows repeat across queries: grouped per entity (sort) instead of atomics
-        ent_done = d_ent is not None and L.score_cand_bwd_ent(kind, l_norm, direction, q, ent, cand, s, g, d_ent)
-        L.score_cand_bwd(kind, l_norm, direction, q, ent, cand, s, g, dq, None if ent_done else d_ent)
+        ent_w = window(kind, direction, ent)
+        d_ent_w = window(kind, direction, d_ent) if d_ent is not None else None
+        ent_done = d_ent is not None and L.score_cand_bwd_ent(kind, l_norm, direction, q, ent_w, cand, s, g,
+                                                              d_ent_w)
+        L.score_cand_bwd(kind, l_norm, direction, q, ent_w, cand, s, g, dq, None if ent_done else d_ent_w)
         if dq is not None:
             L.prep_query_bwd(kind, direction, ent, eidx, rel, ridx, n, d_e, d_r, dq, d_ent, d_rel)
         return None, None, None, d_ent, None, d_rel, None, None

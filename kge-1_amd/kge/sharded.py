@@ -105,6 +105,13 @@ class RowShardedScorer:
         self.rank = dist.get_rank(group)
 
     # ---------------------------------------------------------------- helpers
+    def _win(self, direction: int, t: torch.Tensor) -> torch.Tensor:
+        """Entity-row columns the queries of this direction contract with (CP: a half)."""
+        from .engine import window
+
+        kind = getattr(self.ops, "kind", None)
+        return t if kind is None else window(kind, direction, t)
+
     def _all_gather_1d(self, x: torch.Tensor) -> torch.Tensor:
         out = [torch.empty_like(x) for _ in range(self.world)]
         dist.all_gather(out, x.contiguous(), group=self.group)
@@ -137,7 +144,7 @@ class RowShardedScorer:
     def score_sp(self, s: torch.Tensor, p: torch.Tensor, direction: int = 0) -> torch.Tensor:
         """Local shard of the global score matrix: [W*B, hi - lo]."""
         q, _, _ = self.queries(s, p, direction)
-        return self.ops.score(q, self.ent)
+        return self.ops.score(q, self._win(direction, self.ent))
 
     def queries_local(self, e: torch.Tensor, p: torch.Tensor, direction: int = 0) -> torch.Tensor:
         """Shard-affine batches (a loader that routes each query to the rank owning its
@@ -154,7 +161,7 @@ class RowShardedScorer:
 
     def score_sp_local(self, s: torch.Tensor, p: torch.Tensor, direction: int = 0) -> torch.Tensor:
         """score_sp for shard-affine batches: [W*B, hi - lo] local slice of the scores."""
-        return self.ops.score(self.queries_local(s, p, direction), self.ent)
+        return self.ops.score(self.queries_local(s, p, direction), self._win(direction, self.ent))
 
     def topk(self, scores_local: torch.Tensor, k: int):
         """All-gather of per-shard top-k (score, global entity id), merged on every rank."""
@@ -201,7 +208,7 @@ class RowShardedScorer:
             q = torch.where(owned[:, None], q, torch.zeros_like(q))
             dist.all_reduce(q, group=self.group)
             buf = torch.empty(n, (E_k + 3) // 4 * 4, device=q.device, dtype=torch.float32)
-            logits = self.ops.score(q, self.ent, out=buf[:, :E_k])
+            logits = self.ops.score(q, self._win(direction, self.ent), out=buf[:, :E_k])
             mx, sm, tg = self.ops.row_stats(logits, self.lo, labels)
             M = mx.clone()
             dist.all_reduce(M, op=dist.ReduceOp.MAX, group=self.group)
@@ -212,7 +219,7 @@ class RowShardedScorer:
             loss += ((lse - tg).double().sum() * scale)
             g = self.ops.softmax_grad(logits, self.lo, labels, lse, scale, logits)
             dq = torch.empty_like(q)
-            self.ops.score_bwd(g, q, self.ent, dq, d_ent)
+            self.ops.score_bwd(g, q, self._win(direction, self.ent), dq, self._win(direction, d_ent))
             dist.all_reduce(dq, group=self.group)
             dq = torch.where(owned[:, None], dq, torch.zeros_like(dq))
             self.ops.prep_bwd(direction, self.ent, local, self.rel, p_all, dq, d_ent, d_rel)
@@ -232,7 +239,7 @@ class RowShardedScorer:
         counts = torch.zeros(2, 2, 3 * B, dtype=torch.int64, device=s.device)
         for di, (eidx, direction, tgt, f, t) in enumerate(((ar, 0, o, f_sp, t_sp), (ar + B, 1, s, f_po, t_po))):
             q = self.ops.prep(direction, rows, eidx, self.rel, p)
-            sc = self.ops.score(q, self.ent)
+            sc = self.ops.score(q, self._win(direction, self.ent))
             self.ops.rank_counts(sc, self.lo, tgt, true, f[0], f[1], t[0] if t is not None else None,
                                  t[1] if t is not None else None, counts[di, 0], counts[di, 1])
         dist.all_reduce(counts, group=self.group)

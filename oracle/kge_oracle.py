@@ -20,7 +20,7 @@ from typing import Dict, List, Optional, Sequence, Tuple
 
 import numpy as np
 
-BILINEAR = ("complex", "distmult", "rescal")
+BILINEAR = ("complex", "distmult", "rescal", "cp", "simple")
 DISTANCE = ("transe", "rotate")
 PAIRWISE_EPS = 1e-6  # torch.nn.functional.pairwise_distance default eps
 
@@ -50,15 +50,34 @@ def _lp(x, p, axis=-1):
 # Every bilinear scorer is "prep + one contraction with the entity table".
 
 
+def window(model: str, direction: str, e: np.ndarray) -> np.ndarray:
+    """The columns of a candidate entity row that the query contracts with: CP scores
+    subjects with the first half and objects with the second (cp.py:17-19), so sp_
+    contracts with e[d/2:] and _po with e[:d/2]; every other model uses the whole row."""
+    if model == "cp":
+        h = e.shape[-1] // 2
+        return e[..., h:] if direction == "sp_" else e[..., :h]
+    return e
+
+
 def prep_sp(model: str, s: np.ndarray, r: np.ndarray) -> np.ndarray:
-    """Query vector q such that score(s, r, e) = q . e for every entity e.
+    """Query vector q such that score(s, r, e) = q . window(e) for every entity e.
 
     complex  -- complex.py:31-38: (s_all * r_all) @ o_all^T with
                s_all=[s_re,s_im,s_re,s_im], r_all=[r_re,r_re,r_im,-r_im],
                o_all=[o_re,o_im,o_im,o_re]  ==  cmul(s, r) . [e_re | e_im].
     distmult -- distmult.py:83: (s * p) @ o^T.
     rescal   -- rescal.py:145-151: s^T M_r, M_r = p.view(d, d) (row-major).
+    cp       -- cp.py:23: (s_h * p) @ o_t^T.
+    simple   -- simple.py:24-26,34: ((s_h * p_f) @ o_t^T + (s_t * p_b) @ o_h^T) / 2
+               == 0.5 [s_t * p_b | s_h * p_f] . [e_h | e_t].
     """
+    if model == "cp":
+        return _halves(s)[0] * r
+    if model == "simple":
+        s_h, s_t = _halves(s)
+        r_f, r_b = _halves(r)
+        return 0.5 * _cat(s_t * r_b, s_h * r_f)
     if model == "complex":
         s_re, s_im = _halves(s)
         r_re, r_im = _halves(r)
@@ -78,7 +97,16 @@ def prep_po(model: str, r: np.ndarray, o: np.ndarray) -> np.ndarray:
     complex  -- complex.py:40: (r_all * o_all) @ s_all^T == conj(r) * o.
     distmult -- distmult.py:85: (o * p) @ s^T.
     rescal   -- rescal.py:152-157: M_r o.
+    cp       -- cp.py:25: (o_t * p) @ s_h^T.
+    simple   -- simple.py:28-30,34: ((o_t * p_f) @ s_h^T + (o_h * p_b) @ s_t^T) / 2
+               == 0.5 [o_t * p_f | o_h * p_b] . [e_h | e_t].
     """
+    if model == "cp":
+        return _halves(o)[1] * r
+    if model == "simple":
+        o_h, o_t = _halves(o)
+        r_f, r_b = _halves(r)
+        return 0.5 * _cat(o_t * r_f, o_h * r_b)
     if model == "complex":
         r_re, r_im = _halves(r)
         o_re, o_im = _halves(o)
@@ -114,11 +142,11 @@ def score_emb(model: str, s, p, o, combine: str, l_norm: float = 1.0) -> np.ndar
     n = p.shape[0]
     if model in BILINEAR:
         if combine == "spo":
-            return (prep_sp(model, s, p) * o).sum(-1)
+            return (prep_sp(model, s, p) * window(model, "sp_", o)).sum(-1)
         if combine == "sp_":
-            return prep_sp(model, s, p) @ o.T
+            return prep_sp(model, s, p) @ window(model, "sp_", o).T
         if combine == "_po":
-            return prep_po(model, p, o) @ s.T
+            return prep_po(model, p, o) @ window(model, "_po", s).T
     elif model == "transe":
         # transe.py:220-225: spo uses F.pairwise_distance (adds eps to the difference),
         # sp_/_po use torch.cdist (no eps).  Scores are NEGATED distances.
@@ -183,6 +211,14 @@ def model_scores(model, ent, rel, s, p, o, subset, l_norm=1.0) -> Dict[str, np.n
 
 
 def _vjp_prep_sp(model, s, r, dq):
+    if model == "cp":
+        s_h = _halves(s)[0]
+        return _cat(dq * r, np.zeros_like(s_h)), dq * s_h
+    if model == "simple":
+        s_h, s_t = _halves(s)
+        r_f, r_b = _halves(r)
+        g1, g2 = _halves(dq)
+        return 0.5 * _cat(g2 * r_f, g1 * r_b), 0.5 * _cat(g2 * s_h, g1 * s_t)
     if model == "complex":
         s_re, s_im = _halves(s)
         r_re, r_im = _halves(r)
@@ -202,6 +238,14 @@ def _vjp_prep_sp(model, s, r, dq):
 
 
 def _vjp_prep_po(model, r, o, dq):
+    if model == "cp":
+        o_t = _halves(o)[1]
+        return dq * o_t, _cat(np.zeros_like(o_t), dq * r)
+    if model == "simple":
+        o_h, o_t = _halves(o)
+        r_f, r_b = _halves(r)
+        g1, g2 = _halves(dq)
+        return 0.5 * _cat(g1 * o_t, g2 * o_h), 0.5 * _cat(g2 * r_b, g1 * r_f)
     if model == "complex":
         r_re, r_im = _halves(r)
         o_re, o_im = _halves(o)
@@ -251,22 +295,24 @@ def model_grads(model, ent, rel, s, p, o, w_sp, w_po, w_spo, l_norm=1.0):
     g_rel = np.zeros_like(rel)
     S, P, O = ent[s], rel[p], ent[o]
     if model in BILINEAR:
-        # sp_: scores = q_sp @ E^T
+        # sp_: scores = q_sp @ window_sp(E)^T
         q = prep_sp(model, S, P)
-        g_ent += w_sp.T @ q
-        ds, dr = _vjp_prep_sp(model, S, P, w_sp @ ent)
+        window(model, "sp_", g_ent)[...] += w_sp.T @ q
+        ds, dr = _vjp_prep_sp(model, S, P, w_sp @ window(model, "sp_", ent))
         np.add.at(g_ent, s, ds)
         np.add.at(g_rel, p, dr)
-        # _po: scores = q_po @ E^T
+        # _po: scores = q_po @ window_po(E)^T
         q = prep_po(model, P, O)
-        g_ent += w_po.T @ q
-        dr, do = _vjp_prep_po(model, P, O, w_po @ ent)
+        window(model, "_po", g_ent)[...] += w_po.T @ q
+        dr, do = _vjp_prep_po(model, P, O, w_po @ window(model, "_po", ent))
         np.add.at(g_rel, p, dr)
         np.add.at(g_ent, o, do)
-        # spo: sum(q_sp * o)
+        # spo: sum(q_sp * window_sp(o))
         q = prep_sp(model, S, P)
-        np.add.at(g_ent, o, w_spo[:, None] * q)
-        ds, dr = _vjp_prep_sp(model, S, P, w_spo[:, None] * O)
+        g_o = np.zeros_like(O)
+        window(model, "sp_", g_o)[...] = w_spo[:, None] * q
+        np.add.at(g_ent, o, g_o)
+        ds, dr = _vjp_prep_sp(model, S, P, w_spo[:, None] * window(model, "sp_", O))
         np.add.at(g_ent, s, ds)
         np.add.at(g_rel, p, dr)
         return g_ent, g_rel

@@ -20,7 +20,7 @@ Fixtures written (see tests/golden/README.md for the schema):
 
 * ``scorer_<model>_<regime>.npz`` -- F1: embedding tables, index vectors and the
   outputs of score_spo / score_sp / score_po / score_sp_po (all and subset) for
-  ComplEx, DistMult, RESCAL, TransE (L1, L2) and RotatE (L1, L2), in the N(0, 0.1) and
+  ComplEx, DistMult, RESCAL, TransE (L1, L2), RotatE (L1, L2), CP and SimplE, in the N(0, 0.1) and
   the dyadic (k/8, |k| <= 16) value regimes, plus F2 gradients of a weighted sum of
   the outputs w.r.t. both tables;
 * ``eval_<regime>.npz`` -- F3: a synthetic dataset, a ComplEx model and the per-query
@@ -30,7 +30,7 @@ Fixtures written (see tests/golden/README.md for the schema):
   with per-batch losses and the final tables;
 * ``shapes.npz`` -- F5: config-derived relation dims (RotatE d/2, RESCAL d^2).
 
-Run:  PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden.py
+Run:  PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden.py [case,case,...]
 """
 import collections
 import collections.abc
@@ -147,6 +147,8 @@ SCORER_CASES = [
     ("transe_l2", "transe", 64, {"transe.l_norm": 2.0}),
     ("rotate_l1", "rotate", 64, {"rotate.l_norm": 1.0}),
     ("rotate_l2", "rotate", 64, {"rotate.l_norm": 2.0}),
+    ("cp", "cp", 64, {}),
+    ("simple", "simple", 64, {}),
 ]
 
 
@@ -377,17 +379,21 @@ def gen_shapes():
 
 
 def main():
+    # optional argv: names of the scorer cases to (re)generate; nothing else is rewritten
+    only = set(sys.argv[1].split(",")) if len(sys.argv) > 1 else None
     torch.set_num_threads(4)
     written = []
     seed = 1000
     for name, key, dim, extra in SCORER_CASES:
         for regime in ("normal", "dyadic"):
             seed += 1
-            written.append(gen_scorer_fixture(name, key, dim, extra, regime, seed))
-    for regime in ("dyadic", "normal"):
-        written.append(gen_eval_fixture(regime))
-    written.append(gen_train_fixture())
-    written.append(gen_shapes())
+            if only is None or name in only:
+                written.append(gen_scorer_fixture(name, key, dim, extra, regime, seed))
+    if only is None:
+        for regime in ("dyadic", "normal"):
+            written.append(gen_eval_fixture(regime))
+        written.append(gen_train_fixture())
+        written.append(gen_shapes())
     shutil.rmtree(TMP, ignore_errors=True)
     for fn in written:
         print(os.path.relpath(fn, OUT), os.path.getsize(fn))

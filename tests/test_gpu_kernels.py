@@ -21,7 +21,15 @@ from oracle import kge_oracle as K
 
 pytestmark = pytest.mark.gpu
 
-MODEL_IDS = {"complex": 0, "distmult": 1, "rescal": 2, "transe": 3, "rotate": 4}
+MODEL_IDS = {"complex": 0, "distmult": 1, "rescal": 2, "transe": 3, "rotate": 4, "cp": 5, "simple": 6}
+
+
+def win(model, direction, t):
+    """Entity-row columns a query contracts with (CP: second half for sp_, first for _po)."""
+    if model != "cp":
+        return t
+    h = t.shape[1] // 2
+    return t[:, h:] if direction == 0 else t[:, :h]
 SCORER_FILES = sorted(glob.glob(os.path.join(GOLDEN, "scorer_*.npz")))
 
 
@@ -66,10 +74,11 @@ def forward_all(L, meta, f, prec):
     q_sp = L.prep_query(mk, L.DIR_SP, ent, s, rel, p, n, d_e, d_r)
     q_po = L.prep_query(mk, L.DIR_PO, ent, o, rel, p, n, d_e, d_r)
     if model in K.BILINEAR:
-        out["sp_all"] = L.score_dot(q_sp, ent, None, prec)
-        out["po_all"] = L.score_dot(q_po, ent, None, prec)
-        out["sp_sub"] = L.score_dot(q_sp, ent, sub, prec)
-        out["po_sub"] = L.score_dot(q_po, ent, sub, prec)
+        e_sp, e_po = win(model, 0, ent), win(model, 1, ent)
+        out["sp_all"] = L.score_dot(q_sp, e_sp, None, prec)
+        out["po_all"] = L.score_dot(q_po, e_po, None, prec)
+        out["sp_sub"] = L.score_dot(q_sp, e_sp, sub, prec)
+        out["po_sub"] = L.score_dot(q_po, e_po, sub, prec)
     else:
         kind, sign = dist_kind(model, ln)
         out["sp_all"] = L.score_dist(kind, sign, q_sp, ent, None)
@@ -119,8 +128,8 @@ def test_gradients_vs_golden(L, fn, prec):
         q = L.prep_query(mk, direction, ent, e_idx, rel, p, n, d_e, d_r)
         dq = torch.zeros_like(q)
         if model in K.BILINEAR:
-            L.score_dot_bwd_q(w, ent, None, P, dq=dq, accumulate=False)
-            L.score_dot_bwd_t(w, q, None, g_ent, P)
+            L.score_dot_bwd_q(w, win(model, direction, ent), None, P, dq=dq, accumulate=False)
+            L.score_dot_bwd_t(w, q, None, win(model, direction, g_ent), P)
         else:
             kind, sign = dist_kind(model, ln)
             L.score_dist_bwd(kind, sign, w, q, ent, None, dq, g_ent)

@@ -20,7 +20,7 @@ from oracle import kge_oracle as K
 
 pytestmark = pytest.mark.gpu
 
-MODEL_IDS = {"complex": 0, "distmult": 1, "rescal": 2, "transe": 3, "rotate": 4}
+MODEL_IDS = {"complex": 0, "distmult": 1, "rescal": 2, "transe": 3, "rotate": 4, "cp": 5, "simple": 6}
 FILES = sorted(glob.glob(os.path.join(GOLDEN, "scorer_*_normal.npz")))
 
 
@@ -101,7 +101,7 @@ def _ns_job(model, impl, num_neg=31, dim=64, shared=False, filtering=False, E=50
     return job
 
 
-@pytest.mark.parametrize("model", ["rotate", "complex", "transe"])
+@pytest.mark.parametrize("model", ["rotate", "complex", "transe", "cp", "simple"])
 def test_ns_implementations_agree(model):
     """Column 0 = the positive; same negatives through every scoring implementation."""
     job = _ns_job(model, "triple")
