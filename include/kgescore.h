@@ -133,6 +133,13 @@ int kge_score_dot_bwd_t(const float* g, int64_t ldg, const float* q, int64_t ldq
                         const int64_t* tidx, int64_t n, int64_t m, int d, float* dt,
                         int64_t lddt, int precision, void* stream);
 
+/* kge_score_dot_bwd_t with accumulate = 0: dT[j, k] = sum_i G[i, j] * Q[i, k] overwrites
+ * rows 0 .. m-1 (no zero-fill pass, no read of dT; tidx must be NULL).  accumulate = 1 is
+ * kge_score_dot_bwd_t. */
+int kge_score_dot_bwd_t_ex(const float* g, int64_t ldg, const float* q, int64_t ldq,
+                           const int64_t* tidx, int64_t n, int64_t m, int d, float* dt,
+                           int64_t lddt, int accumulate, int precision, void* stream);
+
 /* ---- all-entities distance scoring (TransE, RotatE; VALU, no MFMA) -------------
  * S[i, j] = sign * dist_kind(Q[i, :], T[row(j), :])
  * Replaces torch.cdist in transe.py:223,225 and the pairwise tensors of rotate.py:288-307.
@@ -241,6 +248,17 @@ int kge_score_cand_bwd_ent(int model, float l_norm, int dir, const float* q, int
  * kge_score_cand_bwd_ent. */
 int kge_bucket_scatter(const int64_t* idx, int64_t n, int64_t* cursor, int64_t* order,
                        void* stream);
+
+/* ---- optimizer ------------------------------------------------------------------------
+ * One fused Adagrad step over n contiguous fp32 elements (an embedding table, its dense
+ * gradient and its state sum), element-wise as torch.optim.Adagrad's multi-tensor path:
+ *   g = maximize ? -grad : grad;  g += weight_decay * p;  sum += g * g;
+ *   p += (g * minus_clr) / (sqrt(sum) + eps),   minus_clr = -lr / (1 + (step - 1) lr_decay)
+ * Replaces the torch.optim.Adagrad step behind train.optimizer "Adagrad"
+ * (kge/util/optimizer.py:11-32). */
+int kge_adagrad_step(float* param, const float* grad, float* state_sum, int64_t n,
+                     float minus_clr, float eps, float weight_decay, int maximize,
+                     void* stream);
 
 /* ---- entity-ranking counts (eval) --------------------------------------------------
  * For row i of a score chunk S[n, m] covering entities [c0, c0 + m):

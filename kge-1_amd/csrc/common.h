@@ -64,7 +64,7 @@ static inline int kge_num_cus() {
 int kge_bwd3_q(const float* g, int64_t ldg, const float* t, int64_t ldt, const int64_t* tidx, int64_t n,
                int64_t m, int d, float* dq, int64_t lddq, int cus, hipStream_t st);
 int kge_bwd3_t(const float* g, int64_t ldg, const float* q, int64_t ldq, const int64_t* tidx, int64_t n,
-               int64_t m, int d, float* dt, int64_t lddt, hipStream_t st);
+               int64_t m, int d, float* dt, int64_t lddt, int accumulate, hipStream_t st);
 
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll

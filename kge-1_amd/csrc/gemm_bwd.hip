@@ -148,12 +148,25 @@ extern "C" int kge_score_dot_bwd_q(const float* g, int64_t ldg, const float* t, 
 extern "C" int kge_score_dot_bwd_t(const float* g, int64_t ldg, const float* q, int64_t ldq,
                                    const int64_t* tidx, int64_t n, int64_t m, int d, float* dt,
                                    int64_t lddt, int precision, void* stream) {
+  return kge_score_dot_bwd_t_ex(g, ldg, q, ldq, tidx, n, m, d, dt, lddt, 1, precision, stream);
+}
+
+extern "C" int kge_score_dot_bwd_t_ex(const float* g, int64_t ldg, const float* q, int64_t ldq,
+                                      const int64_t* tidx, int64_t n, int64_t m, int d, float* dt,
+                                      int64_t lddt, int accumulate, int precision, void* stream) {
   KGE_REQUIRE(n >= 0 && m >= 0 && d > 0 && n < (1LL << 31) && m < (1LL << 31));
   KGE_REQUIRE(g && q && dt && ldg >= m && ldq >= d && lddt >= d);
   KGE_REQUIRE(precision == KGE_PREC_FP32 || precision == KGE_PREC_BF16X3);
-  if (n == 0 || m == 0) return 0;
+  KGE_REQUIRE(accumulate || !tidx);
+  if (m == 0) return 0;
   hipStream_t st = as_stream(stream);
-  if (precision == KGE_PREC_BF16X3) return kge_bwd3_t(g, ldg, q, ldq, tidx, n, m, d, dt, lddt, st);
+  if (!accumulate && (n == 0 || precision == KGE_PREC_FP32)) {  // fp32 path: zero, then accumulate
+    hipError_t e = hipMemset2DAsync(dt, lddt * sizeof(float), 0, d * sizeof(float), m, st);
+    if (e != hipSuccess) return (int)e;
+    accumulate = 1;
+  }
+  if (n == 0) return 0;
+  if (precision == KGE_PREC_BF16X3) return kge_bwd3_t(g, ldg, q, ldq, tidx, n, m, d, dt, lddt, accumulate, st);
   const int gm = (int)((m + BM - 1) / BM), gn = (d + BN - 1) / BN;
   // C[j][k] = sum_i G[i][j] Q[i][k]: A = G^T (M contiguous), B = Q
   if (tidx)

@@ -40,7 +40,8 @@ __device__ __forceinline__ void split8(const float (&v)[8], bf16x8& h, bf16x8& l
 //   A_T = false: A(i, k) = a[i * lda + k]     (G for dQ)
 //   A_T = true : A(i, k) = a[k * lda + i]     (G^T for dT)
 //   B(k, j) = b[brow(k) * ldb + j]            (T gathered through tidx for dQ; Q for dT)
-// C_MODE 0: atomicAdd c[i * ldc + j]; 1: c[i * ldc + j] += v; 2: atomicAdd c[crow[i] * ldc + j]
+// C_MODE 0: atomicAdd c[i * ldc + j]; 1: c[i * ldc + j] += v; 2: atomicAdd c[crow[i] * ldc + j];
+// 3: c[i * ldc + j] = v (K not split: one block owns the element)
 template <bool A_T, int C_MODE, bool GATHER>
 __global__ void __launch_bounds__(NT, 1)
     gemm3_kernel(const float* __restrict__ a, int64_t lda, const float* __restrict__ b, int64_t ldb,
@@ -198,6 +199,8 @@ __global__ void __launch_bounds__(NT, 1)
           atomicAdd(c + (int64_t)i * ldc + j, v);
         } else if (C_MODE == 1) {
           c[(int64_t)i * ldc + j] += v;
+        } else if (C_MODE == 3) {
+          c[(int64_t)i * ldc + j] = v;
         } else {
           atomicAdd(c + crow[i] * ldc + j, v);
         }
@@ -437,6 +440,8 @@ __global__ void __launch_bounds__(NT, 1)
           atomicAdd(c + (int64_t)i * ldc + j, v);
         } else if (C_MODE == 1) {
           c[(int64_t)i * ldc + j] += v;
+        } else if (C_MODE == 3) {
+          c[(int64_t)i * ldc + j] = v;
         } else {
           atomicAdd(c + crow[i] * ldc + j, v);
         }
@@ -493,11 +498,13 @@ int kge_bwd3_q(const float* g, int64_t ldg, const float* t, int64_t ldt, const i
 }
 
 int kge_bwd3_t(const float* g, int64_t ldg, const float* q, int64_t ldq, const int64_t* tidx, int64_t n,
-               int64_t m, int d, float* dt, int64_t lddt, hipStream_t st) {
+               int64_t m, int d, float* dt, int64_t lddt, int accumulate, hipStream_t st) {
   if (vec_ok(g, ldg, m, q, ldq, d)) {
     if (tidx) return launch<true, 2, false, true>(g, ldg, q, ldq, nullptr, dt, lddt, tidx, m, d, n, 1, st);
+    if (!accumulate) return launch<true, 3, false, true>(g, ldg, q, ldq, nullptr, dt, lddt, nullptr, m, d, n, 1, st);
     return launch<true, 1, false, true>(g, ldg, q, ldq, nullptr, dt, lddt, nullptr, m, d, n, 1, st);
   }
   if (tidx) return launch<true, 2, false, false>(g, ldg, q, ldq, nullptr, dt, lddt, tidx, m, d, n, 1, st);
+  if (!accumulate) return launch<true, 3, false, false>(g, ldg, q, ldq, nullptr, dt, lddt, nullptr, m, d, n, 1, st);
   return launch<true, 1, false, false>(g, ldg, q, ldq, nullptr, dt, lddt, nullptr, m, d, n, 1, st);
 }

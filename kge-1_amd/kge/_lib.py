@@ -45,6 +45,8 @@ SIGNATURES = {
     "kge_score_dot_split": ([_P, _P, _I64, _P, _I64, _P, _I64, _I64, _I, _P, _I64, _P], _I),
     "kge_score_dot_bwd_q": ([_P, _I64, _P, _I64, _P, _I64, _I64, _I, _P, _I64, _I, _I, _P], _I),
     "kge_score_dot_bwd_t": ([_P, _I64, _P, _I64, _P, _I64, _I64, _I, _P, _I64, _I, _P], _I),
+    "kge_adagrad_step": ([_P, _P, _P, _I64, ctypes.c_float, ctypes.c_float, ctypes.c_float, _I, _P], _I),
+    "kge_score_dot_bwd_t_ex": ([_P, _I64, _P, _I64, _P, _I64, _I64, _I, _P, _I64, _I, _I, _P], _I),
     "kge_score_dist": ([_I, _F, _P, _I64, _P, _I64, _P, _I64, _I64, _I, _P, _I64, _P], _I),
     "kge_score_dist_bwd": ([_I, _F, _P, _I64, _P, _I64, _P, _I64, _P, _I64, _I64, _I, _P, _I64, _P,
                             _I64, _P], _I),
@@ -160,17 +162,22 @@ def prep_query(model, direction, ent, eidx, rel, ridx, n, d_e, d_r, out=None):
     return q
 
 
-def prep_query_split(model, direction, ent, eidx, rel, ridx, n, d_e, d_r, want_fp32=True):
-    """Query rows as fp32 (optional) plus bf16 hi / lo planes [n, round32(width)] in one pass."""
+def prep_query_split(model, direction, ent, eidx, rel, ridx, n, d_e, d_r, want_fp32=True, out=None):
+    """Query rows as fp32 (optional) plus bf16 hi / lo planes [n, round32(width)] in one pass
+    (into out = (q or None, hi, lo) when given)."""
     require_device(ent, rel)
     eidx, ridx = idx64(eidx), idx64(ridx)
     check_index(eidx, ent.shape[0], "entity index")
     check_index(ridx, rel.shape[0], "relation index")
     qw = query_width(model, d_e)
-    ldp = (qw + 31) // 32 * 32
-    q = torch.empty(n, qw, device=ent.device, dtype=torch.float32) if want_fp32 else None
-    hi = torch.empty(n, ldp, device=ent.device, dtype=torch.bfloat16)
-    lo = torch.empty_like(hi)
+    if out is not None:
+        q, hi, lo = out
+        ldp = hi.stride(0)
+    else:
+        ldp = (qw + 31) // 32 * 32
+        q = torch.empty(n, qw, device=ent.device, dtype=torch.float32) if want_fp32 else None
+        hi = torch.empty(n, ldp, device=ent.device, dtype=torch.bfloat16)
+        lo = torch.empty_like(hi)
     _check(lib().kge_prep_query_split(model, direction, ptr(ent), rows(ent), ptr(eidx), ptr(rel), rows(rel),
                                       ptr(ridx), n, d_e, d_r, ptr(q), rows(q) if q is not None else 0, ptr(hi),
                                       ptr(lo), ldp, stream()), "kge_prep_query_split")
@@ -247,12 +254,13 @@ def score_dot_bwd_q(g, t, tidx, precision, dq=None, accumulate=False):
     return dq
 
 
-def score_dot_bwd_t(g, q, tidx, dt, precision):
+def score_dot_bwd_t(g, q, tidx, dt, precision, accumulate=True):
+    """dt (+)= g^T . q (rows scattered through tidx); accumulate=False overwrites dt."""
     tidx = idx64(tidx)
     n, m = g.shape
     d = q.shape[1]
-    _check(lib().kge_score_dot_bwd_t(ptr(g), rows(g), ptr(q), rows(q), ptr(tidx), n, m, d, ptr(dt),
-                                     rows(dt), precision, stream()), "kge_score_dot_bwd_t")
+    _check(lib().kge_score_dot_bwd_t_ex(ptr(g), rows(g), ptr(q), rows(q), ptr(tidx), n, m, d, ptr(dt),
+                                        rows(dt), int(accumulate), precision, stream()), "kge_score_dot_bwd_t_ex")
     return dt
 
 
@@ -421,3 +429,9 @@ def softmax_kl(s, l_ptr, l_col, smoothing, scale, g=None, loss=None):
     _check(lib().kge_softmax_kl(ptr(s), rows(s), n, m, ptr(l_ptr), ptr(l_col), float(smoothing), float(scale),
                                 ptr(loss), ptr(g), rows(g) if g is not None else 0, stream()), "kge_softmax_kl")
     return loss
+
+
+def adagrad_step(param, grad, state_sum, minus_clr, eps, weight_decay, maximize):
+    """One fused Adagrad step in place on contiguous fp32 CUDA tensors (kge_adagrad_step)."""
+    _check(lib().kge_adagrad_step(ptr(param), ptr(grad), ptr(state_sum), param.numel(), float(minus_clr),
+                                  float(eps), float(weight_decay), int(bool(maximize)), stream()), "kge_adagrad_step")

@@ -179,6 +179,89 @@ def score_all_xent(kind: int, direction: int, precision: int, l_norm: float, ent
                             tab, L.idx64(tidx), L.idx64(labels), L.idx64(l_ptr), float(smoothing), float(scale))
 
 
+class _ScoreXent2(torch.autograd.Function):
+    """Two query batches against the same table in ONE engine pass (the sp_ and _po halves of
+    a 1vsAll / KvsAll step): the query rows of both are prepared into one [n_a + n_b, d]
+    block, scored by one contraction, turned into G by one loss launch, and the backward
+    runs one dQ GEMM and one dT GEMM over the stacked block.  dT = G^T Q over the
+    concatenated K = n_a + n_b is written, not accumulated (no zero fill, no read), and the
+    table gradient leaves as a single tensor (no autograd accumulation of two halves)."""
+
+    @staticmethod
+    def forward(ctx, kind, precision, ent, rel, dir_a, eidx_a, ridx_a, lab_a, lptr_a, dir_b, eidx_b, ridx_b,
+                lab_b, lptr_b, smoothing, scale):
+        ent, rel = _rows(ent), _rows(rel)
+        n_a, n_b = eidx_a.numel(), eidx_b.numel()
+        n, m = n_a + n_b, ent.shape[0]
+        d_e, d_r = ent.shape[1], rel.shape[1]
+        qw, tab_w = L.query_width(kind, d_e), window(kind, dir_a, ent)
+        need = ctx.needs_input_grad[2] or ctx.needs_input_grad[3]
+        buf = torch.empty(n, (m + 3) // 4 * 4, device=ent.device, dtype=torch.float32)
+        s = buf[:, :m]
+        q = torch.empty(n, qw, device=ent.device, dtype=torch.float32) if need else None
+        parts = ((dir_a, eidx_a, ridx_a, 0, n_a), (dir_b, eidx_b, ridx_b, n_a, n))
+        if L.split_ok(qw, tab_w, precision):
+            ldp = (qw + 31) // 32 * 32
+            hi = torch.empty(n, ldp, device=ent.device, dtype=torch.bfloat16)
+            lo = torch.empty_like(hi)
+            for dr, ei, ri, r0, r1 in parts:
+                L.prep_query_split(kind, dr, ent, ei, rel, ri, r1 - r0, d_e, d_r,
+                                   out=(q[r0:r1] if need else None, hi[r0:r1], lo[r0:r1]))
+            _timed(L.score_dot_split, hi, lo, tab_w, None, qw, out=s)
+        else:
+            if q is None:
+                q = torch.empty(n, qw, device=ent.device, dtype=torch.float32)
+            for dr, ei, ri, r0, r1 in parts:
+                L.prep_query(kind, dr, ent, ei, rel, ri, r1 - r0, d_e, d_r, out=q[r0:r1])
+            _timed(L.contract, q, tab_w, None, precision, out=s)
+        if lptr_a is None:  # index labels (1vsAll)
+            loss_rows = L.softmax_xent(s, torch.cat((lab_a, lab_b)), scale, g=s)
+        else:  # CSR positives (KvsAll)
+            l_ptr = torch.cat((lptr_a[:-1], lptr_b + lptr_a[-1]))
+            loss_rows = L.softmax_kl(s, l_ptr, torch.cat((lab_a, lab_b)), smoothing, scale, g=s)
+        ctx.meta = (kind, precision, n_a, n, d_e, d_r, dir_a, dir_b)
+        ctx.save_for_backward(ent, rel, eidx_a, ridx_a, eidx_b, ridx_b, q if q is not None else s.new_empty(0), s)
+        return torch.stack((loss_rows[:n_a].sum(), loss_rows[n_a:].sum())) * scale
+
+    @staticmethod
+    def backward(ctx, gl):
+        kind, precision, n_a, n, d_e, d_r, dir_a, dir_b = ctx.meta
+        ent, rel, eidx_a, ridx_a, eidx_b, ridx_b, q, g = ctx.saved_tensors
+        tab_w = window(kind, dir_a, ent)
+        # dL/dS = gl[part] * G on each part's rows: folded into the [n, d] operands
+        row_scale = torch.cat((gl[0].expand(n_a), gl[1].expand(n - n_a)))[:, None]
+        dq = L.score_dot_bwd_q(g, tab_w, None, precision)
+        dq.mul_(row_scale)
+        if tab_w.shape[1] == d_e:  # the GEMM covers every column: write, do not accumulate
+            d_ent = torch.empty_like(ent)
+            L.score_dot_bwd_t(g, q * row_scale, None, d_ent, precision, accumulate=False)
+        else:
+            d_ent = torch.zeros_like(ent)
+            L.score_dot_bwd_t(g, q * row_scale, None, window(kind, dir_a, d_ent), precision)
+        d_rel = torch.zeros_like(rel)
+        L.prep_query_bwd(kind, dir_a, ent, eidx_a, rel, ridx_a, n_a, d_e, d_r, dq[:n_a], d_ent, d_rel)
+        L.prep_query_bwd(kind, dir_b, ent, eidx_b, rel, ridx_b, n - n_a, d_e, d_r, dq[n_a:], d_ent, d_rel)
+        return (None, None, d_ent if ctx.needs_input_grad[2] else None, d_rel if ctx.needs_input_grad[3] else None,
+                None, None, None, None, None, None, None, None, None, None, None, None)
+
+
+def score_all_xent2(kind: int, precision: int, ent: torch.Tensor, rel: torch.Tensor, part_a, part_b, scale: float,
+                    smoothing: float = 0.0) -> Optional[torch.Tensor]:
+    """[scale * sum of part a's per-row losses, the same for part b]: two query batches scored
+    against every row of ent in one engine pass (see _ScoreXent2).  part = (direction, eidx, ridx, labels, l_ptr) with the
+    label conventions of score_all_xent (both parts index labels, or both CSR).  None when
+    the batches cannot share one contraction (distance models; CP queries of different
+    directions contract different halves of the rows) -- the caller runs them separately."""
+    dir_a, eidx_a, ridx_a, lab_a, lptr_a = part_a
+    dir_b, eidx_b, ridx_b, lab_b, lptr_b = part_b
+    if kind not in BILINEAR or (kind == L.CP and dir_a != dir_b) or (lptr_a is None) != (lptr_b is None):
+        return None
+    L.require_device(ent, rel)
+    return _ScoreXent2.apply(kind, precision, ent, rel, dir_a, L.idx64(eidx_a), L.idx64(ridx_a), L.idx64(lab_a),
+                             L.idx64(lptr_a), dir_b, L.idx64(eidx_b), L.idx64(ridx_b), L.idx64(lab_b),
+                             L.idx64(lptr_b), float(smoothing), float(scale))
+
+
 def score_all(kind: int, direction: int, precision: int, l_norm: float, ent: torch.Tensor,
               eidx: Optional[torch.Tensor], rel: torch.Tensor, ridx: Optional[torch.Tensor],
               tab: torch.Tensor, tidx: Optional[torch.Tensor] = None) -> torch.Tensor:

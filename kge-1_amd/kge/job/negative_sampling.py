@@ -110,4 +110,4 @@ class TrainingJobNegativeSampling(TrainingJob):
                 loss.backward()
                 bwd += time.time()
                 total = total + loss.detach()
-        return TrainingJob._ProcessBatchResult(float(total.item()), bs, prepare, fwd, bwd)
+        return TrainingJob._ProcessBatchResult(total.detach(), bs, prepare, fwd, bwd)

@@ -4,7 +4,8 @@ and TrainingJobKvsAll (train.py:493-756) over the TrainingJob epoch loop (train.
 Per batch they call KgeModel.score_sp / score_po exactly as the reference does; the
 engine runs the fused gather + contraction forward and the MFMA backward.  Difference
 from the reference, by design (Q11): the per-direction ``loss.item()`` host syncs are
-deferred to one sync per batch.
+replaced by an asynchronous copy of each batch loss that the epoch loop reads one batch
+later, so the host never drains the device queue inside the epoch.
 """
 from __future__ import annotations
 
@@ -27,11 +28,15 @@ S, P, O = 0, 1, 2
 class TrainingJob(Job):
     @dataclass
     class _ProcessBatchResult:
-        avg_loss: float
+        loss: Any  # float, or a 0-dim device tensor read by the epoch loop one batch later
         size: int
         prepare_time: float
         forward_time: float
         backward_time: float
+
+        @property
+        def avg_loss(self) -> float:
+            return float(self.loss)
 
     def __init__(self, config, dataset, parent_job=None, model=None):
         super().__init__(config, dataset, parent_job)
@@ -93,27 +98,53 @@ class TrainingJob(Job):
         epoch_time = -time.time()
         fwd = bwd = prep = opt_t = 0.0
         n_batches = 0
+        pending = None  # (pinned host copy of a batch loss, its event, batch size, penalty)
+
+        def settle(p):
+            nonlocal sum_loss
+            buf, ev, size, penalty = p
+            if ev is not None:
+                ev.synchronize()
+            v = float(buf)
+            sum_loss += v * size
+            if self.abort_on_nan and math.isnan(v + penalty):
+                raise FloatingPointError("Cost became nan, aborting training job")
+
         for batch_index, example_ids in enumerate(self._batches()):
             for f in self.pre_batch_hooks:
                 f(self)
             self.optimizer.zero_grad()
             batch = self._collate(example_ids)
             res = self.process_batch(batch_index, batch)
-            sum_loss += res.avg_loss * res.size
             penalty = 0.0
             for _, pv in self.model.penalty(epoch=self.epoch, batch_index=batch_index, batch=batch):
                 pv.backward()
                 penalty += pv.item()
             sum_penalty += penalty
-            if self.abort_on_nan and math.isnan(res.avg_loss + penalty):
-                raise FloatingPointError("Cost became nan, aborting training job")
             t0 = time.time()
             self.optimizer.step()
             opt_t += time.time() - t0
+            # The batch loss is read one batch late (an async copy + event): the host queues
+            # batch b + 1 while the device still runs batch b, instead of draining the queue
+            # every batch as loss.item() would (the reference's per-batch sync, Q11).  A NaN
+            # aborts one optimizer step later than in the reference.
+            if torch.is_tensor(res.loss) and res.loss.is_cuda:
+                buf = torch.empty((), dtype=res.loss.dtype, pin_memory=True)
+                buf.copy_(res.loss.detach(), non_blocking=True)
+                ev = torch.cuda.Event()
+                ev.record()
+                cur = (buf, ev, res.size, penalty)
+            else:
+                cur = (float(res.loss), None, res.size, penalty)
+            if pending is not None:
+                settle(pending)
+            pending = cur
             prep += res.prepare_time
             fwd += res.forward_time
             bwd += res.backward_time
             n_batches += 1
+        if pending is not None:
+            settle(pending)
         epoch_time += time.time()
         trace = dict(type=self.type_str, scope="epoch", epoch=self.epoch, split=self.train_split,
                      batches=n_batches, size=self.num_examples, avg_loss=sum_loss / max(1, self.num_examples),
@@ -146,14 +177,22 @@ class TrainingJob1vsAll(TrainingJob):
 
     def _process_batch(self, batch_index, batch) -> TrainingJob._ProcessBatchResult:
         """train.py:1032-1062: sp then po, each loss / B followed by backward.  With
-        engine.fused_loss and the kl loss, scoring + cross entropy + its gradient run as one
-        engine op per direction (KgeModel.score_sp_xent / score_po_xent)."""
+        engine.fused_loss and the kl loss, scoring + cross entropy + its gradient of both
+        directions run as one engine op (KgeModel.score_sp_po_xent; per direction with
+        score_sp_xent / score_po_xent when the scorer cannot share one contraction)."""
         t = -time.time()
         triples = batch["triples"].to(self.device, non_blocking=True)
         bs = len(triples)
         t += time.time()
         fused = self.config.get("engine.fused_loss") and isinstance(self.loss, KLDivWithSoftmaxKgeLoss)
         fwd = -time.time()
+        both = self.model.score_sp_po_xent(triples[:, S], triples[:, P], triples[:, O], 1.0 / bs) if fused else None
+        if both is not None:  # sp_ and _po in one engine pass; one backward (same gradient sum)
+            fwd += time.time()
+            bwd = -time.time()
+            both.sum().backward()
+            bwd += time.time()
+            return TrainingJob._ProcessBatchResult(both.detach().sum(), bs, t, fwd, bwd)
         loss_sp = self.model.score_sp_xent(triples[:, S], triples[:, P], triples[:, O], 1.0 / bs) if fused else None
         if loss_sp is None:
             scores_sp = self.model.score_sp(triples[:, S], triples[:, P])
@@ -173,8 +212,7 @@ class TrainingJob1vsAll(TrainingJob):
         bwd -= time.time()
         loss_po.backward()
         bwd += time.time()
-        loss_value = (loss_sp.detach() + loss_po.detach()).item()  # one host sync per batch
-        return TrainingJob._ProcessBatchResult(loss_value, bs, t, fwd, bwd)
+        return TrainingJob._ProcessBatchResult(loss_sp.detach() + loss_po.detach(), bs, t, fwd, bwd)
 
 
 class TrainingJobKvsAll(TrainingJob):
@@ -218,6 +256,11 @@ class TrainingJobKvsAll(TrainingJob):
         t += time.time()
         fwd = bwd = 0.0
         total = None
+        fused = self.config.get("engine.fused_loss") and isinstance(self.loss, KLDivWithSoftmaxKgeLoss)
+        if fused and len(self.query_types) == 2:
+            res = self._process_batch_fused2(ex, bs)
+            if res is not None:
+                return res
         start = 0
         for qi, qt in enumerate(self.query_types):
             end = self.query_last_example[qi]
@@ -264,4 +307,39 @@ class TrainingJobKvsAll(TrainingJob):
             loss.backward()
             bwd += time.time()
             total = loss.detach()  # reference keeps the last query type's value (Q10)
-        return TrainingJob._ProcessBatchResult(float(total.item()) if total is not None else 0.0, bs, t, fwd, bwd)
+        return TrainingJob._ProcessBatchResult(total if total is not None else 0.0, bs, t, fwd, bwd)
+
+    def _process_batch_fused2(self, ex, bs):
+        """Both query types of the batch in one engine pass (KgeModel.score_xent_parts):
+        one contraction, one KL launch and one backward for the stacked sp_ and _po query
+        rows; the reported loss is the last query type's, as in the reference (Q10).
+        None when a query type has no example in this batch or the scorer cannot fuse."""
+        t = -time.time()
+        parts, start = [], 0
+        for qi, qt in enumerate(self.query_types):
+            end = self.query_last_example[qi]
+            sel = ex[(ex >= start) & (ex < end)] - start
+            start = end
+            if len(sel) == 0:
+                return None
+            keys, offs, vals = self._dev[qi]
+            sel_d = torch.from_numpy(sel).to(self.device)
+            q = keys[sel_d]
+            lo, hi = offs[sel_d], offs[sel_d + 1]
+            lens = hi - lo
+            pos = torch.arange(int(lens.sum().item()), device=self.device) - torch.repeat_interleave(
+                torch.cumsum(lens, 0) - lens, lens) + torch.repeat_interleave(lo, lens)
+            l_ptr = torch.cat((lens.new_zeros(1), torch.cumsum(lens, 0)))
+            l_col = vals[pos]
+            part = self.model.xent_part_sp if qt == "sp_" else self.model.xent_part_po
+            parts.append(part(q[:, 0], q[:, 1], l_col, l_ptr))
+        t += time.time()
+        fwd = -time.time()
+        losses = self.model.score_xent_parts(parts[0], parts[1], 1.0 / bs, self.label_smoothing)
+        fwd += time.time()
+        if losses is None:
+            return None
+        bwd = -time.time()
+        losses.sum().backward()
+        bwd += time.time()
+        return TrainingJob._ProcessBatchResult(losses[1].detach(), bs, t, fwd, bwd)

@@ -142,6 +142,23 @@ class RelationalScorer(KgeBase):
         return engine.score_all_xent(self.engine_kind, d, self.precision(), self.l_norm(), ent, e_idx, rel, p_idx,
                                      ent, None, labels, scale, l_ptr, smoothing)
 
+    def score_lookup_xent2(self, ent: Tensor, rel: Tensor, part_a, part_b, scale: float,
+                           smoothing: float = 0.0) -> Optional[Tensor]:
+        """Both halves of a training step in one engine pass: part = (direction "sp_" / "_po",
+        e_idx, p_idx, labels, l_ptr).  Returns [loss_a, loss_b] (see engine.score_all_xent2),
+        or None when this scorer cannot share one contraction between the parts."""
+        from .. import engine, _lib
+
+        if self.engine_kind is None:
+            return None
+
+        def conv(part):
+            d, e, p, lab, lp = part
+            return (_lib.DIR_SP if d == "sp_" else _lib.DIR_PO), e, p, lab, lp
+
+        return engine.score_all_xent2(self.engine_kind, self.precision(), ent, rel, conv(part_a), conv(part_b),
+                                      scale, smoothing)
+
     def score_lookup_cand(self, ent: Tensor, rel: Tensor, e_idx: Tensor, p_idx: Tensor, direction: str,
                           cand: Tensor) -> Tensor:
         """[n, k]: query (ent[e_idx[i]], rel[p_idx[i]]) in direction "sp_" / "_po" against its
@@ -350,6 +367,28 @@ class KgeModel(KgeBase):
         if tabs is None:
             return None
         return self._scorer.score_lookup_xent(tabs[0], tabs[1], o, p, "_po", s, scale)
+
+    # --- both directions of a training step in one engine pass
+    def xent_part_sp(self, s: Tensor, p: Tensor, labels: Tensor, l_ptr: Optional[Tensor] = None):
+        """The (s, p, ?) query batch of a fused loss: (direction, e_idx, p_idx, labels, l_ptr)."""
+        return ("sp_", s, p, labels, l_ptr)
+
+    def xent_part_po(self, p: Tensor, o: Tensor, labels: Tensor, l_ptr: Optional[Tensor] = None):
+        """The (?, p, o) query batch of a fused loss."""
+        return ("_po", o, p, labels, l_ptr)
+
+    def score_xent_parts(self, part_a, part_b, scale: float, smoothing: float = 0.0) -> Optional[Tensor]:
+        """[loss_a, loss_b] of two query batches (xent_part_sp / xent_part_po) in one engine
+        pass; None when not fusable (the caller then runs score_*_xent / score_*_kl)."""
+        tabs = self._lookup_tables()
+        if tabs is None:
+            return None
+        return self._scorer.score_lookup_xent2(tabs[0], tabs[1], part_a, part_b, scale, smoothing)
+
+    def score_sp_po_xent(self, s: Tensor, p: Tensor, o: Tensor, scale: float) -> Optional[Tensor]:
+        """[score_sp_xent(s, p, o, scale), score_po_xent(p, o, s, scale)] in one engine pass
+        (the two losses of a 1vsAll step, train.py:1041-1057), or None."""
+        return self.score_xent_parts(self.xent_part_sp(s, p, o), self.xent_part_po(p, o, s), scale)
 
     def score_sp_cand(self, s: Tensor, p: Tensor, cand: Tensor) -> Optional[Tensor]:
         """[n, k] = score_spo(s_i, p_i, cand[i, c]) for every candidate object, without

@@ -53,6 +53,10 @@ class ReciprocalRelationsModel(KgeModel):
         return self._scorer.score_lookup_xent(tabs[0], tabs[1], o, p + self.dataset.num_relations(), "sp_", s,
                                               scale)
 
+    def xent_part_po(self, p: Tensor, o: Tensor, labels: Tensor, l_ptr=None):
+        """(?, p, o) is scored as (o, p + R, ?) (reciprocal_relations_model.py:67-74)."""
+        return ("sp_", o, p + self.dataset.num_relations(), labels, l_ptr)
+
     def score_po_cand(self, p: Tensor, o: Tensor, cand: Tensor):
         """score_spo(cand, p, o, direction="s") == score of (o, p + R, cand) as "sp_"
         (reciprocal_relations_model.py:57-65)."""

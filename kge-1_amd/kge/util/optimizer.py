@@ -1,19 +1,69 @@
-"""Optimizer / LR-scheduler factories (kge/util/optimizer.py:6-71): stock torch.optim
-classes selected by name with ``train.optimizer_args``."""
+"""Optimizer / LR-scheduler factories (kge/util/optimizer.py:6-71): torch.optim classes
+selected by name with ``train.optimizer_args``; "Adagrad" runs on the engine's fused step
+(engine.fused_optimizer, default on) with torch.optim.Adagrad's semantics and state."""
 from __future__ import annotations
 
 import torch
+
+
+class FusedAdagrad(torch.optim.Adagrad):
+    """torch.optim.Adagrad (same arguments, state_dict layout and per-element arithmetic)
+    whose step runs one engine kernel per parameter (kge_adagrad_step: a single pass over
+    param, grad and state sum) instead of the five-pass multi-tensor sequence.  Parameters
+    the kernel does not take (not CUDA fp32 contiguous, sparse or complex gradients,
+    differentiable mode) are stepped by torch."""
+
+    @torch.no_grad()
+    def step(self, closure=None):
+        from .. import _lib
+
+        loss = None
+        if closure is not None:
+            with torch.enable_grad():
+                loss = closure()
+        rest = []
+        for group in self.param_groups:
+            fallback = []
+            for p in group["params"]:
+                if p.grad is None:
+                    continue
+                g = p.grad
+                st = self.state[p]
+                if (group["differentiable"] or g.is_sparse or not p.is_cuda or p.dtype != torch.float32
+                        or g.dtype != torch.float32 or not p.is_contiguous() or not g.is_contiguous()
+                        or not st["sum"].is_contiguous() or st["step"].is_cuda):
+                    fallback.append(p)
+                    continue
+                st["step"] += 1
+                step = float(st["step"])
+                lr = float(group["lr"])
+                minus_clr = -lr / (1 + (step - 1) * group["lr_decay"])
+                _lib.adagrad_step(p, g, st["sum"], minus_clr, group["eps"], group["weight_decay"], group["maximize"])
+            if fallback:
+                rest.append((group, fallback))
+        for group, params in rest:  # torch's own step for what the kernel does not take
+            saved = group["params"]
+            group["params"] = params
+            try:
+                super().step()
+            finally:
+                group["params"] = saved
+        return loss
 
 
 class KgeOptimizer:
     @staticmethod
     def create(config, model):
         name = config.get("train.optimizer")
+        params = [p for p in model.parameters() if p.requires_grad]
+        args = config.get("train.optimizer_args")
+        if name == "Adagrad" and config.get("engine.fused_optimizer"):
+            return FusedAdagrad(params, **args)
         try:
             cls = getattr(torch.optim, name)
         except AttributeError as e:
             raise ValueError(f"Could not create optimizer {name}") from e
-        return cls([p for p in model.parameters() if p.requires_grad], **config.get("train.optimizer_args"))
+        return cls(params, **args)
 
 
 class KgeLRScheduler:

@@ -260,6 +260,39 @@ def test_reciprocal_relations_model():
         m.score_spo(p, p, o)
 
 
+@pytest.mark.parametrize("prec", ["bf16x3", "fp32"])
+@pytest.mark.parametrize("fn", SCORER_FILES, ids=lambda f: os.path.basename(f)[7:-4])
+def test_fused_xent2_matches_separate(fn, prec):
+    """KgeModel.score_sp_po_xent (both directions stacked into one contraction, one loss
+    launch, one backward that writes dE) == score_sp_xent + score_po_xent."""
+    f = np.load(fn)
+    if json.loads(str(f["meta"]))["regime"] != "normal":
+        pytest.skip("one regime is enough")
+    s, p, o = (torch.from_numpy(f[k]).cuda() for k in ("s", "p", "o"))
+    B = len(s)
+    res = []
+    for combined in (True, False):
+        m, meta = model_from_fixture(f, prec)
+        m.train()
+        m.zero_grad()
+        if combined:
+            both = m.score_sp_po_xent(s, p, o, 1.0 / B)
+            if both is None:
+                assert meta["model"] in K.DISTANCE or meta["model"] == "cp"
+                pytest.skip("not fusable across directions")
+            l_sp, l_po = both[0], both[1]
+            (both * torch.tensor([0.75, 1.25], device="cuda")).sum().backward()  # unequal upstream grads
+        else:
+            l_sp, l_po = m.score_sp_xent(s, p, o, 1.0 / B), m.score_po_xent(p, o, s, 1.0 / B)
+            (0.75 * l_sp + 1.25 * l_po).backward()
+        res.append((l_sp.item(), l_po.item(), m._entity_embedder._embeddings.weight.grad.cpu().numpy(),
+                    m._relation_embedder._embeddings.weight.grad.cpu().numpy()))
+    (a1, b1, ge1, gr1), (a0, b0, ge0, gr0) = res
+    assert abs(a1 - a0) <= 1e-5 * abs(a0) and abs(b1 - b0) <= 1e-5 * abs(b0)
+    assert np.abs(ge1 - ge0).max() <= 1e-5 * np.abs(ge0).max()
+    assert np.abs(gr1 - gr0).max() <= 1e-5 * np.abs(gr0).max()
+
+
 def test_reciprocal_fused_xent():
     """ReciprocalRelationsModel.score_po_xent == CE over score_po (base sp_ kernel, p + R)."""
     from kge import Config, Dataset, KgeModel
@@ -281,3 +314,7 @@ def test_reciprocal_fused_xent():
     fused = m.score_po_xent(p, o, s, 0.5)
     ref = torch.nn.CrossEntropyLoss(reduction="sum")(m.score_po(p, o), s) * 0.5
     assert abs(fused.item() - ref.item()) <= 1e-5 * abs(ref.item())
+    both = m.score_sp_po_xent(s, p, o, 0.5)  # both halves as "sp_" queries in one pass
+    ref_sp = torch.nn.CrossEntropyLoss(reduction="sum")(m.score_sp(s, p), o) * 0.5
+    assert abs(both[0].item() - ref_sp.item()) <= 1e-5 * abs(ref_sp.item())
+    assert abs(both[1].item() - ref.item()) <= 1e-5 * abs(ref.item())

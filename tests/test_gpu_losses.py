@@ -100,7 +100,8 @@ def test_kvsall_fused_matches_unfused(model, smoothing):
     for fused in (True, False):
         job = _kvsall_job(model, fused, smoothing)
         out = []
-        for b, ex in enumerate((torch.arange(0, 64), torch.arange(job.num_examples - 64, job.num_examples))):
+        mixed = torch.randperm(job.num_examples, generator=torch.Generator().manual_seed(5))[:64]  # sp_ and _po
+        for b, ex in enumerate((torch.arange(0, 64), torch.arange(job.num_examples - 64, job.num_examples), mixed)):
             job.optimizer.zero_grad()
             loss = job._process_batch(b, job._collate(ex)).avg_loss
             out.append((loss, job.model._entity_embedder._embeddings.weight.grad.cpu().numpy().copy(),
@@ -111,3 +112,31 @@ def test_kvsall_fused_matches_unfused(model, smoothing):
         tol = 1e-4  # bf16x3 backward GEMMs on both paths; G from the fused kernel vs torch
         assert np.abs(ge1 - ge0).max() <= tol * np.abs(ge0).max()
         assert np.abs(gr1 - gr0).max() <= tol * np.abs(gr0).max()
+
+
+@pytest.mark.parametrize("kw", [{}, {"lr_decay": 0.01, "weight_decay": 0.1}, {"maximize": True, "eps": 1e-6},
+                                {"initial_accumulator_value": 0.5}])
+def test_fused_adagrad_matches_torch(kw):
+    """util.optimizer.FusedAdagrad (kge_adagrad_step) == torch.optim.Adagrad, step by step,
+    including a parameter that falls back to torch (odd size: scalar kernel path; CPU)."""
+    from kge.util.optimizer import FusedAdagrad
+
+    torch.manual_seed(0)
+    shapes = [(300, 64), (7, 33), (5,)]
+    ref = [torch.randn(s, device="cuda") for s in shapes] + [torch.randn(4, 4)]
+    mine = [t.clone() for t in ref]
+    for t in ref + mine:
+        t.requires_grad_(True)
+    o_ref = torch.optim.Adagrad(ref, lr=0.1, **kw)
+    o_mine = FusedAdagrad(mine, lr=0.1, **kw)
+    for _ in range(4):
+        grads = [torch.randn_like(t) for t in ref]
+        for a, b, g in zip(ref, mine, grads):
+            a.grad, b.grad = g.clone(), g.clone()
+        o_ref.step()
+        o_mine.step()
+    for a, b in zip(ref, mine):
+        assert torch.allclose(a, b, rtol=0, atol=1e-6 * a.abs().max().item()), (a - b).abs().max()
+    sd = o_mine.state_dict()  # torch's layout: loads into a stock Adagrad
+    o2 = torch.optim.Adagrad(ref, lr=0.1, **kw)
+    o2.load_state_dict(sd)
