@@ -322,10 +322,14 @@ def extras(args, model, c, E, R, device):
     ej._prepare()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
+    ej._run()  # first run: lazily built filter indexes and allocator warm-up
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
     tr = ej._run()
     torch.cuda.synchronize()
     res["eval_test_triples"] = int(len(ds.split("test")))
-    res["eval_seconds"] = round(time.perf_counter() - t0, 4)
+    res["eval_seconds"] = round(time.perf_counter() - t1, 4)
+    res["eval_first_run_seconds"] = round(t1 - t0, 4)
     res["eval_mrr_filtered"] = tr["mean_reciprocal_rank_filtered"]
     res["eval_hits_at_10_filtered"] = tr["hits_at_10_filtered"]
     res.update(other_configs(device))

@@ -508,3 +508,19 @@ int kge_bwd3_t(const float* g, int64_t ldg, const float* q, int64_t ldq, const i
   if (!accumulate) return launch<true, 3, false, false>(g, ldg, q, ldq, nullptr, dt, lddt, nullptr, m, d, n, 1, st);
   return launch<true, 1, false, false>(g, ldg, q, ldq, nullptr, dt, lddt, nullptr, m, d, n, 1, st);
 }
+
+// Dev-only variants for scripts/tune_bwd.py (not in include/kgescore.h): 0 = dQ as shipped
+// (split-K atomics), 1 = dQ with plain stores (wrong sums: prices the atomics), 2 = dT
+// written (C_MODE 3), 3 = dT read-modify-write (C_MODE 1).
+extern "C" int kge_dev_bwd3(int variant, const float* g, int64_t ldg, const float* x, int64_t ldx, int64_t n,
+                            int64_t m, int d, float* c, int64_t ldc, int splits, void* stream) {
+  hipStream_t st = as_stream(stream);
+  if (!vec_ok(g, ldg, m, x, ldx, d)) return KGE_ERR_ALIGN;
+  switch (variant) {
+    case 0: return launch<false, 0, false, true>(g, ldg, x, ldx, nullptr, c, ldc, nullptr, n, d, m, splits, st);
+    case 1: return launch<false, 3, false, true>(g, ldg, x, ldx, nullptr, c, ldc, nullptr, n, d, m, splits, st);
+    case 2: return launch<true, 3, false, true>(g, ldg, x, ldx, nullptr, c, ldc, nullptr, m, d, n, 1, st);
+    case 3: return launch<true, 1, false, true>(g, ldg, x, ldx, nullptr, c, ldc, nullptr, m, d, n, 1, st);
+    default: return KGE_ERR_ARG;
+  }
+}

@@ -73,7 +73,7 @@ __global__ void __launch_bounds__(64 * WM * WN, 1)
   constexpr int A_G = BM / 16 / NW;                      // 1-KB A chunks per plane per wave
   constexpr int XS = TM / 4 > 0 ? TM / 4 : 1;            // bands computed before the staging block
   static_assert((BM / 16) % NW == 0, "A chunks");
-  static_assert(C::B_PER_T == 4, "KGE_WAIT_VM names 4 registers");
+  static_assert(C::B_PER_T == 4 || C::B_PER_T == 2, "KGE_WAIT_VM names the B registers");
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -122,8 +122,13 @@ __global__ void __launch_bounds__(64 * WM * WN, 1)
 
     // Every VMEM operation of the K loop is inline asm, counted by hand: per stage a wave
     // issues 2 A_G DMAs (stage st + 1), then B_PER_T register loads (stage st + 2).
-#define KGE_WAIT_VM(N) \
-  asm volatile("s_waitcnt vmcnt(%4)" : "+v"(rv[0]), "+v"(rv[1]), "+v"(rv[2]), "+v"(rv[3]) : "i"(N) : "memory")
+#define KGE_WAIT_VM(N)                                                                                   \
+  do {                                                                                                   \
+    if constexpr (C::B_PER_T == 4)                                                                       \
+      asm volatile("s_waitcnt vmcnt(%4)" : "+v"(rv[0]), "+v"(rv[1]), "+v"(rv[2]), "+v"(rv[3]) : "i"(N) : "memory"); \
+    else                                                                                                 \
+      asm volatile("s_waitcnt vmcnt(%2)" : "+v"(rv[0]), "+v"(rv[C::B_PER_T - 1]) : "i"(N) : "memory");  \
+  } while (0)
     auto glds_a = [&](int buf, int k0) {
       const unsigned base = smem_base + buf * C::STAGE;
 #pragma unroll
@@ -373,6 +378,8 @@ extern "C" int kge_dev_score_dot_persist(int variant, const void* qhi, const voi
   switch (variant) {
     case 0: return launch_persist16<256, 256, 2, 4>(h, l, ldq, t, ldt, tidx, n, m, d, s, lds, st);
     case 1: return launch_persist16<128, 256, 2, 4>(h, l, ldq, t, ldt, tidx, n, m, d, s, lds, st);
+    case 2: return launch_persist16<256, 128, 4, 2>(h, l, ldq, t, ldt, tidx, n, m, d, s, lds, st);
+    case 3: return launch_persist16<256, 128, 2, 4>(h, l, ldq, t, ldt, tidx, n, m, d, s, lds, st);
     case 11: return launch_persist16<256, 256, 2, 4, 1>(h, l, ldq, t, ldt, tidx, n, m, d, s, lds, st);
     case 12: return launch_persist16<256, 256, 2, 4, 2>(h, l, ldq, t, ldt, tidx, n, m, d, s, lds, st);
     case 13: return launch_persist16<256, 256, 2, 4, 3>(h, l, ldq, t, ldt, tidx, n, m, d, s, lds, st);

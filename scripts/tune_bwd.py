@@ -1,0 +1,39 @@
+"""Dev sweep of the backward GEMM variants at the stacked C2 shape (2048 queries x 14541
+entities x 512): interleaved rounds in one process (kge_dev_bwd3 / the shipped entries)."""
+import ctypes, sys
+sys.path.insert(0, '.'); sys.path.insert(0, 'kge-1_amd')
+import numpy as np, torch
+from kge import _lib as L
+lib = L.lib()
+lib.kge_dev_bwd3.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_int64,
+                             ctypes.c_int64, ctypes.c_int64, ctypes.c_int, ctypes.c_void_p, ctypes.c_int64,
+                             ctypes.c_int, ctypes.c_void_p]
+n, m, d = 2048, 14541, 512
+if len(sys.argv) > 1: n = int(sys.argv[1])
+torch.manual_seed(0)
+mp = (m + 3) // 4 * 4
+gbuf = torch.randn(n, mp, device='cuda') * 1e-4
+g = gbuf[:, :m]
+ent = torch.randn(m, d, device='cuda') * 0.1
+q = torch.randn(n, d, device='cuda') * 0.1
+dq = torch.zeros(n, d, device='cuda'); de = torch.zeros(m, d, device='cuda')
+st = L.stream()
+splits = int(sys.argv[2]) if len(sys.argv) > 2 else 8
+def run(v):
+    if v in (0, 1):
+        assert lib.kge_dev_bwd3(v, g.data_ptr(), mp, ent.data_ptr(), d, n, m, d, dq.data_ptr(), d, splits, st) == 0
+    else:
+        assert lib.kge_dev_bwd3(v, g.data_ptr(), mp, q.data_ptr(), d, n, m, d, de.data_ptr(), d, 1, st) == 0
+variants = [int(x) for x in sys.argv[3].split(',')] if len(sys.argv) > 3 else [0, 1, 2, 3]
+res = {v: [] for v in variants}
+for rnd in range(5):
+    for v in variants:
+        for _ in range(2): run(v)
+        a = torch.cuda.Event(enable_timing=True); b = torch.cuda.Event(enable_timing=True)
+        a.record()
+        for _ in range(10): run(v)
+        b.record(); torch.cuda.synchronize()
+        res[v].append(a.elapsed_time(b) / 10 * 1e3)
+for v in variants:
+    t = np.median(res[v])
+    print(f"variant {v}: median {t:.1f} us  -> {3 * 2 * n * m * d / t / 1e6:.0f} TF bf16")
