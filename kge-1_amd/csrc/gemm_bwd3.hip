@@ -246,7 +246,7 @@ __device__ __forceinline__ bf16x8 tr_frag(const unsigned char* img, int c0, int 
   return f;
 }
 
-__device__ __forceinline__ void split4(const float4& v, bf16x4& h, bf16x4& l) { split_bf16x4(v, h, l); }
+__device__ __forceinline__ void split4(const float4& v, bf16x4& h, bf16x4& l) { split_bf16x4_pk(v, h, l); }
 
 template <bool A_T, int C_MODE, bool GATHER>
 __global__ void __launch_bounds__(NT, 1)

@@ -112,7 +112,7 @@ __global__ void __launch_bounds__(256) prep_elementwise_vec(const float* __restr
     if (out.q) *reinterpret_cast<float4*>(out.q + i * out.ldq + k) = v;
     if (out.hi) {
       bf16x4 h, l;
-      split_bf16x4(v, h, l);
+      split_bf16x4_pk(v, h, l);
       *reinterpret_cast<bf16x4*>(out.hi + i * out.ldp + k) = h;
       *reinterpret_cast<bf16x4*>(out.lo + i * out.ldp + k) = l;
     }

@@ -72,6 +72,11 @@ __global__ void __launch_bounds__(64 * WM * WN, 1)
   constexpr int SCR_LD = WCOLS + 4;                      // padded scratch row (floats)
   constexpr int A_G = BM / 16 / NW;                      // 1-KB A chunks per plane per wave
   constexpr int XS = TM / 4 > 0 ? TM / 4 : 1;            // bands computed before the staging block
+  constexpr bool TR = (ABL & 8) != 0;                    // transposed MFMA, stores from registers
+  constexpr bool TRL = (ABL & 64) != 0;                  // transposed MFMA, float4 LDS scratch epilogue
+  constexpr bool TRM = TR || TRL;
+  constexpr bool PRIO = (ABL & 16) != 0;                 // s_setprio(1) around the MFMA bands
+  static_assert(!TR || WN > 1, "TR: x-outer compute");
   static_assert((BM / 16) % NW == 0, "A chunks");
   static_assert(C::B_PER_T == 4 || C::B_PER_T == 2, "KGE_WAIT_VM names the B registers");
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -146,17 +151,48 @@ __global__ void __launch_bounds__(64 * WM * WN, 1)
       unsigned char* bhi = stg + 2 * C::PLANE_A;
       unsigned char* blo = bhi + C::PLANE_B;
       const bool tail = k0 + BK > d;  // only the K tail needs zeros
+      if constexpr ((ABL & 128) != 0) {
+        if (!tail) {  // wave-uniform: no per-lane masking outside the K tail
+#pragma unroll
+          for (int i = 0; i < C::B_PER_T; ++i) {
+            const float4 v = make_float4(__uint_as_float(rv[i].x), __uint_as_float(rv[i].y),
+                                         __uint_as_float(rv[i].z), __uint_as_float(rv[i].w));
+            bf16x4 h, l;
+            split_bf16x4_pk(v, h, l);
+            if (i == C::B_PER_T - 1 && !b_last) continue;
+            *reinterpret_cast<bf16x4*>(bhi + b_off0 + i * (C::NT / 8) * 64) = h;
+            *reinterpret_cast<bf16x4*>(blo + b_off0 + i * (C::NT / 8) * 64) = l;
+          }
+          return;
+        }
+      }
 #pragma unroll
       for (int i = 0; i < C::B_PER_T; ++i) {
         const unsigned mk = (!tail || k0 + b_col < d) ? 0xffffffffu : 0u;
         const float4 v = make_float4(__uint_as_float(rv[i].x & mk), __uint_as_float(rv[i].y & mk),
                                      __uint_as_float(rv[i].z & mk), __uint_as_float(rv[i].w & mk));
         bf16x4 h, l;
-        split_bf16x4(v, h, l);
+        if constexpr ((ABL & 128) != 0)
+          split_bf16x4_pk(v, h, l);
+        else
+          split_bf16x4(v, h, l);
         if (i == C::B_PER_T - 1 && !b_last) continue;
         *reinterpret_cast<bf16x4*>(bhi + b_off0 + i * (C::NT / 8) * 64) = h;
         *reinterpret_cast<bf16x4*>(blo + b_off0 + i * (C::NT / 8) * 64) = l;
       }
+    };
+
+    // one slot of store_b outside the K tail (ABL & 256: the slots are spread over the bands)
+    auto store_b_slot = [&](unsigned char* stg, int i) {
+      unsigned char* bhi = stg + 2 * C::PLANE_A;
+      unsigned char* blo = bhi + C::PLANE_B;
+      const float4 v = make_float4(__uint_as_float(rv[i].x), __uint_as_float(rv[i].y),
+                                   __uint_as_float(rv[i].z), __uint_as_float(rv[i].w));
+      bf16x4 h, l;
+      split_bf16x4_pk(v, h, l);
+      if (i == C::B_PER_T - 1 && !b_last) return;
+      *reinterpret_cast<bf16x4*>(bhi + b_off0 + i * (C::NT / 8) * 64) = h;
+      *reinterpret_cast<bf16x4*>(blo + b_off0 + i * (C::NT / 8) * 64) = l;
     };
 
     f32x4 acc[TM][TN];
@@ -186,9 +222,15 @@ __global__ void __launch_bounds__(64 * WM * WN, 1)
         const bf16x8 a_l = *reinterpret_cast<const bf16x8*>(alo + sw16_off(ra, fs));
 #pragma unroll
         for (int y = 0; y < TN; ++y) {
-          acc[x][y] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a_l, b_h[y], acc[x][y], 0, 0, 0);
-          acc[x][y] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a_h, b_l[y], acc[x][y], 0, 0, 0);
-          acc[x][y] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a_h, b_h[y], acc[x][y], 0, 0, 0);
+          if constexpr (TRM) {  // C^T tile: entity rows x query columns
+            acc[x][y] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b_h[y], a_l, acc[x][y], 0, 0, 0);
+            acc[x][y] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b_l[y], a_h, acc[x][y], 0, 0, 0);
+            acc[x][y] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b_h[y], a_h, acc[x][y], 0, 0, 0);
+          } else {
+            acc[x][y] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a_l, b_h[y], acc[x][y], 0, 0, 0);
+            acc[x][y] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a_h, b_l[y], acc[x][y], 0, 0, 0);
+            acc[x][y] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a_h, b_h[y], acc[x][y], 0, 0, 0);
+          }
         }
       }
     };
@@ -237,12 +279,35 @@ __global__ void __launch_bounds__(64 * WM * WN, 1)
       const unsigned char* cur = smem + (st & 1) * C::STAGE;
       const bool more = !(ABL & 2) && st + 1 < nst;
       if (more) glds_a(nb, (st + 1) * BK);
+      if constexpr ((ABL & 256) != 0 && WN > 1) {
+        static_assert(TM - XS > C::B_PER_T, "one slot per band after the first XS");
+        compute_b(cur);
+        compute_x(cur, 0, XS);
+        const bool tail_next = (st + 2) * BK > d;
+        if (more) {
+          KGE_WAIT_VM(2 * A_G);  // B(st + 1) has landed
+          if (tail_next) store_b(smem + nb * C::STAGE, (st + 1) * BK);
+        }
+#pragma unroll
+        for (int x = XS; x < TM; ++x) {
+          compute_x(cur, x, x + 1);
+          if (x - XS < C::B_PER_T && more && !tail_next) store_b_slot(smem + nb * C::STAGE, x - XS);
+          if (x - XS == C::B_PER_T - 1) load_b(min(st + 2, nst - 1) * BK);
+        }
+        KGE_WAIT_VM(C::B_PER_T);  // A(st + 1) has landed
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        continue;
+      }
       if constexpr (WN == 1) {
         compute_a(cur);
         compute_y(cur, 0, YS);
       } else {
         compute_b(cur);
+        if constexpr (PRIO) __builtin_amdgcn_s_setprio(1);
         compute_x(cur, 0, XS);
+        if constexpr (PRIO) __builtin_amdgcn_s_setprio(0);
       }
       if (more) {
         KGE_WAIT_VM(2 * A_G);  // B(st + 1) has landed
@@ -251,8 +316,11 @@ __global__ void __launch_bounds__(64 * WM * WN, 1)
       if (!(ABL & 2)) load_b(min(st + 2, nst - 1) * BK);
       if constexpr (WN == 1)
         compute_y(cur, YS, TN);
-      else
+      else {
+        if constexpr (PRIO) __builtin_amdgcn_s_setprio(1);
         compute_x(cur, XS, TM);
+        if constexpr (PRIO) __builtin_amdgcn_s_setprio(0);
+      }
       KGE_WAIT_VM(C::B_PER_T);  // A(st + 1) has landed
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
@@ -261,16 +329,51 @@ __global__ void __launch_bounds__(64 * WM * WN, 1)
     KGE_WAIT_VM(0);
 #undef KGE_WAIT_VM
 
+    if constexpr (TR) {
+      // C^T of 16x16: lane holds query (lane & 15) and 4 consecutive entities 4 (lane >> 4) + r,
+      // i.e. a float4 of one score row: stored straight from the accumulators (16 rows x 64 B
+      // per wave-instruction, the four y tiles of a band complete 256-B row segments)
+#pragma unroll
+      for (int x = 0; x < TM; ++x) {
+        const int i = m0 + wr * (BM / WM) + x * 16 + fr;
+#pragma unroll
+        for (int y = 0; y < TN; ++y) {
+          const int j = n0 + wc * WCOLS + y * 16 + 4 * fs;
+          float* dst = s + (int64_t)i * lds + j;
+          const f32x4 v = acc[x][y];
+          if (i >= n) continue;
+          if (ABL & 1) {
+            if (v.x == 1234.5f) dst[0] = v.y;
+          } else if (j + 3 < m) {
+            if constexpr ((ABL & 32) != 0)
+              __builtin_nontemporal_store(f32x4u{v.x, v.y, v.z, v.w}, reinterpret_cast<f32x4u*>(dst));
+            else
+              *reinterpret_cast<f32x4u*>(dst) = f32x4u{v.x, v.y, v.z, v.w};
+          } else {
+            if (j < m) dst[0] = v.x;
+            if (j + 1 < m) dst[1] = v.y;
+            if (j + 2 < m) dst[2] = v.z;
+          }
+        }
+      }
+      __syncthreads();
+      continue;
+    }
     // epilogue: C/D of 16x16 -- lane holds column (lane & 15), rows 4 (lane >> 4) + r
     __syncthreads();  // stage buffers free: per-wave scratch of 16 rows x WCOLS (+4) floats
     float* scr = reinterpret_cast<float*>(smem) + wave * 16 * SCR_LD;
     constexpr int LPR = WCOLS / 4;  // lanes per scratch row (float4 each)
 #pragma unroll
     for (int x = 0; x < TM; ++x) {
+      if constexpr (TRL) {  // lane: query fr, entities y 16 + 4 fs .. +3 -- one float4 per y
 #pragma unroll
-      for (int y = 0; y < TN; ++y)
+        for (int y = 0; y < TN; ++y) *reinterpret_cast<f32x4*>(scr + fr * SCR_LD + y * 16 + 4 * fs) = acc[x][y];
+      } else {
 #pragma unroll
-        for (int r = 0; r < 4; ++r) scr[(4 * fs + r) * SCR_LD + y * 16 + fr] = acc[x][y][r];
+        for (int y = 0; y < TN; ++y)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) scr[(4 * fs + r) * SCR_LD + y * 16 + fr] = acc[x][y][r];
+      }
       const int i0 = m0 + wr * (BM / WM) + x * 16;
 #pragma unroll
       for (int pass = 0; pass < (16 * LPR + 63) / 64; ++pass) {
@@ -285,7 +388,12 @@ __global__ void __launch_bounds__(64 * WM * WN, 1)
         if (ABL & 1) {
           if (v.x == 1234.5f) dst[0] = v.y;  // keep the values live, store (almost) nothing
         } else if (j + 3 < m) {
-          *reinterpret_cast<f32x4u*>(dst) = f32x4u{v.x, v.y, v.z, v.w};
+          if constexpr ((ABL & 512) != 0)
+            asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(dst), "v"(f32x4{v.x, v.y, v.z, v.w}) : "memory");
+          else if constexpr ((ABL & 1024) != 0)
+            asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1" ::"v"(dst), "v"(f32x4{v.x, v.y, v.z, v.w}) : "memory");
+          else
+            *reinterpret_cast<f32x4u*>(dst) = f32x4u{v.x, v.y, v.z, v.w};
         } else {
           if (j < m) dst[0] = v.x;
           if (j + 1 < m) dst[1] = v.y;
@@ -304,7 +412,8 @@ __global__ void __launch_bounds__(64 * WM * WN, 1)
 
 template <int BM, int BN, int WM, int WN, int ABL = 0>
 int launch_persist16(const __bf16* qhi, const __bf16* qlo, int64_t ldq, const float* t, int64_t ldt,
-                     const int64_t* tidx, int64_t n, int64_t m, int d, float* s, int64_t lds, hipStream_t st) {
+                     const int64_t* tidx, int64_t n, int64_t m, int d, float* s, int64_t lds, hipStream_t st,
+                     int tiles_per_wg = 0) {
   using C = PCfg<BM, BN, WM, WN>;
   const int nrt = (int)((n + BM - 1) / BM);
   const int64_t ntiles = (int64_t)nrt * ((m + BN - 1) / BN);
@@ -320,6 +429,7 @@ int launch_persist16(const __bf16* qhi, const __bf16* qlo, int64_t ldq, const fl
   int grid = kge_num_cus();
   grid = (int)std::min<int64_t>(grid, (ntiles + 7) / 8 * 8);
   grid = std::max(8, grid / 8 * 8);
+  if (tiles_per_wg > 0) grid = (int)std::max<int64_t>(8, ((ntiles + tiles_per_wg - 1) / tiles_per_wg + 7) / 8 * 8);
   score_dot_persist16_kernel<BM, BN, WM, WN, ABL><<<dim3(grid), dim3(C::NT), shmem, st>>>(
       qhi, qlo, ldq, t, ldt, tidx, (int)n, (int)m, d, s, lds, nrt, (int)ntiles);
   KGE_CHECK_LAUNCH();
@@ -363,8 +473,10 @@ extern "C" int kge_score_dot_split(const void* qhi, const void* qlo, int64_t ldq
   hipStream_t st = as_stream(stream);
   const __bf16* h = (const __bf16*)qhi;
   const __bf16* l = (const __bf16*)qlo;
-  if (n > 128) return launch_persist16<256, 256, 2, 4>(h, l, ldq, t, ldt, tidx, n, m, d, s, lds, st);
-  return launch_persist16<128, 256, 2, 4>(h, l, ldq, t, ldt, tidx, n, m, d, s, lds, st);
+  // ABL 128: paired bf16 split with the K-tail mask only in the tail stage (-2.6 % vs the
+  // per-element split, interleaved A/B on MI355X)
+  if (n > 128) return launch_persist16<256, 256, 2, 4, 128>(h, l, ldq, t, ldt, tidx, n, m, d, s, lds, st);
+  return launch_persist16<128, 256, 2, 4, 128>(h, l, ldq, t, ldt, tidx, n, m, d, s, lds, st);
 }
 
 extern "C" int kge_dev_score_dot_persist(int variant, const void* qhi, const void* qlo, int64_t ldq,
@@ -385,6 +497,25 @@ extern "C" int kge_dev_score_dot_persist(int variant, const void* qhi, const voi
     case 13: return launch_persist16<256, 256, 2, 4, 3>(h, l, ldq, t, ldt, tidx, n, m, d, s, lds, st);
     case 14: return launch_persist16<256, 256, 2, 4, 4>(h, l, ldq, t, ldt, tidx, n, m, d, s, lds, st);
     case 17: return launch_persist16<256, 256, 2, 4, 7>(h, l, ldq, t, ldt, tidx, n, m, d, s, lds, st);
+    case 30: return launch_persist16<256, 256, 2, 4, 8>(h, l, ldq, t, ldt, tidx, n, m, d, s, lds, st);
+    case 31: return launch_persist16<256, 256, 2, 4, 9>(h, l, ldq, t, ldt, tidx, n, m, d, s, lds, st);
+    case 32: return launch_persist16<256, 256, 2, 4, 24>(h, l, ldq, t, ldt, tidx, n, m, d, s, lds, st);
+    case 33: return launch_persist16<256, 256, 2, 4, 16>(h, l, ldq, t, ldt, tidx, n, m, d, s, lds, st);
+    case 34: return launch_persist16<256, 256, 2, 4, 12>(h, l, ldq, t, ldt, tidx, n, m, d, s, lds, st);
+    case 35: return launch_persist16<256, 128, 2, 4, 8>(h, l, ldq, t, ldt, tidx, n, m, d, s, lds, st, 2);
+    case 36: return launch_persist16<256, 128, 2, 4, 8>(h, l, ldq, t, ldt, tidx, n, m, d, s, lds, st);
+    case 37: return launch_persist16<256, 128, 4, 2, 8>(h, l, ldq, t, ldt, tidx, n, m, d, s, lds, st, 2);
+    case 38: return launch_persist16<256, 256, 2, 4, 40>(h, l, ldq, t, ldt, tidx, n, m, d, s, lds, st);
+    case 40: return launch_persist16<256, 256, 2, 4, 64>(h, l, ldq, t, ldt, tidx, n, m, d, s, lds, st);
+    case 41: return launch_persist16<256, 256, 2, 4, 65>(h, l, ldq, t, ldt, tidx, n, m, d, s, lds, st);
+    case 42: return launch_persist16<256, 256, 2, 4, 68>(h, l, ldq, t, ldt, tidx, n, m, d, s, lds, st);
+    case 50: return launch_persist16<256, 256, 2, 4, 128>(h, l, ldq, t, ldt, tidx, n, m, d, s, lds, st);
+    case 51: return launch_persist16<256, 256, 2, 4, 132>(h, l, ldq, t, ldt, tidx, n, m, d, s, lds, st);
+    case 52: return launch_persist16<256, 256, 2, 4, 129>(h, l, ldq, t, ldt, tidx, n, m, d, s, lds, st);
+    case 53: return launch_persist16<256, 256, 2, 4, 384>(h, l, ldq, t, ldt, tidx, n, m, d, s, lds, st);
+    case 54: return launch_persist16<256, 256, 2, 4, 388>(h, l, ldq, t, ldt, tidx, n, m, d, s, lds, st);
+    case 55: return launch_persist16<256, 256, 2, 4, 640>(h, l, ldq, t, ldt, tidx, n, m, d, s, lds, st);
+    case 56: return launch_persist16<256, 256, 2, 4, 1152>(h, l, ldq, t, ldt, tidx, n, m, d, s, lds, st);
     case 20: return launch_persist16<256, 240, 8, 1>(h, l, ldq, t, ldt, tidx, n, m, d, s, lds, st);
     case 21: return launch_persist16<256, 240, 8, 1, 1>(h, l, ldq, t, ldt, tidx, n, m, d, s, lds, st);
     case 22: return launch_persist16<256, 256, 8, 1>(h, l, ldq, t, ldt, tidx, n, m, d, s, lds, st);

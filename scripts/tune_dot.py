@@ -19,7 +19,24 @@ st = L.stream()
 assert lib.kge_split_rows(q.data_ptr(), d, B, d, qh.data_ptr(), ql.data_ptr(), ldo, st) == 0
 ref = (q.double() @ ent.double().T)
 out = torch.empty(B, E, device='cuda')
+LDA = (E + 31) // 32 * 32  # 128-B aligned score rows ('a' suffix)
+outa_buf = torch.empty(B, LDA, device='cuda')
+outa = outa_buf[:, :E]
 def run(v):
+    global out
+    if v == 'fill':
+        out.fill_(1.0); return
+    if v == 'filla':
+        outa.fill_(1.0); return
+    if isinstance(v, str) and v.endswith('a'):
+        o = out
+        out = outa
+        try:
+            assert lib.kge_dev_score_dot_persist(int(v[1:-1]), qh.data_ptr(), ql.data_ptr(), ldo, ent.data_ptr(), d, None,
+                                                 B, E, d, outa_buf.data_ptr(), LDA, st) == 0
+        finally:
+            out = o
+        return
     if v == 'old': L.score_dot(q, ent, None, 1, out=out)
     elif v == 'old32': L.score_dot(q, ent, None, 0, out=out)
     elif isinstance(v, str) and v.startswith('p'):
@@ -30,8 +47,11 @@ def run(v):
 variants = sys.argv[2].split(',') if len(sys.argv) > 2 else ['p0', 'p1']
 res = {v: [] for v in variants}
 for v in variants:
-    out.zero_(); run(v); torch.cuda.synchronize()
-    err = ((out.double() - ref).abs().amax(1) / ref.abs().amax(1)).max().item() 
+    if v.startswith('fill'):
+        continue
+    o = outa if v.endswith('a') else out
+    o.zero_(); run(v); torch.cuda.synchronize()
+    err = ((o.double() - ref).abs().amax(1) / ref.abs().amax(1)).max().item()
     print(f"variant {v}: max rel err {err:.2e}", flush=True)
 for rnd in range(5):
     for v in variants:
