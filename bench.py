@@ -333,7 +333,63 @@ def extras(args, model, c, E, R, device):
     res["eval_mrr_filtered"] = tr["mean_reciprocal_rank_filtered"]
     res["eval_hits_at_10_filtered"] = tr["hits_at_10_filtered"]
     res.update(other_configs(device))
+    res.update(c5_shard(args, device))
     return res
+
+
+def c5_shard(args, device):
+    """BASELINE configs[4] per GPU: ComplEx-512 1vsAll on Wikidata5M with the entity table
+    row-sharded over 8 GPUs -- one rank's shard of ceil(4,594,485 / 8) = 574,311 rows scored
+    by a batch of 1024 queries (score_sp through the model API; 2.35 GB of scores per step),
+    plus the contraction kernel alone (HIP events around back-to-back launches)."""
+    from kge import Dataset, KgeModel, _lib
+
+    E_full, R, _ = __import__("kge.dataset", fromlist=["SHAPES"]).SHAPES["wikidata5m"]
+    E = (E_full + 7) // 8
+    B, d = args.batch, args.dim
+    c = make_config(args, device)
+    c.set("dataset.num_entities", E)
+    c.set("dataset.num_relations", R)
+    torch.manual_seed(0)
+    model = KgeModel.create(c, Dataset(c, None))
+    model.eval()
+    g = torch.Generator(device=device).manual_seed(3)
+    s = torch.randint(0, E, (8, B), device=device, generator=g)
+    p = torch.randint(0, R, (8, B), device=device, generator=g)
+    out = {}
+
+    def step(i):
+        with torch.no_grad():
+            return model.score_sp(s[i % 8], p[i % 8])
+    sec = timed_loop(step, 8, 3, 1)
+    out["c5_shard_rows"] = E
+    out["c5_shard_score_sp_ms"] = round(sec * 1e3, 3)
+    out["c5_shard_scored_triples_per_s"] = B * E / sec
+    ent = model._entity_embedder._embeddings.weight.detach()
+    rel = model._relation_embedder._embeddings.weight.detach()
+    with torch.no_grad():
+        q = _lib.prep_query(_lib.COMPLEX, _lib.DIR_SP, ent, s[0], rel, p[0], B, d, d)
+        qh, ql = _lib.split_rows(q)
+        buf = torch.empty(B, E, device=device)
+        for _ in range(3):
+            _lib.score_dot_split(qh, ql, ent, None, d, out=buf)
+        a = torch.cuda.Event(enable_timing=True)
+        b = torch.cuda.Event(enable_timing=True)
+        a.record()
+        for _ in range(10):
+            _lib.score_dot_split(qh, ql, ent, None, d, out=buf)
+        b.record()
+        torch.cuda.synchronize()
+    k_s = a.elapsed_time(b) / 10 / 1e3
+    flops = 2.0 * B * E * d
+    nbytes = 4.0 * (B * d + E * d + B * E)
+    out["c5_shard_kernel_us"] = round(k_s * 1e6, 1)
+    out["c5_shard_kernel_tflops"] = round(flops / k_s / 1e12, 1)
+    out["c5_shard_kernel_mfma_frac"] = round(flops / k_s / 1e12 / (BF16_DENSE_TFLOPS / 3.0), 4)
+    out["c5_shard_kernel_hbm_frac"] = round(nbytes / k_s / 1e9 / HBM_PEAK_GBS, 4)
+    del model, buf
+    torch.cuda.empty_cache()
+    return out
 
 
 def _job_step_time(cfg, dataset, batch, steps=10, warmup=3):

@@ -58,6 +58,19 @@ __device__ __forceinline__ unsigned lds_addr(const void* p) {
   return (unsigned)(uintptr_t)(const __attribute__((address_space(3))) void*)p;
 }
 
+// dev: address-check build (ABL & 2048) records the first out-of-range global access here
+// instead of performing it: [0] count, [1] kind (1 A-hi DMA, 2 A-lo DMA, 3 B load, 4 store),
+// [2] tile, [3] stage, [4] thread, [5] element offset from the operand base
+__device__ unsigned long long kge_dbg_rec[8];
+__device__ __forceinline__ bool kge_dbg_bad(int kind, int64_t off, int64_t lim, int tile, int st) {
+  if (off >= 0 && off < lim) return false;
+  if (atomicAdd(&kge_dbg_rec[0], 1ull) == 0) {
+    kge_dbg_rec[1] = kind; kge_dbg_rec[2] = tile; kge_dbg_rec[3] = st;
+    kge_dbg_rec[4] = threadIdx.x + 512ull * blockIdx.x; kge_dbg_rec[5] = (unsigned long long)off;
+  }
+  return true;
+}
+
 // ABL: dev-only ablation / probe switches (kge_dev_score_dot_persist): 1 = no score stores,
 // 2 = no staging after the prologue, 4 = per-workgroup clock probe written to row n of s.
 template <int BM, int BN, int WM, int WN, int ABL = 0>
@@ -139,13 +152,26 @@ __global__ void __launch_bounds__(64 * WM * WN, 1)
 #pragma unroll
       for (int i = 0; i < A_G; ++i) {
         const unsigned c = (unsigned)(wave * A_G + i) * 1024u;
+        if constexpr ((ABL & 2048) != 0) {
+          const int64_t oh = (ga[i] + k0) - qhi, ol = (ga[i] + lo_off + k0) - qlo;
+          if (kge_dbg_bad(6, (int64_t)(base + C::PLANE_A + c - smem_base), 2 * C::STAGE - 1023, tile, k0)) continue;
+          const bool bad = (int)kge_dbg_bad(1, oh, (int64_t)n * ldq - 7, tile, k0) | (int)kge_dbg_bad(2, ol, (int64_t)n * ldq - 7, tile, k0);
+          glds16_asm(bad ? qhi : ga[i] + k0, base + c);
+          glds16_asm(bad ? qlo : ga[i] + lo_off + k0, base + C::PLANE_A + c);
+          continue;
+        }
         glds16_asm(ga[i] + k0, base + c);
         glds16_asm(ga[i] + lo_off + k0, base + C::PLANE_A + c);
       }
     };
     auto load_b = [&](int k0) {
 #pragma unroll
-      for (int i = 0; i < C::B_PER_T; ++i) rv[i] = gload16_asm(b_src[i] + min(k0, d - 4 - b_col));
+      for (int i = 0; i < C::B_PER_T; ++i) {
+        const float* src = b_src[i] + min(k0, d - 4 - b_col);
+        if constexpr ((ABL & 2048) != 0)
+          if (kge_dbg_bad(3, src - t, (int64_t)(m - 1) * ldt + d - 3, tile, k0)) src = t;
+        rv[i] = gload16_asm(src);
+      }
     };
     auto store_b = [&](unsigned char* stg, int k0) {  // split fp32 -> bf16 hi / lo, LDS image
       unsigned char* bhi = stg + 2 * C::PLANE_A;
@@ -388,6 +414,9 @@ __global__ void __launch_bounds__(64 * WM * WN, 1)
         if (ABL & 1) {
           if (v.x == 1234.5f) dst[0] = v.y;  // keep the values live, store (almost) nothing
         } else if (j + 3 < m) {
+          if constexpr ((ABL & 2048) != 0) {
+            if (kge_dbg_bad(4, dst - s, (int64_t)(n - 1) * lds + m - 3, tile, -1)) continue;
+          }
           if constexpr ((ABL & 512) != 0)
             asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(dst), "v"(f32x4{v.x, v.y, v.z, v.w}) : "memory");
           else if constexpr ((ABL & 1024) != 0)
@@ -395,6 +424,9 @@ __global__ void __launch_bounds__(64 * WM * WN, 1)
           else
             *reinterpret_cast<f32x4u*>(dst) = f32x4u{v.x, v.y, v.z, v.w};
         } else {
+          if constexpr ((ABL & 2048) != 0) {
+            if (kge_dbg_bad(5, dst - s, (int64_t)(n - 1) * lds + m, tile, -1)) continue;
+          }
           if (j < m) dst[0] = v.x;
           if (j + 1 < m) dst[1] = v.y;
           if (j + 2 < m) dst[2] = v.z;
@@ -516,10 +548,27 @@ extern "C" int kge_dev_score_dot_persist(int variant, const void* qhi, const voi
     case 54: return launch_persist16<256, 256, 2, 4, 388>(h, l, ldq, t, ldt, tidx, n, m, d, s, lds, st);
     case 55: return launch_persist16<256, 256, 2, 4, 640>(h, l, ldq, t, ldt, tidx, n, m, d, s, lds, st);
     case 56: return launch_persist16<256, 256, 2, 4, 1152>(h, l, ldq, t, ldt, tidx, n, m, d, s, lds, st);
+    case 60: return launch_persist16<512, 128, 4, 2, 128>(h, l, ldq, t, ldt, tidx, n, m, d, s, lds, st);
+    case 61: return launch_persist16<512, 128, 4, 2, 129>(h, l, ldq, t, ldt, tidx, n, m, d, s, lds, st);
+    case 62: return launch_persist16<512, 128, 4, 2, 132>(h, l, ldq, t, ldt, tidx, n, m, d, s, lds, st);
+    case 63: return launch_persist16<512, 128, 4, 2, 384>(h, l, ldq, t, ldt, tidx, n, m, d, s, lds, st);
+    case 70: return launch_persist16<256, 256, 2, 4, 2176>(h, l, ldq, t, ldt, tidx, n, m, d, s, lds, st);
+    case 71: return launch_persist16<512, 128, 4, 2, 2176>(h, l, ldq, t, ldt, tidx, n, m, d, s, lds, st);
+    case 72: return launch_persist16<256, 256, 2, 4, 2048>(h, l, ldq, t, ldt, tidx, n, m, d, s, lds, st);
     case 20: return launch_persist16<256, 240, 8, 1>(h, l, ldq, t, ldt, tidx, n, m, d, s, lds, st);
     case 21: return launch_persist16<256, 240, 8, 1, 1>(h, l, ldq, t, ldt, tidx, n, m, d, s, lds, st);
     case 22: return launch_persist16<256, 256, 8, 1>(h, l, ldq, t, ldt, tidx, n, m, d, s, lds, st);
     case 24: return launch_persist16<256, 240, 8, 1, 4>(h, l, ldq, t, ldt, tidx, n, m, d, s, lds, st);
     default: return KGE_ERR_ARG;
   }
+}
+
+extern "C" int kge_dev_dbg_read(unsigned long long* host8, int reset) {
+  hipError_t e = hipMemcpyFromSymbol(host8, HIP_SYMBOL(kge_dbg_rec), sizeof(unsigned long long) * 8);
+  if (e != hipSuccess) return (int)e;
+  if (reset) {
+    unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    e = hipMemcpyToSymbol(HIP_SYMBOL(kge_dbg_rec), z, sizeof(z));
+  }
+  return (int)e;
 }

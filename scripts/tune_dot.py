@@ -9,6 +9,8 @@ lib.kge_dev_score_dot_persist.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.
                                           ctypes.c_int64, ctypes.c_int, ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p]
 E, R, B, d = 14541, 237, 1024, 512
 if len(sys.argv) > 1: B = int(sys.argv[1])
+import os
+E = int(os.environ.get('KGE_E', E))
 torch.manual_seed(0)
 ent = (torch.randn(E, d) * 0.1).cuda(); rel = (torch.randn(R, d) * 0.1).cuda()
 s = torch.randint(0, E, (B,)).cuda(); p = torch.randint(0, R, (B,)).cuda()
