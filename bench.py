@@ -52,6 +52,7 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-extras", action="store_true")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--c5", action="store_true", help="also time one rank's Wikidata5M shard (configs[4])")
     return ap.parse_args()
 
 
@@ -333,7 +334,8 @@ def extras(args, model, c, E, R, device):
     res["eval_mrr_filtered"] = tr["mean_reciprocal_rank_filtered"]
     res["eval_hits_at_10_filtered"] = tr["hits_at_10_filtered"]
     res.update(other_configs(device))
-    res.update(c5_shard(args, device))
+    if args.c5:
+        res.update(c5_shard(args, device))
     return res
 
 
