@@ -75,6 +75,16 @@ __device__ __forceinline__ void split_bf16x4_pk(const float4& v, bf16x4& hi, bf1
   lo = __builtin_bit_cast(bf16x4, (uint2){l0, l1});
 }
 
+// The paired split with plain C++ subtractions (dev A/B against the asm form above).
+__device__ __forceinline__ void split_bf16x4_pk_c(const float4& v, bf16x4& hi, bf16x4& lo) {
+  const unsigned h0 = pack_bf16x2(v.x, v.y), h1 = pack_bf16x2(v.z, v.w);
+  const float rx = v.x - __uint_as_float(h0 << 16), ry = v.y - __uint_as_float(h0 & 0xffff0000u);
+  const float rz = v.z - __uint_as_float(h1 << 16), rw = v.w - __uint_as_float(h1 & 0xffff0000u);
+  const unsigned l0 = pack_bf16x2(rx, ry), l1 = pack_bf16x2(rz, rw);
+  hi = __builtin_bit_cast(bf16x4, (uint2){h0, h1});
+  lo = __builtin_bit_cast(bf16x4, (uint2){l0, l1});
+}
+
 // Compute units of the current device (256 on MI355X); cached per translation unit.
 static inline int kge_num_cus() {
   static int cus = 0;
@@ -92,6 +102,10 @@ int kge_bwd3_q(const float* g, int64_t ldg, const float* t, int64_t ldt, const i
                int64_t m, int d, float* dq, int64_t lddq, int cus, hipStream_t st);
 int kge_bwd3_t(const float* g, int64_t ldg, const float* q, int64_t ldq, const int64_t* tidx, int64_t n,
                int64_t m, int d, float* dt, int64_t lddt, int accumulate, hipStream_t st);
+
+// packed-VALU all-entities distance kernel (score_dist2.hip); -1 when the layout does not fit
+int kge_score_dist2(int kind, float sign, const float* q, int64_t ldq, const float* t, int64_t ldt,
+                    const int64_t* tidx, int64_t n, int64_t m, int d, float* s, int64_t lds, hipStream_t st);
 
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll

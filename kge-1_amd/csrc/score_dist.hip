@@ -259,6 +259,14 @@ __global__ void __launch_bounds__(NT) score_dist_bwd_kernel(float sign, const fl
 
 }  // namespace
 
+static int g_dist_impl = 2;  // 2: packed kernel when applicable, 1: this file's kernel (dev A/B)
+
+extern "C" int kge_dev_dist_impl(int impl) {
+  const int old = g_dist_impl;
+  if (impl == 1 || impl == 2) g_dist_impl = impl;
+  return old;
+}
+
 extern "C" int kge_score_dist(int kind, float sign, const float* q, int64_t ldq, const float* t, int64_t ldt,
                               const int64_t* tidx, int64_t n, int64_t m, int d, float* s, int64_t lds,
                               void* stream) {
@@ -269,6 +277,10 @@ extern "C" int kge_score_dist(int kind, float sign, const float* q, int64_t ldq,
   if (n == 0 || m == 0) return 0;
   KGE_REQUIRE((n + TM - 1) / TM < 65536);
   hipStream_t st = as_stream(stream);
+  if (g_dist_impl == 2) {  // packed-VALU kernel (score_dist2.hip) when the layout allows
+    const int r = kge_score_dist2(kind, sign, q, ldq, t, ldt, tidx, n, m, d, s, lds, st);
+    if (r >= 0) return r;
+  }
   dim3 grid((unsigned)((m + TN - 1) / TN), (unsigned)((n + TM - 1) / TM));
   switch (kind) {
     case KGE_DIST_L1: score_dist_kernel<KGE_DIST_L1><<<grid, NT, 0, st>>>(sign, q, ldq, t, ldt, tidx, (int)n, (int)m, d, s, lds); break;

@@ -184,7 +184,7 @@ __global__ void __launch_bounds__(64 * WM * WN, 1)
             const float4 v = make_float4(__uint_as_float(rv[i].x), __uint_as_float(rv[i].y),
                                          __uint_as_float(rv[i].z), __uint_as_float(rv[i].w));
             bf16x4 h, l;
-            split_bf16x4_pk(v, h, l);
+            if constexpr ((ABL & 16384) != 0) split_bf16x4_pk_c(v, h, l); else split_bf16x4_pk(v, h, l);
             if (i == C::B_PER_T - 1 && !b_last) continue;
             *reinterpret_cast<bf16x4*>(bhi + b_off0 + i * (C::NT / 8) * 64) = h;
             *reinterpret_cast<bf16x4*>(blo + b_off0 + i * (C::NT / 8) * 64) = l;
@@ -199,7 +199,7 @@ __global__ void __launch_bounds__(64 * WM * WN, 1)
                                      __uint_as_float(rv[i].z & mk), __uint_as_float(rv[i].w & mk));
         bf16x4 h, l;
         if constexpr ((ABL & 128) != 0)
-          split_bf16x4_pk(v, h, l);
+          if constexpr ((ABL & 16384) != 0) split_bf16x4_pk_c(v, h, l); else split_bf16x4_pk(v, h, l);
         else
           split_bf16x4(v, h, l);
         if (i == C::B_PER_T - 1 && !b_last) continue;
@@ -215,7 +215,7 @@ __global__ void __launch_bounds__(64 * WM * WN, 1)
       const float4 v = make_float4(__uint_as_float(rv[i].x), __uint_as_float(rv[i].y),
                                    __uint_as_float(rv[i].z), __uint_as_float(rv[i].w));
       bf16x4 h, l;
-      split_bf16x4_pk(v, h, l);
+      if constexpr ((ABL & 16384) != 0) split_bf16x4_pk_c(v, h, l); else split_bf16x4_pk(v, h, l);
       if (i == C::B_PER_T - 1 && !b_last) return;
       *reinterpret_cast<bf16x4*>(bhi + b_off0 + i * (C::NT / 8) * 64) = h;
       *reinterpret_cast<bf16x4*>(blo + b_off0 + i * (C::NT / 8) * 64) = l;
@@ -555,6 +555,7 @@ extern "C" int kge_dev_score_dot_persist(int variant, const void* qhi, const voi
     case 70: return launch_persist16<256, 256, 2, 4, 2176>(h, l, ldq, t, ldt, tidx, n, m, d, s, lds, st);
     case 71: return launch_persist16<512, 128, 4, 2, 2176>(h, l, ldq, t, ldt, tidx, n, m, d, s, lds, st);
     case 72: return launch_persist16<256, 256, 2, 4, 2048>(h, l, ldq, t, ldt, tidx, n, m, d, s, lds, st);
+    case 90: return launch_persist16<256, 256, 2, 4, 128 + 16384>(h, l, ldq, t, ldt, tidx, n, m, d, s, lds, st);
     case 20: return launch_persist16<256, 240, 8, 1>(h, l, ldq, t, ldt, tidx, n, m, d, s, lds, st);
     case 21: return launch_persist16<256, 240, 8, 1, 1>(h, l, ldq, t, ldt, tidx, n, m, d, s, lds, st);
     case 22: return launch_persist16<256, 256, 8, 1>(h, l, ldq, t, ldt, tidx, n, m, d, s, lds, st);
