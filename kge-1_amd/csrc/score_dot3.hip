@@ -41,6 +41,10 @@ __device__ __forceinline__ int sw16_off(int row, int slot) {
 // VMEM issued from inline asm: hipcc neither counts nor waits for these, the kernel does
 // (mixing LDS-DMA with compiler-visible register loads makes hipcc drain vmcnt to 0 at
 // every use of a loaded register, cdna_hip_programming.md 'Projection GEMM' item 4(b)).
+// An asm register load's destination counts as written at the end of the statement, so
+// every path from a load to the next use of its registers must pass a wait statement that
+// names them ("+v") and retires the load: hipcc is otherwise free to reuse the registers
+// (e.g. for an address) while the data is still in flight (cdna_hip_programming.md §5.7).
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ void glds16_asm(const void* gsrc, unsigned lds_dst) {
   unsigned keep;
@@ -58,19 +62,6 @@ __device__ __forceinline__ unsigned lds_addr(const void* p) {
   return (unsigned)(uintptr_t)(const __attribute__((address_space(3))) void*)p;
 }
 
-// dev: address-check build (ABL & 2048) records the first out-of-range global access here
-// instead of performing it: [0] count, [1] kind (1 A-hi DMA, 2 A-lo DMA, 3 B load, 4 store),
-// [2] tile, [3] stage, [4] thread, [5] element offset from the operand base
-__device__ unsigned long long kge_dbg_rec[8];
-__device__ __forceinline__ bool kge_dbg_bad(int kind, int64_t off, int64_t lim, int tile, int st) {
-  if (off >= 0 && off < lim) return false;
-  if (atomicAdd(&kge_dbg_rec[0], 1ull) == 0) {
-    kge_dbg_rec[1] = kind; kge_dbg_rec[2] = tile; kge_dbg_rec[3] = st;
-    kge_dbg_rec[4] = threadIdx.x + 512ull * blockIdx.x; kge_dbg_rec[5] = (unsigned long long)off;
-  }
-  return true;
-}
-
 // ABL: dev-only ablation / probe switches (kge_dev_score_dot_persist): 1 = no score stores,
 // 2 = no staging after the prologue, 4 = per-workgroup clock probe written to row n of s.
 template <int BM, int BN, int WM, int WN, int ABL = 0>
@@ -85,13 +76,9 @@ __global__ void __launch_bounds__(64 * WM * WN, 1)
   constexpr int SCR_LD = WCOLS + 4;                      // padded scratch row (floats)
   constexpr int A_G = BM / 16 / NW;                      // 1-KB A chunks per plane per wave
   constexpr int XS = TM / 4 > 0 ? TM / 4 : 1;            // bands computed before the staging block
-  constexpr bool TR = (ABL & 8) != 0;                    // transposed MFMA, stores from registers
-  constexpr bool TRL = (ABL & 64) != 0;                  // transposed MFMA, float4 LDS scratch epilogue
-  constexpr bool TRM = TR || TRL;
-  constexpr bool PRIO = (ABL & 16) != 0;                 // s_setprio(1) around the MFMA bands
-  static_assert(!TR || WN > 1, "TR: x-outer compute");
   static_assert((BM / 16) % NW == 0, "A chunks");
   static_assert(C::B_PER_T == 4 || C::B_PER_T == 2, "KGE_WAIT_VM names the B registers");
+  static_assert(WN > 1, "x-outer band loop");
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -152,73 +139,40 @@ __global__ void __launch_bounds__(64 * WM * WN, 1)
 #pragma unroll
       for (int i = 0; i < A_G; ++i) {
         const unsigned c = (unsigned)(wave * A_G + i) * 1024u;
-        if constexpr ((ABL & 2048) != 0) {
-          const int64_t oh = (ga[i] + k0) - qhi, ol = (ga[i] + lo_off + k0) - qlo;
-          if (kge_dbg_bad(6, (int64_t)(base + C::PLANE_A + c - smem_base), 2 * C::STAGE - 1023, tile, k0)) continue;
-          const bool bad = (int)kge_dbg_bad(1, oh, (int64_t)n * ldq - 7, tile, k0) | (int)kge_dbg_bad(2, ol, (int64_t)n * ldq - 7, tile, k0);
-          glds16_asm(bad ? qhi : ga[i] + k0, base + c);
-          glds16_asm(bad ? qlo : ga[i] + lo_off + k0, base + C::PLANE_A + c);
-          continue;
-        }
         glds16_asm(ga[i] + k0, base + c);
         glds16_asm(ga[i] + lo_off + k0, base + C::PLANE_A + c);
       }
     };
     auto load_b = [&](int k0) {
 #pragma unroll
-      for (int i = 0; i < C::B_PER_T; ++i) {
-        const float* src = b_src[i] + min(k0, d - 4 - b_col);
-        if constexpr ((ABL & 2048) != 0)
-          if (kge_dbg_bad(3, src - t, (int64_t)(m - 1) * ldt + d - 3, tile, k0)) src = t;
-        rv[i] = gload16_asm(src);
-      }
+      for (int i = 0; i < C::B_PER_T; ++i) rv[i] = gload16_asm(b_src[i] + min(k0, d - 4 - b_col));
     };
-    auto store_b = [&](unsigned char* stg, int k0) {  // split fp32 -> bf16 hi / lo, LDS image
+    // split fp32 -> bf16 hi / lo into the LDS image; only the K-tail stage masks (the
+    // branch is wave-uniform)
+    auto store_b = [&](unsigned char* stg, int k0) {
       unsigned char* bhi = stg + 2 * C::PLANE_A;
       unsigned char* blo = bhi + C::PLANE_B;
-      const bool tail = k0 + BK > d;  // only the K tail needs zeros
-      if constexpr ((ABL & 128) != 0) {
-        if (!tail) {  // wave-uniform: no per-lane masking outside the K tail
+      const bool tail = k0 + BK > d;
+      const unsigned mk = (!tail || k0 + b_col < d) ? 0xffffffffu : 0u;
+      auto put = [&](bool masked) {
 #pragma unroll
-          for (int i = 0; i < C::B_PER_T; ++i) {
-            const float4 v = make_float4(__uint_as_float(rv[i].x), __uint_as_float(rv[i].y),
-                                         __uint_as_float(rv[i].z), __uint_as_float(rv[i].w));
-            bf16x4 h, l;
-            if constexpr ((ABL & 16384) != 0) split_bf16x4_pk_c(v, h, l); else split_bf16x4_pk(v, h, l);
-            if (i == C::B_PER_T - 1 && !b_last) continue;
-            *reinterpret_cast<bf16x4*>(bhi + b_off0 + i * (C::NT / 8) * 64) = h;
-            *reinterpret_cast<bf16x4*>(blo + b_off0 + i * (C::NT / 8) * 64) = l;
-          }
-          return;
+        for (int i = 0; i < C::B_PER_T; ++i) {
+          float4 v = make_float4(__uint_as_float(rv[i].x), __uint_as_float(rv[i].y), __uint_as_float(rv[i].z),
+                                 __uint_as_float(rv[i].w));
+          if (masked)
+            v = make_float4(__uint_as_float(rv[i].x & mk), __uint_as_float(rv[i].y & mk),
+                            __uint_as_float(rv[i].z & mk), __uint_as_float(rv[i].w & mk));
+          bf16x4 h, l;
+          split_bf16x4_pk(v, h, l);
+          if (i == C::B_PER_T - 1 && !b_last) continue;
+          *reinterpret_cast<bf16x4*>(bhi + b_off0 + i * (C::NT / 8) * 64) = h;
+          *reinterpret_cast<bf16x4*>(blo + b_off0 + i * (C::NT / 8) * 64) = l;
         }
-      }
-#pragma unroll
-      for (int i = 0; i < C::B_PER_T; ++i) {
-        const unsigned mk = (!tail || k0 + b_col < d) ? 0xffffffffu : 0u;
-        const float4 v = make_float4(__uint_as_float(rv[i].x & mk), __uint_as_float(rv[i].y & mk),
-                                     __uint_as_float(rv[i].z & mk), __uint_as_float(rv[i].w & mk));
-        bf16x4 h, l;
-        if constexpr ((ABL & 128) != 0)
-          if constexpr ((ABL & 16384) != 0) split_bf16x4_pk_c(v, h, l); else split_bf16x4_pk(v, h, l);
-        else
-          split_bf16x4(v, h, l);
-        if (i == C::B_PER_T - 1 && !b_last) continue;
-        *reinterpret_cast<bf16x4*>(bhi + b_off0 + i * (C::NT / 8) * 64) = h;
-        *reinterpret_cast<bf16x4*>(blo + b_off0 + i * (C::NT / 8) * 64) = l;
-      }
-    };
-
-    // one slot of store_b outside the K tail (ABL & 256: the slots are spread over the bands)
-    auto store_b_slot = [&](unsigned char* stg, int i) {
-      unsigned char* bhi = stg + 2 * C::PLANE_A;
-      unsigned char* blo = bhi + C::PLANE_B;
-      const float4 v = make_float4(__uint_as_float(rv[i].x), __uint_as_float(rv[i].y),
-                                   __uint_as_float(rv[i].z), __uint_as_float(rv[i].w));
-      bf16x4 h, l;
-      if constexpr ((ABL & 16384) != 0) split_bf16x4_pk_c(v, h, l); else split_bf16x4_pk(v, h, l);
-      if (i == C::B_PER_T - 1 && !b_last) return;
-      *reinterpret_cast<bf16x4*>(bhi + b_off0 + i * (C::NT / 8) * 64) = h;
-      *reinterpret_cast<bf16x4*>(blo + b_off0 + i * (C::NT / 8) * 64) = l;
+      };
+      if (tail)  // wave-uniform
+        put(true);
+      else
+        put(false);
     };
 
     f32x4 acc[TM][TN];
@@ -248,105 +202,40 @@ __global__ void __launch_bounds__(64 * WM * WN, 1)
         const bf16x8 a_l = *reinterpret_cast<const bf16x8*>(alo + sw16_off(ra, fs));
 #pragma unroll
         for (int y = 0; y < TN; ++y) {
-          if constexpr (TRM) {  // C^T tile: entity rows x query columns
-            acc[x][y] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b_h[y], a_l, acc[x][y], 0, 0, 0);
-            acc[x][y] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b_l[y], a_h, acc[x][y], 0, 0, 0);
-            acc[x][y] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b_h[y], a_h, acc[x][y], 0, 0, 0);
-          } else {
-            acc[x][y] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a_l, b_h[y], acc[x][y], 0, 0, 0);
-            acc[x][y] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a_h, b_l[y], acc[x][y], 0, 0, 0);
-            acc[x][y] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a_h, b_h[y], acc[x][y], 0, 0, 0);
-          }
+          acc[x][y] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a_l, b_h[y], acc[x][y], 0, 0, 0);
+          acc[x][y] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a_h, b_l[y], acc[x][y], 0, 0, 0);
+          acc[x][y] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a_h, b_h[y], acc[x][y], 0, 0, 0);
         }
       }
     };
-
-    // WN == 1 (a wave spans the tile's columns): A fragments of the wave's TM bands are read
-    // once per stage and the B fragments stream through, y-outer
-    bf16x8 a_hf[TM], a_lf[TM];
-    auto compute_a = [&](const unsigned char* cur) {
-#pragma unroll
-      for (int x = 0; x < TM; ++x) {
-        const int ra = wr * (BM / WM) + x * 16 + fr;
-        a_hf[x] = *reinterpret_cast<const bf16x8*>(cur + sw16_off(ra, fs));
-        a_lf[x] = *reinterpret_cast<const bf16x8*>(cur + C::PLANE_A + sw16_off(ra, fs));
-      }
-    };
-    auto compute_y = [&](const unsigned char* cur, int y0, int y1) {
-      const unsigned char* bhi = cur + 2 * C::PLANE_A;
-      const unsigned char* blo = bhi + C::PLANE_B;
-#pragma unroll
-      for (int y = y0; y < y1; ++y) {
-        const int rb_ = y * 16 + fr;
-        const bf16x8 bh = *reinterpret_cast<const bf16x8*>(bhi + sw16_off(rb_, fs));
-        const bf16x8 bl = *reinterpret_cast<const bf16x8*>(blo + sw16_off(rb_, fs));
-#pragma unroll
-        for (int x = 0; x < TM; ++x) {
-          acc[x][y] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a_lf[x], bh, acc[x][y], 0, 0, 0);
-          acc[x][y] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a_hf[x], bl, acc[x][y], 0, 0, 0);
-          acc[x][y] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a_hf[x], bh, acc[x][y], 0, 0, 0);
-        }
-      }
-    };
-    constexpr int YS = TN / 4 > 0 ? TN / 4 : 1;  // y-outer: columns before the staging block
 
     glds_a(0, 0);
     load_b(0);
     KGE_WAIT_VM(0);
     store_b(smem, 0);
-    load_b(nst > 1 ? BK : 0);
+    if (nst > 1) load_b(BK);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
     // One barrier per stage.  Stage st + 1 is staged into the other buffer between the first
     // XS bands of stage st's MFMAs and the rest (measured: 8 % over staging ahead of them).
+    // The stage body is branch-free: the last stage re-stages its own K chunk into the idle
+    // buffer, so every path keeps the same in-flight counts and the B registers stay put --
+    // with a conditional wait, hipcc copied the registers of loads still in flight at the
+    // merge and reused them (a rare memory fault under multi-tile schedules).
     for (int st = 0; st < nst; ++st) {
       const int nb = (st + 1) & 1;
       const unsigned char* cur = smem + (st & 1) * C::STAGE;
-      const bool more = !(ABL & 2) && st + 1 < nst;
-      if (more) glds_a(nb, (st + 1) * BK);
-      if constexpr ((ABL & 256) != 0 && WN > 1) {
-        static_assert(TM - XS > C::B_PER_T, "one slot per band after the first XS");
-        compute_b(cur);
-        compute_x(cur, 0, XS);
-        const bool tail_next = (st + 2) * BK > d;
-        if (more) {
-          KGE_WAIT_VM(2 * A_G);  // B(st + 1) has landed
-          if (tail_next) store_b(smem + nb * C::STAGE, (st + 1) * BK);
-        }
-#pragma unroll
-        for (int x = XS; x < TM; ++x) {
-          compute_x(cur, x, x + 1);
-          if (x - XS < C::B_PER_T && more && !tail_next) store_b_slot(smem + nb * C::STAGE, x - XS);
-          if (x - XS == C::B_PER_T - 1) load_b(min(st + 2, nst - 1) * BK);
-        }
-        KGE_WAIT_VM(C::B_PER_T);  // A(st + 1) has landed
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier();
-        asm volatile("" ::: "memory");
-        continue;
-      }
-      if constexpr (WN == 1) {
-        compute_a(cur);
-        compute_y(cur, 0, YS);
-      } else {
-        compute_b(cur);
-        if constexpr (PRIO) __builtin_amdgcn_s_setprio(1);
-        compute_x(cur, 0, XS);
-        if constexpr (PRIO) __builtin_amdgcn_s_setprio(0);
-      }
-      if (more) {
+      const int k1 = min(st + 1, nst - 1) * BK;
+      if constexpr (!(ABL & 2)) glds_a(nb, k1);
+      compute_b(cur);
+      compute_x(cur, 0, XS);
+      if constexpr (!(ABL & 2)) {
         KGE_WAIT_VM(2 * A_G);  // B(st + 1) has landed
-        store_b(smem + nb * C::STAGE, (st + 1) * BK);
+        store_b(smem + nb * C::STAGE, k1);
+        load_b(min(st + 2, nst - 1) * BK);
       }
-      if (!(ABL & 2)) load_b(min(st + 2, nst - 1) * BK);
-      if constexpr (WN == 1)
-        compute_y(cur, YS, TN);
-      else {
-        if constexpr (PRIO) __builtin_amdgcn_s_setprio(1);
-        compute_x(cur, XS, TM);
-        if constexpr (PRIO) __builtin_amdgcn_s_setprio(0);
-      }
+      compute_x(cur, XS, TM);
       KGE_WAIT_VM(C::B_PER_T);  // A(st + 1) has landed
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
@@ -355,51 +244,16 @@ __global__ void __launch_bounds__(64 * WM * WN, 1)
     KGE_WAIT_VM(0);
 #undef KGE_WAIT_VM
 
-    if constexpr (TR) {
-      // C^T of 16x16: lane holds query (lane & 15) and 4 consecutive entities 4 (lane >> 4) + r,
-      // i.e. a float4 of one score row: stored straight from the accumulators (16 rows x 64 B
-      // per wave-instruction, the four y tiles of a band complete 256-B row segments)
-#pragma unroll
-      for (int x = 0; x < TM; ++x) {
-        const int i = m0 + wr * (BM / WM) + x * 16 + fr;
-#pragma unroll
-        for (int y = 0; y < TN; ++y) {
-          const int j = n0 + wc * WCOLS + y * 16 + 4 * fs;
-          float* dst = s + (int64_t)i * lds + j;
-          const f32x4 v = acc[x][y];
-          if (i >= n) continue;
-          if (ABL & 1) {
-            if (v.x == 1234.5f) dst[0] = v.y;
-          } else if (j + 3 < m) {
-            if constexpr ((ABL & 32) != 0)
-              __builtin_nontemporal_store(f32x4u{v.x, v.y, v.z, v.w}, reinterpret_cast<f32x4u*>(dst));
-            else
-              *reinterpret_cast<f32x4u*>(dst) = f32x4u{v.x, v.y, v.z, v.w};
-          } else {
-            if (j < m) dst[0] = v.x;
-            if (j + 1 < m) dst[1] = v.y;
-            if (j + 2 < m) dst[2] = v.z;
-          }
-        }
-      }
-      __syncthreads();
-      continue;
-    }
     // epilogue: C/D of 16x16 -- lane holds column (lane & 15), rows 4 (lane >> 4) + r
     __syncthreads();  // stage buffers free: per-wave scratch of 16 rows x WCOLS (+4) floats
     float* scr = reinterpret_cast<float*>(smem) + wave * 16 * SCR_LD;
     constexpr int LPR = WCOLS / 4;  // lanes per scratch row (float4 each)
 #pragma unroll
     for (int x = 0; x < TM; ++x) {
-      if constexpr (TRL) {  // lane: query fr, entities y 16 + 4 fs .. +3 -- one float4 per y
 #pragma unroll
-        for (int y = 0; y < TN; ++y) *reinterpret_cast<f32x4*>(scr + fr * SCR_LD + y * 16 + 4 * fs) = acc[x][y];
-      } else {
+      for (int y = 0; y < TN; ++y)
 #pragma unroll
-        for (int y = 0; y < TN; ++y)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) scr[(4 * fs + r) * SCR_LD + y * 16 + fr] = acc[x][y][r];
-      }
+        for (int r = 0; r < 4; ++r) scr[(4 * fs + r) * SCR_LD + y * 16 + fr] = acc[x][y][r];
       const int i0 = m0 + wr * (BM / WM) + x * 16;
 #pragma unroll
       for (int pass = 0; pass < (16 * LPR + 63) / 64; ++pass) {
@@ -414,19 +268,8 @@ __global__ void __launch_bounds__(64 * WM * WN, 1)
         if (ABL & 1) {
           if (v.x == 1234.5f) dst[0] = v.y;  // keep the values live, store (almost) nothing
         } else if (j + 3 < m) {
-          if constexpr ((ABL & 2048) != 0) {
-            if (kge_dbg_bad(4, dst - s, (int64_t)(n - 1) * lds + m - 3, tile, -1)) continue;
-          }
-          if constexpr ((ABL & 512) != 0)
-            asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(dst), "v"(f32x4{v.x, v.y, v.z, v.w}) : "memory");
-          else if constexpr ((ABL & 1024) != 0)
-            asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1" ::"v"(dst), "v"(f32x4{v.x, v.y, v.z, v.w}) : "memory");
-          else
-            *reinterpret_cast<f32x4u*>(dst) = f32x4u{v.x, v.y, v.z, v.w};
+          *reinterpret_cast<f32x4u*>(dst) = f32x4u{v.x, v.y, v.z, v.w};
         } else {
-          if constexpr ((ABL & 2048) != 0) {
-            if (kge_dbg_bad(5, dst - s, (int64_t)(n - 1) * lds + m, tile, -1)) continue;
-          }
           if (j < m) dst[0] = v.x;
           if (j + 1 < m) dst[1] = v.y;
           if (j + 2 < m) dst[2] = v.z;
@@ -444,8 +287,7 @@ __global__ void __launch_bounds__(64 * WM * WN, 1)
 
 template <int BM, int BN, int WM, int WN, int ABL = 0>
 int launch_persist16(const __bf16* qhi, const __bf16* qlo, int64_t ldq, const float* t, int64_t ldt,
-                     const int64_t* tidx, int64_t n, int64_t m, int d, float* s, int64_t lds, hipStream_t st,
-                     int tiles_per_wg = 0) {
+                     const int64_t* tidx, int64_t n, int64_t m, int d, float* s, int64_t lds, hipStream_t st) {
   using C = PCfg<BM, BN, WM, WN>;
   const int nrt = (int)((n + BM - 1) / BM);
   const int64_t ntiles = (int64_t)nrt * ((m + BN - 1) / BN);
@@ -461,7 +303,6 @@ int launch_persist16(const __bf16* qhi, const __bf16* qlo, int64_t ldq, const fl
   int grid = kge_num_cus();
   grid = (int)std::min<int64_t>(grid, (ntiles + 7) / 8 * 8);
   grid = std::max(8, grid / 8 * 8);
-  if (tiles_per_wg > 0) grid = (int)std::max<int64_t>(8, ((ntiles + tiles_per_wg - 1) / tiles_per_wg + 7) / 8 * 8);
   score_dot_persist16_kernel<BM, BN, WM, WN, ABL><<<dim3(grid), dim3(C::NT), shmem, st>>>(
       qhi, qlo, ldq, t, ldt, tidx, (int)n, (int)m, d, s, lds, nrt, (int)ntiles);
   KGE_CHECK_LAUNCH();
@@ -505,10 +346,8 @@ extern "C" int kge_score_dot_split(const void* qhi, const void* qlo, int64_t ldq
   hipStream_t st = as_stream(stream);
   const __bf16* h = (const __bf16*)qhi;
   const __bf16* l = (const __bf16*)qlo;
-  // ABL 128: paired bf16 split with the K-tail mask only in the tail stage (-2.6 % vs the
-  // per-element split, interleaved A/B on MI355X)
-  if (n > 128) return launch_persist16<256, 256, 2, 4, 128>(h, l, ldq, t, ldt, tidx, n, m, d, s, lds, st);
-  return launch_persist16<128, 256, 2, 4, 128>(h, l, ldq, t, ldt, tidx, n, m, d, s, lds, st);
+  if (n > 128) return launch_persist16<256, 256, 2, 4>(h, l, ldq, t, ldt, tidx, n, m, d, s, lds, st);
+  return launch_persist16<128, 256, 2, 4>(h, l, ldq, t, ldt, tidx, n, m, d, s, lds, st);
 }
 
 extern "C" int kge_dev_score_dot_persist(int variant, const void* qhi, const void* qlo, int64_t ldq,
@@ -522,54 +361,10 @@ extern "C" int kge_dev_score_dot_persist(int variant, const void* qhi, const voi
   switch (variant) {
     case 0: return launch_persist16<256, 256, 2, 4>(h, l, ldq, t, ldt, tidx, n, m, d, s, lds, st);
     case 1: return launch_persist16<128, 256, 2, 4>(h, l, ldq, t, ldt, tidx, n, m, d, s, lds, st);
-    case 2: return launch_persist16<256, 128, 4, 2>(h, l, ldq, t, ldt, tidx, n, m, d, s, lds, st);
-    case 3: return launch_persist16<256, 128, 2, 4>(h, l, ldq, t, ldt, tidx, n, m, d, s, lds, st);
     case 11: return launch_persist16<256, 256, 2, 4, 1>(h, l, ldq, t, ldt, tidx, n, m, d, s, lds, st);
     case 12: return launch_persist16<256, 256, 2, 4, 2>(h, l, ldq, t, ldt, tidx, n, m, d, s, lds, st);
     case 13: return launch_persist16<256, 256, 2, 4, 3>(h, l, ldq, t, ldt, tidx, n, m, d, s, lds, st);
     case 14: return launch_persist16<256, 256, 2, 4, 4>(h, l, ldq, t, ldt, tidx, n, m, d, s, lds, st);
-    case 17: return launch_persist16<256, 256, 2, 4, 7>(h, l, ldq, t, ldt, tidx, n, m, d, s, lds, st);
-    case 30: return launch_persist16<256, 256, 2, 4, 8>(h, l, ldq, t, ldt, tidx, n, m, d, s, lds, st);
-    case 31: return launch_persist16<256, 256, 2, 4, 9>(h, l, ldq, t, ldt, tidx, n, m, d, s, lds, st);
-    case 32: return launch_persist16<256, 256, 2, 4, 24>(h, l, ldq, t, ldt, tidx, n, m, d, s, lds, st);
-    case 33: return launch_persist16<256, 256, 2, 4, 16>(h, l, ldq, t, ldt, tidx, n, m, d, s, lds, st);
-    case 34: return launch_persist16<256, 256, 2, 4, 12>(h, l, ldq, t, ldt, tidx, n, m, d, s, lds, st);
-    case 35: return launch_persist16<256, 128, 2, 4, 8>(h, l, ldq, t, ldt, tidx, n, m, d, s, lds, st, 2);
-    case 36: return launch_persist16<256, 128, 2, 4, 8>(h, l, ldq, t, ldt, tidx, n, m, d, s, lds, st);
-    case 37: return launch_persist16<256, 128, 4, 2, 8>(h, l, ldq, t, ldt, tidx, n, m, d, s, lds, st, 2);
-    case 38: return launch_persist16<256, 256, 2, 4, 40>(h, l, ldq, t, ldt, tidx, n, m, d, s, lds, st);
-    case 40: return launch_persist16<256, 256, 2, 4, 64>(h, l, ldq, t, ldt, tidx, n, m, d, s, lds, st);
-    case 41: return launch_persist16<256, 256, 2, 4, 65>(h, l, ldq, t, ldt, tidx, n, m, d, s, lds, st);
-    case 42: return launch_persist16<256, 256, 2, 4, 68>(h, l, ldq, t, ldt, tidx, n, m, d, s, lds, st);
-    case 50: return launch_persist16<256, 256, 2, 4, 128>(h, l, ldq, t, ldt, tidx, n, m, d, s, lds, st);
-    case 51: return launch_persist16<256, 256, 2, 4, 132>(h, l, ldq, t, ldt, tidx, n, m, d, s, lds, st);
-    case 52: return launch_persist16<256, 256, 2, 4, 129>(h, l, ldq, t, ldt, tidx, n, m, d, s, lds, st);
-    case 53: return launch_persist16<256, 256, 2, 4, 384>(h, l, ldq, t, ldt, tidx, n, m, d, s, lds, st);
-    case 54: return launch_persist16<256, 256, 2, 4, 388>(h, l, ldq, t, ldt, tidx, n, m, d, s, lds, st);
-    case 55: return launch_persist16<256, 256, 2, 4, 640>(h, l, ldq, t, ldt, tidx, n, m, d, s, lds, st);
-    case 56: return launch_persist16<256, 256, 2, 4, 1152>(h, l, ldq, t, ldt, tidx, n, m, d, s, lds, st);
-    case 60: return launch_persist16<512, 128, 4, 2, 128>(h, l, ldq, t, ldt, tidx, n, m, d, s, lds, st);
-    case 61: return launch_persist16<512, 128, 4, 2, 129>(h, l, ldq, t, ldt, tidx, n, m, d, s, lds, st);
-    case 62: return launch_persist16<512, 128, 4, 2, 132>(h, l, ldq, t, ldt, tidx, n, m, d, s, lds, st);
-    case 63: return launch_persist16<512, 128, 4, 2, 384>(h, l, ldq, t, ldt, tidx, n, m, d, s, lds, st);
-    case 70: return launch_persist16<256, 256, 2, 4, 2176>(h, l, ldq, t, ldt, tidx, n, m, d, s, lds, st);
-    case 71: return launch_persist16<512, 128, 4, 2, 2176>(h, l, ldq, t, ldt, tidx, n, m, d, s, lds, st);
-    case 72: return launch_persist16<256, 256, 2, 4, 2048>(h, l, ldq, t, ldt, tidx, n, m, d, s, lds, st);
-    case 90: return launch_persist16<256, 256, 2, 4, 128 + 16384>(h, l, ldq, t, ldt, tidx, n, m, d, s, lds, st);
-    case 20: return launch_persist16<256, 240, 8, 1>(h, l, ldq, t, ldt, tidx, n, m, d, s, lds, st);
-    case 21: return launch_persist16<256, 240, 8, 1, 1>(h, l, ldq, t, ldt, tidx, n, m, d, s, lds, st);
-    case 22: return launch_persist16<256, 256, 8, 1>(h, l, ldq, t, ldt, tidx, n, m, d, s, lds, st);
-    case 24: return launch_persist16<256, 240, 8, 1, 4>(h, l, ldq, t, ldt, tidx, n, m, d, s, lds, st);
     default: return KGE_ERR_ARG;
   }
-}
-
-extern "C" int kge_dev_dbg_read(unsigned long long* host8, int reset) {
-  hipError_t e = hipMemcpyFromSymbol(host8, HIP_SYMBOL(kge_dbg_rec), sizeof(unsigned long long) * 8);
-  if (e != hipSuccess) return (int)e;
-  if (reset) {
-    unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    e = hipMemcpyToSymbol(HIP_SYMBOL(kge_dbg_rec), z, sizeof(z));
-  }
-  return (int)e;
 }
