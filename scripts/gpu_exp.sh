@@ -9,5 +9,5 @@ timeout -k 10 200 python scripts/dist_ab.py 512 > gpurun_out/exp/dist.txt 2>&1 |
 grep -v amdgpu.ids gpurun_out/exp/dist.txt
 timeout -k 10 200 python scripts/tune_dot.py 1024 "$1" > gpurun_out/exp/tune.txt 2>&1 || { echo "tune failed"; tail gpurun_out/exp/tune.txt; exit 1; }
 grep -v amdgpu.ids gpurun_out/exp/tune.txt
-timeout -k 10 200 python scripts/stress_c5.py 574311 200 > gpurun_out/exp/stress.txt 2>&1 || { echo "stress failed"; tail gpurun_out/exp/stress.txt; exit 1; }
+timeout -k 10 300 python scripts/stress_c5.py 574311 400 > gpurun_out/exp/stress.txt 2>&1 || { echo "stress failed"; tail gpurun_out/exp/stress.txt; exit 1; }
 grep -v amdgpu.ids gpurun_out/exp/stress.txt
