@@ -238,6 +238,66 @@ def test_score_dot_split_shapes(L, n, m, d):
     assert torch.equal(s.double(), qd.double() @ td[tidx].double().T)
 
 
+def test_score_dot_split_multitile(L):
+    """Persistent schedule with many tiles per workgroup (m = 200,003: 782 column tiles x 4
+    row tiles over <= 256 workgroups), launched repeatedly: the schedule under which an
+    in-flight register load once had its registers reused (a rare memory fault).  Rows are
+    checked against float64 after the last launch; a dyadic copy must be bit-exact."""
+    g = torch.Generator().manual_seed(11)
+    n, m, d = 1024, 200003, 512
+    t = (torch.randint(-16, 17, (m, d), generator=g) / 8).float().cuda()
+    q = (torch.randint(-16, 17, (n, d), generator=g) / 8).float().cuda()
+    hi, lo = L.split_rows(q)
+    s = torch.empty(n, m, device="cuda")
+    for _ in range(20):
+        L.score_dot_split(hi, lo, t, None, d, out=s)
+    torch.cuda.synchronize()
+    rows = torch.arange(0, n, 61, device="cuda")
+    assert torch.equal(s[rows].double(), q[rows].double() @ t.double().T)
+    tr = (torch.randn(m, d, generator=g) * 0.1).cuda()
+    L.score_dot_split(hi, lo, tr, None, d, out=s)
+    ref = (q[rows].double() @ tr.double().T).cpu().numpy()
+    assert rel_err(s[rows].cpu().numpy(), ref) < 2e-5
+
+
+@pytest.mark.parametrize("kind", [0, 1, 2, 3])
+@pytest.mark.parametrize("d", [64, 512, 30])
+def test_score_dist_packed_vs_scalar(L, kind, d):
+    """The packed-VALU distance kernel (score_dist2.hip) against the scalar one
+    (score_dist.hip, selected with kge_dev_dist_impl) and float64; d = 30 (RotatE 15
+    complex components) takes the scalar kernel in both cases (layout fallback)."""
+    import ctypes
+    lib = L.lib()
+    lib.kge_dev_dist_impl.argtypes = [ctypes.c_int]
+    g = torch.Generator().manual_seed(kind * 100 + d)
+    n, m = 100, 501
+    q = (torch.randn(n, d, generator=g) * 0.1).cuda()
+    t = (torch.randn(m + 7, d, generator=g) * 0.1).cuda()
+    sub = torch.randint(0, m + 7, (m,), generator=g).cuda()
+    outs = {}
+    try:
+        for impl in (1, 2):
+            lib.kge_dev_dist_impl(impl)
+            outs[impl] = (L.score_dist(kind, -1.0, q, t, None), L.score_dist(kind, -1.0, q, t, sub))
+    finally:
+        lib.kge_dev_dist_impl(2)
+    qq, tt = q.double().cpu(), t.double().cpu()
+    if kind < 2:
+        diff = qq[:, None, :] - tt[None, :, :]
+        ref = -(diff.abs().sum(-1) if kind == 0 else diff.pow(2).sum(-1).sqrt())
+    else:
+        h = d // 2
+        dr = qq[:, None, :h] - tt[None, :, :h]
+        di = qq[:, None, h:] - tt[None, :, h:]
+        mod = (dr * dr + di * di).sqrt()
+        ref = -(mod.sum(-1) if kind == 2 else mod.pow(2).sum(-1).sqrt())
+    for impl in (1, 2):
+        a, b = outs[impl]
+        assert rel_err(a.cpu().numpy(), ref.numpy()) < 1e-5, (impl, "all")
+        assert rel_err(b.cpu().numpy(), ref[:, sub.cpu()].numpy()) < 1e-5, (impl, "subset")
+    assert rel_err(outs[2][0].cpu().numpy(), outs[1][0].cpu().double().numpy()) < 1e-5
+
+
 def test_contract_dispatch_and_errors(L):
     q = torch.randn(8, 6).cuda()
     t = torch.randn(20, 6).cuda()
