@@ -77,7 +77,7 @@ __global__ void __launch_bounds__(64 * WM * WN, 1)
   constexpr int A_G = BM / 16 / NW;                      // 1-KB A chunks per plane per wave
   constexpr int XS = TM / 4 > 0 ? TM / 4 : 1;            // bands computed before the staging block
   static_assert((BM / 16) % NW == 0, "A chunks");
-  static_assert(C::B_PER_T == 4 || C::B_PER_T == 2, "KGE_WAIT_VM names the B registers");
+  static_assert(C::B_PER_T == 8 || C::B_PER_T == 4 || C::B_PER_T == 2, "KGE_WAIT_VM names the B registers");
   static_assert(WN > 1, "x-outer band loop");
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int tid = threadIdx.x, lane = tid & 63;
@@ -129,7 +129,13 @@ __global__ void __launch_bounds__(64 * WM * WN, 1)
     // issues 2 A_G DMAs (stage st + 1), then B_PER_T register loads (stage st + 2).
 #define KGE_WAIT_VM(N)                                                                                   \
   do {                                                                                                   \
-    if constexpr (C::B_PER_T == 4)                                                                       \
+    if constexpr (C::B_PER_T == 8)                                                                       \
+      asm volatile("s_waitcnt vmcnt(%8)"                                                                 \
+                   : "+v"(rv[0]), "+v"(rv[1]), "+v"(rv[2]), "+v"(rv[3]), "+v"(rv[4]), "+v"(rv[5]),       \
+                     "+v"(rv[6]), "+v"(rv[7])                                                            \
+                   : "i"(N)                                                                              \
+                   : "memory");                                                                          \
+    else if constexpr (C::B_PER_T == 4)                                                                  \
       asm volatile("s_waitcnt vmcnt(%4)" : "+v"(rv[0]), "+v"(rv[1]), "+v"(rv[2]), "+v"(rv[3]) : "i"(N) : "memory"); \
     else                                                                                                 \
       asm volatile("s_waitcnt vmcnt(%2)" : "+v"(rv[0]), "+v"(rv[C::B_PER_T - 1]) : "i"(N) : "memory");  \
@@ -365,6 +371,9 @@ extern "C" int kge_dev_score_dot_persist(int variant, const void* qhi, const voi
     case 12: return launch_persist16<256, 256, 2, 4, 2>(h, l, ldq, t, ldt, tidx, n, m, d, s, lds, st);
     case 13: return launch_persist16<256, 256, 2, 4, 3>(h, l, ldq, t, ldt, tidx, n, m, d, s, lds, st);
     case 14: return launch_persist16<256, 256, 2, 4, 4>(h, l, ldq, t, ldt, tidx, n, m, d, s, lds, st);
+    // one wave per SIMD, 128 x 128 wave tiles (accumulators in AGPRs)
+    case 20: return launch_persist16<256, 256, 2, 2>(h, l, ldq, t, ldt, tidx, n, m, d, s, lds, st);
+    case 24: return launch_persist16<256, 256, 2, 2, 4>(h, l, ldq, t, ldt, tidx, n, m, d, s, lds, st);
     default: return KGE_ERR_ARG;
   }
 }

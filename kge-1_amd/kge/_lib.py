@@ -142,7 +142,9 @@ def idx64(t: Optional[torch.Tensor]) -> Optional[torch.Tensor]:
 
 
 def check_index(idx: Optional[torch.Tensor], num_rows: int, what: str):
-    if CHECK_INDEX and idx is not None and idx.numel() > 0:
+    # (skipped while a HIP graph is being recorded: the check syncs; the recorded step's
+    # indexes were checked by the eager warm-up steps of the same shapes)
+    if CHECK_INDEX and idx is not None and idx.numel() > 0 and not torch.cuda.is_current_stream_capturing():
         lo, hi = int(idx.min()), int(idx.max())
         if lo < 0 or hi >= num_rows:
             raise IndexError(f"{what}: index out of range [{lo}, {hi}] for {num_rows} rows")

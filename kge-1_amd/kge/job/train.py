@@ -113,17 +113,10 @@ class TrainingJob(Job):
         for batch_index, example_ids in enumerate(self._batches()):
             for f in self.pre_batch_hooks:
                 f(self)
-            self.optimizer.zero_grad()
             batch = self._collate(example_ids)
-            res = self.process_batch(batch_index, batch)
-            penalty = 0.0
-            for _, pv in self.model.penalty(epoch=self.epoch, batch_index=batch_index, batch=batch):
-                pv.backward()
-                penalty += pv.item()
+            res, penalty, t_opt = self.train_step(batch_index, batch)
             sum_penalty += penalty
-            t0 = time.time()
-            self.optimizer.step()
-            opt_t += time.time() - t0
+            opt_t += t_opt
             # The batch loss is read one batch late (an async copy + event): the host queues
             # batch b + 1 while the device still runs batch b, instead of draining the queue
             # every batch as loss.item() would (the reference's per-batch sync, Q11).  A NaN
@@ -160,6 +153,123 @@ class TrainingJob(Job):
     def process_batch(self, batch_index, batch) -> "TrainingJob._ProcessBatchResult":
         return self._process_batch(batch_index, batch)
 
+    def train_step(self, batch_index, batch):
+        """One optimizer step on one batch -- zero_grad, forward/backward (process_batch),
+        penalty backward, optimizer.step: the body of the reference's batch loop
+        (train.py:309-429).  Returns (result, penalty, optimizer seconds).  Replayed from a
+        recorded HIP graph when the job has one for this batch (engine.graph_step)."""
+        graph = getattr(self, "_graph_step", None)
+        if graph is not None:
+            res = graph.run(batch_index, batch)
+            if res is not None:
+                return res, 0.0, 0.0
+        self.optimizer.zero_grad()
+        res = self.process_batch(batch_index, batch)
+        penalty = 0.0
+        for _, pv in self.model.penalty(epoch=self.epoch, batch_index=batch_index, batch=batch):
+            pv.backward()
+            penalty += pv.item()
+            if graph is not None:
+                graph.disable()  # a penalty syncs on its value: not recordable
+        t0 = time.time()
+        self.optimizer.step()
+        return res, penalty, time.time() - t0
+
+
+class _GraphStep:
+    """A 1vsAll training step recorded once as a HIP graph and replayed per batch
+    (engine.graph_step).
+
+    The step's device work is fixed for a full batch: the index columns, one fused
+    sp+po scoring / softmax-CE pass, its backward GEMMs and prep backward, the fused
+    Adagrad kernels -- ~30 launches plus autograd bookkeeping on the host, which at C2 costs
+    as long as the device work itself.  Two full batches run eagerly first (kernel
+    attributes, optimizer state, allocator warm-up); the third is recorded (recording runs
+    nothing) and replayed, and every later full batch is copied into the recorded index
+    buffer and replayed.  The optimizer's host-side step counters are advanced per replay.
+    A partial last batch, or any step the recording cannot take, runs eagerly."""
+
+    WARMUP = 2
+
+    def __init__(self, job: "TrainingJob"):
+        self.job = job
+        self.graph = None
+        self.static = None  # recorded [B, 3] int64 device index buffer
+        self.pinned = []  # two pinned host staging buffers (+ their copy events) for the batch
+        self.turn = 0
+        self.loss = None  # recorded 0-dim loss
+        self.stepped = []
+        self.warm = 0
+        self.disabled = False
+        self.error = None  # why recording was abandoned, if it was
+
+    def disable(self):
+        self.disabled = True
+        self.graph = None
+
+    def run(self, batch_index, batch):
+        job = self.job
+        triples = batch["triples"]
+        if self.disabled or triples.dim() != 2 or triples.shape[0] != job.batch_size:
+            return None
+        t = -time.time()
+        if self.graph is None:
+            if self.warm < self.WARMUP:
+                self.warm += 1
+                return None  # the caller runs this batch eagerly
+            if not self._record(batch_index, triples):
+                return None
+            # recording counted this step in the optimizer state already
+        else:
+            # a copy from pageable memory would block the host until the device drains;
+            # stage through pinned memory (two buffers: the copy of batch b - 1 may still
+            # be in flight)
+            if not self.pinned:
+                self.pinned = [[torch.empty(self.static.shape, dtype=torch.int64, pin_memory=True), None]
+                               for _ in range(2)]
+            slot = self.pinned[self.turn]
+            self.turn ^= 1
+            if slot[1] is not None:
+                slot[1].synchronize()
+            slot[0].copy_(triples)
+            self.static.copy_(slot[0], non_blocking=True)
+            slot[1] = torch.cuda.Event()
+            slot[1].record()
+            job.optimizer.advance_steps(self.stepped)
+        self.graph.replay()
+        t += time.time()
+        return TrainingJob._ProcessBatchResult(self.loss, triples.shape[0], 0.0, t, 0.0)
+
+    def _record(self, batch_index, triples) -> bool:
+        job = self.job
+        opt = job.optimizer
+        steps = {p: st["step"].clone() for p, st in opt.state.items() if "step" in st}
+        self.static = triples.to(job.device).long()
+        opt.zero_grad(set_to_none=True)
+        g = torch.cuda.CUDAGraph()
+        try:
+            with torch.cuda.graph(g):
+                res = job.process_batch(batch_index, {"triples": self.static})
+                opt.step()
+        except Exception as e:  # not recordable: this and every later batch run eagerly
+            for p, s in steps.items():
+                opt.state[p]["step"] = s
+            opt.zero_grad(set_to_none=True)
+            import traceback
+
+            self.error = f"{type(e).__name__}: {e}\n{traceback.format_exc()}"
+            job.config.log(f"engine.graph_step disabled: {self.error}")
+            self.disable()
+            return False
+        if not torch.is_tensor(res.loss):
+            self.error = "the recorded step returned a host loss"
+            self.disable()
+            return False
+        self.graph = g
+        self.loss = res.loss
+        self.stepped = [p for grp in opt.param_groups for p in grp["params"] if p.grad is not None]
+        return True
+
 
 class TrainingJob1vsAll(TrainingJob):
     """Each (s, p, o) scores (s, p, ?) and (?, p, o) against all entities; CE loss."""
@@ -167,10 +277,19 @@ class TrainingJob1vsAll(TrainingJob):
     def __init__(self, config, dataset, parent_job=None, model=None):
         super().__init__(config, dataset, parent_job, model=model)
         self.type_str = "1vsAll"
+        self._graph_step = None
 
     def _prepare(self):
         super()._prepare()
         self.num_examples = self.dataset.split(self.train_split).size(0)
+        opt = self.optimizer
+        if (self.config.get("engine.graph_step") and self.config.get("engine.fused_loss")
+                and isinstance(self.loss, KLDivWithSoftmaxKgeLoss)
+                and torch.device(self.device).type == "cuda"
+                and hasattr(opt, "graph_safe") and opt.graph_safe()
+                and self.kge_lr_scheduler._lr_scheduler is None
+                and self.model._lookup_tables() is not None):
+            self._graph_step = _GraphStep(self)
 
     def _collate(self, example_ids):
         return {"triples": self.dataset.split(self.train_split)[example_ids, :].long()}

@@ -50,6 +50,26 @@ class FusedAdagrad(torch.optim.Adagrad):
                 group["params"] = saved
         return loss
 
+    def graph_safe(self) -> bool:
+        """True when every step issues the same device work with the same arguments, so it
+        can be recorded once and replayed (TrainingJob graph_step): all parameters are
+        stepped by the kernel and the effective learning rate does not depend on the step
+        count (lr_decay 0).  The host-side step counters are advanced by advance_steps."""
+        for group in self.param_groups:
+            if group["differentiable"] or group["lr_decay"] != 0:
+                return False
+            for p in group["params"]:
+                if not (p.is_cuda and p.dtype == torch.float32 and p.is_contiguous()
+                        and not self.state[p]["step"].is_cuda):
+                    return False
+        return True
+
+    def advance_steps(self, params):
+        """The host-side part of step() for a replayed step: count it in the state of the
+        parameters the recorded step updated (those that had a gradient)."""
+        for p in params:
+            self.state[p]["step"] += 1
+
 
 class KgeOptimizer:
     @staticmethod

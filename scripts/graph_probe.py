@@ -1,4 +1,5 @@
-"""Dev probe: host (issue) time vs device time of the 1vsAll training step (C2 shape)."""
+"""Dev probe: the recorded 1vsAll step (C2 shape) -- replay alone, pinned copy + replay, and
+job.train_step, each 50x without host syncs."""
 import os, sys, time
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT); sys.path.insert(0, os.path.join(ROOT, "kge-1_amd"))
@@ -18,26 +19,23 @@ ds = Dataset.synthetic(c, "fb15k-237", seed=0)
 job = TrainingJob.create(c, ds); job._prepare()
 train = ds.split("train")
 perm = torch.randperm(len(train), generator=torch.Generator().manual_seed(0))
-batches = [{"triples": train[perm[i * B:(i + 1) * B]].long()} for i in range(60)]
+batches = [{"triples": train[perm[i * B:(i + 1) * B]].long()} for i in range(120)]
+for i in range(6):
+    job.train_step(i, batches[i])
+gs = job._graph_step
+torch.cuda.synchronize()
 
-def step(i, sync):
-    r, _, _ = job.train_step(i, batches[i])
-    if sync:
-        float(r.avg_loss)
-
-for sync in (False, True):
-    for i in range(5): step(i, sync)
+def timeit(name, fn, n=50):
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for i in range(5, 55): step(i, sync)
+    for i in range(n):
+        fn(i)
     t1 = time.perf_counter()
     torch.cuda.synchronize()
     t2 = time.perf_counter()
-    print(f"sync={sync}: issue {(t1 - t0) / 50 * 1e3:.3f} ms/step, total {(t2 - t0) / 50 * 1e3:.3f} ms/step")
-# host-side breakdown of one step
-import cProfile, pstats
-torch.cuda.synchronize()
-pr = cProfile.Profile(); pr.enable()
-for i in range(5, 25): step(i, False)
-pr.disable(); torch.cuda.synchronize()
-pstats.Stats(pr).sort_stats("tottime").print_stats(18)
+    print(f"{name}: issue {(t1 - t0) / n * 1e3:.3f} ms, total {(t2 - t0) / n * 1e3:.3f} ms per step", flush=True)
+
+timeit("replay only", lambda i: gs.graph.replay())
+timeit("copy(pinned)+replay", lambda i: (gs.static.copy_(gs.pinned[0][0], non_blocking=True), gs.graph.replay()))
+timeit("train_step", lambda i: job.train_step(10 + i, batches[10 + i]))
+timeit("replay only", lambda i: gs.graph.replay())

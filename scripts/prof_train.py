@@ -30,17 +30,10 @@ job._prepare()
 B = c.get("train.batch_size")
 perm = torch.randperm(job.num_examples, generator=torch.Generator().manual_seed(0))
 for i in range(8):
-    job.optimizer.zero_grad()
-    ex = perm[i * B:(i + 1) * B]
-    batch = job._collate(ex)
-    job._process_batch(i, batch)
-    job.optimizer.step()
+    job.train_step(i, job._collate(perm[i * B:(i + 1) * B]))
 torch.cuda.synchronize()
 t0 = time.perf_counter()
 for i in range(8, 18):
-    job.optimizer.zero_grad()
-    batch = job._collate(perm[i * B:(i + 1) * B])
-    job._process_batch(i, batch)
-    job.optimizer.step()
+    job.train_step(i, job._collate(perm[i * B:(i + 1) * B]))
 torch.cuda.synchronize()
 print(f"{model_name} {train_type} step {(time.perf_counter() - t0) / 10 * 1e3:.3f} ms")
