@@ -1,7 +1,7 @@
 """Dev sweep of the backward GEMM variants at the stacked C2 shape (2048 queries x 14541
 entities x 512): interleaved rounds in one process (kge_dev_bwd3 / the shipped entries)."""
 import ctypes, sys
-sys.path.insert(0, '.'); sys.path.insert(0, 'kge-1_amd')
+import os as _os; _R = _os.path.dirname(_os.path.dirname(_os.path.abspath(__file__))); sys.path.insert(0, _R); sys.path.insert(0, _os.path.join(_R, 'kge-1_amd'))
 import numpy as np, torch
 from kge import _lib as L
 lib = L.lib()
@@ -26,6 +26,12 @@ def run(v):
         assert lib.kge_dev_bwd3(v, g.data_ptr(), mp, q.data_ptr(), d, n, m, d, de.data_ptr(), d, 1, st) == 0
 variants = [int(x) for x in sys.argv[3].split(',')] if len(sys.argv) > 3 else [0, 1, 2, 3]
 res = {v: [] for v in variants}
+ref_q = (g.double() @ ent.double()); ref_t = (g.double().T @ q.double())
+for v in variants:
+    dq.zero_(); de.zero_(); run(v); torch.cuda.synchronize()
+    out, ref = (dq, ref_q) if v in (0, 1) else (de, ref_t)
+    err = ((out.double() - ref).abs().max() / ref.abs().max()).item()
+    print(f"variant {v}: max err / max|ref| {err:.2e}", flush=True)
 for rnd in range(5):
     for v in variants:
         for _ in range(2): run(v)
