@@ -360,12 +360,29 @@ class TrainingJobKvsAll(TrainingJob):
             self.query_indexes.append(idx)
             self.num_examples += len(idx)
             self.query_last_example.append(self.num_examples)
-        # device copies of the label CSRs (one per query type)
-        self._dev = [(torch.from_numpy(ix.keys).to(self.device), torch.from_numpy(ix.offsets).to(self.device),
-                      torch.from_numpy(ix.values).to(self.device)) for ix in self.query_indexes]
 
     def _collate(self, example_ids):
         return {"examples": example_ids}
+
+    def _queries(self, qi, sel):
+        """(query pairs [n, 2], label CSR pointer [n + 1], label columns) of the selected
+        examples of query type qi, on the device.  Built on the host from the index (numpy)
+        and shipped in ONE pinned non-blocking copy: no device sync (a device-side build
+        needs the label count on the host, i.e. a sync that drains the queue every batch)."""
+        ix = self.query_indexes[qi]
+        q = ix.keys[sel].astype(np.int64, copy=False)
+        lo = ix.offsets[sel].astype(np.int64, copy=False)
+        lens = ix.offsets[sel + 1].astype(np.int64, copy=False) - lo
+        l_ptr = np.zeros(len(sel) + 1, dtype=np.int64)
+        np.cumsum(lens, out=l_ptr[1:])
+        pos = np.arange(l_ptr[-1], dtype=np.int64) - np.repeat(l_ptr[:-1], lens) + np.repeat(lo, lens)
+        l_col = ix.values[pos].astype(np.int64, copy=False)
+        n = len(sel)
+        host = torch.from_numpy(np.concatenate((q.reshape(-1), l_ptr, l_col)))
+        if torch.device(self.device).type == "cuda":
+            host = host.pin_memory()
+        dev = host.to(self.device, non_blocking=True)
+        return dev[:2 * n].view(n, 2), dev[2 * n:3 * n + 1], dev[3 * n + 1:]
 
     def _process_batch(self, batch_index, batch) -> TrainingJob._ProcessBatchResult:
         t = -time.time()
@@ -388,19 +405,10 @@ class TrainingJobKvsAll(TrainingJob):
             if len(sel) == 0:
                 continue
             t -= time.time()
-            keys, offs, vals = self._dev[qi]
-            sel_d = torch.from_numpy(sel).to(self.device)
-            q = keys[sel_d]
-            lo, hi = offs[sel_d], offs[sel_d + 1]
-            lens = hi - lo
-            rows = torch.repeat_interleave(torch.arange(len(sel), device=self.device), lens)
-            pos = torch.arange(int(lens.sum().item()), device=self.device) - torch.repeat_interleave(
-                torch.cumsum(lens, 0) - lens, lens) + torch.repeat_interleave(lo, lens)
+            q, l_ptr, l_col = self._queries(qi, sel)
             loss = None
             if self.config.get("engine.fused_loss") and isinstance(self.loss, KLDivWithSoftmaxKgeLoss):
                 # positives as a CSR (no dense label matrix); KL + gradient in the engine
-                l_ptr = torch.cat((lens.new_zeros(1), torch.cumsum(lens, 0)))
-                l_col = vals[pos]
                 t += time.time()
                 fwd -= time.time()
                 fn = self.model.score_sp_kl if qt == "sp_" else self.model.score_po_kl
@@ -409,7 +417,8 @@ class TrainingJobKvsAll(TrainingJob):
                 t -= time.time()
             if loss is None:
                 labels = torch.zeros(len(sel), E, device=self.device)
-                labels[rows, vals[pos]] = 1.0
+                rows = torch.repeat_interleave(torch.arange(len(sel), device=self.device), l_ptr[1:] - l_ptr[:-1])
+                labels[rows, l_col] = 1.0
                 if self.label_smoothing > 0.0:
                     labels = (1.0 - self.label_smoothing) * labels + 1.0 / E
                 t += time.time()
@@ -441,15 +450,7 @@ class TrainingJobKvsAll(TrainingJob):
             start = end
             if len(sel) == 0:
                 return None
-            keys, offs, vals = self._dev[qi]
-            sel_d = torch.from_numpy(sel).to(self.device)
-            q = keys[sel_d]
-            lo, hi = offs[sel_d], offs[sel_d + 1]
-            lens = hi - lo
-            pos = torch.arange(int(lens.sum().item()), device=self.device) - torch.repeat_interleave(
-                torch.cumsum(lens, 0) - lens, lens) + torch.repeat_interleave(lo, lens)
-            l_ptr = torch.cat((lens.new_zeros(1), torch.cumsum(lens, 0)))
-            l_col = vals[pos]
+            q, l_ptr, l_col = self._queries(qi, sel)
             part = self.model.xent_part_sp if qt == "sp_" else self.model.xent_part_po
             parts.append(part(q[:, 0], q[:, 1], l_col, l_ptr))
         t += time.time()

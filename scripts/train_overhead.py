@@ -6,19 +6,20 @@ import torch
 from kge import Config, Dataset
 from kge.job import TrainingJob
 
+model_name = sys.argv[1] if len(sys.argv) > 1 else "complex"
+train_type = sys.argv[2] if len(sys.argv) > 2 else "1vsAll"
 c = Config()
-c.set("model", "complex"); c._import("complex")
+c.set("model", model_name); c._import(model_name)
 c.set("job.device", "cuda")
 c.set("lookup_embedder.dim", 512)
 c.set("lookup_embedder.initialize_args", {"mean": 0.0, "std": 0.1})
-c.set("train.type", "1vsAll"); c.set("train.optimizer", "Adagrad"); c.set("train.optimizer_args", {"lr": 0.2})
-B = 1024
+c.set("train.type", train_type); c.set("train.optimizer", "Adagrad"); c.set("train.optimizer_args", {"lr": 0.2})
+B = 1024 if train_type == "1vsAll" else 512
 c.set("train.batch_size", B); c.set("verbose", False)
-ds = Dataset.synthetic(c, "fb15k-237", seed=0)
+ds = Dataset.synthetic(c, "fb15k-237" if train_type == "1vsAll" else "wn18rr", seed=0)
 job = TrainingJob.create(c, ds); job._prepare()
-train = ds.split("train")
-perm = torch.randperm(len(train), generator=torch.Generator().manual_seed(0))
-batches = [{"triples": train[perm[i * B:(i + 1) * B]].long()} for i in range(60)]
+perm = torch.randperm(job.num_examples, generator=torch.Generator().manual_seed(0))
+batches = [job._collate(perm[i * B:(i + 1) * B]) for i in range(60)]
 
 def step(i, sync):
     r, _, _ = job.train_step(i, batches[i])
