@@ -308,7 +308,7 @@ def extras(args, model, c, E, R, device):
 
     def tstep(i):  # the job's batch step: recorded as a HIP graph after two eager batches
         job.train_step(i, {"triples": train[perm[i * B:(i + 1) * B]].long()})
-    sec = timed_loop(tstep, 20, 4, 1)
+    sec = timed_loop(tstep, 30, 6, 1)
     res["train_step_ms"] = round(sec * 1e3, 3)
     res["train_scored_triples_per_s"] = 2 * B * E / sec
     res["train_triples_per_s"] = B / sec

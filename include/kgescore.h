@@ -260,6 +260,12 @@ int kge_adagrad_step(float* param, const float* grad, float* state_sum, int64_t 
                      float minus_clr, float eps, float weight_decay, int maximize,
                      void* stream);
 
+/* Copy n int64 from host-pinned, device-visible memory (hipHostMalloc) into device memory
+ * with a kernel on `stream`: the per-batch index upload of the replayed 1vsAll training
+ * step (engine.graph_step).  Internal plumbing; no reference counterpart (the reference
+ * moves each batch with triples.to(device), train.py:1035). */
+int kge_stage_i64(const int64_t* src, int64_t* dst, int64_t n, void* stream);
+
 /* ---- entity-ranking counts (eval) --------------------------------------------------
  * For row i of a score chunk S[n, m] covering entities [c0, c0 + m):
  *   v_j = S[i, j], with v_{true_i - c0} := true_score[i] when true_i is in the chunk;

@@ -62,3 +62,23 @@ extern "C" int kge_adagrad_step(float* param, const float* grad, float* state_su
   KGE_CHECK_LAUNCH();
   return 0;
 }
+
+// Index staging for the replayed training step: n int64 from host-pinned (device-visible)
+// memory into a device buffer by a kernel on the compute stream -- no DMA-engine hand-off
+// between the copy and the recorded step that reads it.
+namespace {
+__global__ void __launch_bounds__(256) stage_i64_kernel(const int64_t* __restrict__ src, int64_t* __restrict__ dst,
+                                                        int64_t n) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    dst[i] = src[i];
+}
+}  // namespace
+
+extern "C" int kge_stage_i64(const int64_t* src, int64_t* dst, int64_t n, void* stream) {
+  KGE_REQUIRE(n >= 0 && src && dst);
+  if (n == 0) return 0;
+  const int blocks = (int)std::min<int64_t>((n + 255) / 256, 64);
+  stage_i64_kernel<<<dim3(blocks), dim3(256), 0, as_stream(stream)>>>(src, dst, n);
+  KGE_CHECK_LAUNCH();
+  return 0;
+}

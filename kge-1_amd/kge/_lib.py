@@ -63,6 +63,7 @@ SIGNATURES = {
     "kge_score_cand_bwd_ent": ([_I, _F, _I, _P, _I64, _P, _I64, _P, _I64, _I64, _I, _P, _P, _I64, _P, _I64, _P,
                                 _I64, _P, _I64, _P], _I),
     "kge_bucket_scatter": ([_P, _I64, _P, _P, _P], _I),
+    "kge_stage_i64": ([_P, _P, _I64, _P], _I),
     "kge_softmax_row_stats": ([_P, _I64, _I64, _I64, _I64, _P, _P, _P, _P, _P], _I),
     "kge_softmax_grad": ([_P, _I64, _I64, _I64, _I64, _P, _P, _F, _P, _I64, _P], _I),
 }
@@ -431,6 +432,14 @@ def softmax_kl(s, l_ptr, l_col, smoothing, scale, g=None, loss=None):
     _check(lib().kge_softmax_kl(ptr(s), rows(s), n, m, ptr(l_ptr), ptr(l_col), float(smoothing), float(scale),
                                 ptr(loss), ptr(g), rows(g) if g is not None else 0, stream()), "kge_softmax_kl")
     return loss
+
+
+def stage_i64(src_pinned, dst):
+    """dst[:] = src_pinned (int64, host-pinned) by a kernel on the current stream (kge_stage_i64)."""
+    if not (src_pinned.is_pinned() and dst.is_cuda and src_pinned.dtype == dst.dtype == torch.int64
+            and src_pinned.is_contiguous() and dst.is_contiguous() and src_pinned.numel() == dst.numel()):
+        raise ValueError("stage_i64: needs a contiguous pinned int64 source and a same-size CUDA int64 target")
+    _check(lib().kge_stage_i64(ptr(src_pinned), ptr(dst), dst.numel(), stream()), "kge_stage_i64")
 
 
 def adagrad_step(param, grad, state_sum, minus_clr, eps, weight_decay, maximize):

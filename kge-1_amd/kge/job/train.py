@@ -17,6 +17,7 @@ from typing import Any, Dict, Optional
 import numpy as np
 import torch
 
+from .. import _lib
 from ..model.kge_model import KgeModel
 from ..util.loss import KgeLoss, KLDivWithSoftmaxKgeLoss
 from ..util.optimizer import KgeLRScheduler, KgeOptimizer
@@ -222,8 +223,8 @@ class _GraphStep:
             # recording counted this step in the optimizer state already
         else:
             # a copy from pageable memory would block the host until the device drains;
-            # stage through pinned memory (two buffers: the copy of batch b - 1 may still
-            # be in flight)
+            # stage through pinned memory (two buffers: the read of batch b - 1 may still be
+            # pending) and upload it with a kernel in stream order
             if not self.pinned:
                 self.pinned = [[torch.empty(self.static.shape, dtype=torch.int64, pin_memory=True), None]
                                for _ in range(2)]
@@ -232,7 +233,7 @@ class _GraphStep:
             if slot[1] is not None:
                 slot[1].synchronize()
             slot[0].copy_(triples)
-            self.static.copy_(slot[0], non_blocking=True)
+            _lib.stage_i64(slot[0], self.static)  # a kernel, not a DMA copy, on this stream
             slot[1] = torch.cuda.Event()
             slot[1].record()
             job.optimizer.advance_steps(self.stepped)

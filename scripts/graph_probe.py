@@ -36,6 +36,9 @@ def timeit(name, fn, n=50):
     print(f"{name}: issue {(t1 - t0) / n * 1e3:.3f} ms, total {(t2 - t0) / n * 1e3:.3f} ms per step", flush=True)
 
 timeit("replay only", lambda i: gs.graph.replay())
-timeit("copy(pinned)+replay", lambda i: (gs.static.copy_(gs.pinned[0][0], non_blocking=True), gs.graph.replay()))
+timeit("dma copy(pinned)+replay", lambda i: (gs.static.copy_(gs.pinned[0][0], non_blocking=True), gs.graph.replay()))
+from kge import _lib
+timeit("kernel stage(pinned)+replay", lambda i: (_lib.stage_i64(gs.pinned[0][0], gs.static), gs.graph.replay()))
 timeit("train_step", lambda i: job.train_step(10 + i, batches[10 + i]))
+timeit("train_step", lambda i: job.train_step(60 + i, batches[60 + i]))
 timeit("replay only", lambda i: gs.graph.replay())
