@@ -17,8 +17,9 @@
 // kge_softmax_row_stats gives each shard's (max, sum exp(x - max), target score) for the
 // cross-shard reduction, kge_softmax_grad the shard's slice of G from the global lse.
 //
-// HBM-bound: one workgroup per row reads the row once for the online (max, sum-exp, sum),
-// then again (L2 / MALL-resident: 4m bytes just touched) to write G, which may alias S.
+// HBM-bound: one workgroup per row reads the row once for the online (max, sum-exp, sum)
+// and writes G, which may alias S, from registers (rows up to 16,384 columns); longer rows
+// are read a second time (L2 / MALL-resident: 4m bytes just touched) to write G.
 // exp is v_exp_f32 (__expf): relative error ~|x| * 6e-8 for exp(x), x = score - max <= 0,
 // far inside the 1e-4 contract; libm expf made the kernel VALU-bound.
 #include <math.h>
@@ -132,6 +133,102 @@ __device__ __forceinline__ void row_grad(const float* sr, float* gr, int m, floa
   for (int j = j0 + tid; j < m; j += NT) gr[j] = a * __expf(sr[j] - lse) - b;
 }
 
+
+// Rows of at most NI * NT * 4 * U floats (16,384 for NI = 2: every FB15K-237 / WN18RR-sized
+// row): the row is loaded ONCE into registers (NI * U float4 per thread, all loads in flight
+// together), the statistics come from the registers and G is written from them -- one HBM
+// read and one write per element instead of a second (L2 / MALL) read pass.  Same
+// per-thread element order and arithmetic as row_stats / row_grad.
+template <int NI>
+struct RowRegs {
+  float4 v[NI][U];
+};
+
+template <int NI>
+__device__ __forceinline__ void row_load_regs(const float* sr, int m, RowRegs<NI>& r) {
+  const int tid = threadIdx.x, m4 = m & ~3;
+#pragma unroll
+  for (int i = 0; i < NI; ++i)
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      r.v[i][u] = *reinterpret_cast<const float4*>(sr + min(i * NT * 4 * U + (u * NT + tid) * 4, m4 - 4));
+}
+
+template <int NI>
+__device__ __forceinline__ void row_stats_regs(const float* sr, int m, const RowRegs<NI>& r, float (&red)[3][NT / 64],
+                                               float& mx, float& sm, float& rs) {
+  const int tid = threadIdx.x, m4 = m & ~3;
+  mx = -INFINITY;
+  sm = 0.f;
+  rs = 0.f;
+#pragma unroll
+  for (int i = 0; i < NI; ++i)
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const float4 v = r.v[i][u];
+      if (i * NT * 4 * U + (u * NT + tid) * 4 >= m4) continue;
+      rs += (v.x + v.y) + (v.z + v.w);
+      const float vm = fmaxf(fmaxf(v.x, v.y), fmaxf(v.z, v.w));
+      const float nm = fmaxf(mx, vm);
+      if (nm != -INFINITY) {
+        sm = sm * __expf(mx - nm) + __expf(v.x - nm) + __expf(v.y - nm) + __expf(v.z - nm) + __expf(v.w - nm);
+        mx = nm;
+      } else if (v.x != v.x || v.y != v.y || v.z != v.z || v.w != v.w) {
+        sm = NAN;
+      }
+    }
+  for (int j = m4 + tid; j < m; j += NT) {
+    const float v = sr[j];
+    rs += v;
+    if (v > mx) {
+      sm = sm * __expf(mx - v) + 1.f;
+      mx = v;
+    } else if (v != -INFINITY) {
+      sm += __expf(v - mx);
+    }
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    const float m2 = __shfl_xor(mx, off, 64), s2 = __shfl_xor(sm, off, 64);
+    lse_merge(mx, sm, m2, s2);
+    rs += __shfl_xor(rs, off, 64);
+  }
+  if ((tid & 63) == 0) {
+    red[0][tid >> 6] = mx;
+    red[1][tid >> 6] = sm;
+    red[2][tid >> 6] = rs;
+  }
+  __syncthreads();
+  mx = red[0][0];
+  sm = red[1][0];
+  rs = red[2][0];
+#pragma unroll
+  for (int w = 1; w < NT / 64; ++w) {
+    lse_merge(mx, sm, red[0][w], red[1][w]);
+    rs += red[2][w];
+  }
+  __syncthreads();
+}
+
+template <int NI>
+__device__ __forceinline__ void row_grad_regs(const float* sr, float* gr, int m, const RowRegs<NI>& r, float lse,
+                                              float a, float b) {
+  const int tid = threadIdx.x, m4 = m & ~3;
+#pragma unroll
+  for (int i = 0; i < NI; ++i)
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int j = i * NT * 4 * U + (u * NT + tid) * 4;
+      const float4 v = r.v[i][u];
+      if (j < m4)
+        *reinterpret_cast<float4*>(gr + j) = make_float4(a * __expf(v.x - lse) - b, a * __expf(v.y - lse) - b,
+                                                         a * __expf(v.z - lse) - b, a * __expf(v.w - lse) - b);
+    }
+  for (int j = m4 + tid; j < m; j += NT) gr[j] = a * __expf(sr[j] - lse) - b;
+}
+
+__device__ __forceinline__ float block_sum(float v, float* red);
+
 __device__ __forceinline__ float block_sum(float v, float* red) {
   const int tid = threadIdx.x;
 #pragma unroll
@@ -146,7 +243,7 @@ __device__ __forceinline__ float block_sum(float v, float* red) {
 }
 
 // l_ptr == NULL: index labels, P_i = {l_col[i]}
-template <bool VEC>
+template <bool VEC, int NI = 0>
 __global__ void __launch_bounds__(NT) softmax_kl_kernel(const float* s, int64_t lds, int m,
                                                         const int64_t* __restrict__ l_ptr,
                                                         const int64_t* __restrict__ l_col, float eps, float scale,
@@ -165,7 +262,13 @@ __global__ void __launch_bounds__(NT) softmax_kl_kernel(const float* s, int64_t 
     ps += (c >= 0 && c < m) ? sr[c] : NAN;  // a label outside the row poisons the loss
   }
   float mx, sm, rs;
-  row_stats<VEC>(sr, m, red, mx, sm, rs);
+  RowRegs<NI ? NI : 1> regs;
+  if constexpr (NI > 0) {
+    row_load_regs<NI>(sr, m, regs);
+    row_stats_regs<NI>(sr, m, regs, red, mx, sm, rs);
+  } else {
+    row_stats<VEC>(sr, m, red, mx, sm, rs);
+  }
   ps = block_sum(ps, red[0]);
 
   const float lse = mx + __logf(sm);
@@ -187,7 +290,10 @@ __global__ void __launch_bounds__(NT) softmax_kl_kernel(const float* s, int64_t 
 
   // pass 2: G = scale * (T softmax - t0), then positives -= scale * (t1 - t0)
   float* gr = g + row * ldg;
-  row_grad<VEC>(sr, gr, m, lse, scale * T, scale * t0);
+  if constexpr (NI > 0)
+    row_grad_regs<NI>(sr, gr, m, regs, lse, scale * T, scale * t0);
+  else
+    row_grad<VEC>(sr, gr, m, lse, scale * T, scale * t0);
   __syncthreads();  // every write of the row is ordered before the positives' fix-up
   const float d = scale * (t1 - t0);
   for (int64_t k = p0 + tid; k < p1; k += NT) {
@@ -237,7 +343,15 @@ bool vec_ok(const float* s, int64_t lds, const float* g, int64_t ldg) {
 
 int launch(const float* s, int64_t lds, int64_t n, int64_t m, const int64_t* l_ptr, const int64_t* l_col, float eps,
            float scale, float* loss, float* g, int64_t ldg, hipStream_t st) {
-  if (vec_ok(s, lds, g, ldg))
+  const int64_t m4 = m & ~3LL, chunk = (int64_t)NT * 4 * U;
+  const bool vec = vec_ok(s, lds, g, ldg);
+  if (vec && m4 >= 4 && m4 <= chunk)
+    softmax_kl_kernel<true, 1><<<dim3((unsigned)n), dim3(NT), 0, st>>>(s, lds, (int)m, l_ptr, l_col, eps, scale,
+                                                                       loss, g, ldg);
+  else if (vec && m4 > chunk && m4 <= 2 * chunk)
+    softmax_kl_kernel<true, 2><<<dim3((unsigned)n), dim3(NT), 0, st>>>(s, lds, (int)m, l_ptr, l_col, eps, scale,
+                                                                       loss, g, ldg);
+  else if (vec)
     softmax_kl_kernel<true><<<dim3((unsigned)n), dim3(NT), 0, st>>>(s, lds, (int)m, l_ptr, l_col, eps, scale, loss,
                                                                     g, ldg);
   else
