@@ -221,6 +221,8 @@ class _ScoreXent2(torch.autograd.Function):
             loss_rows = L.softmax_kl(s, l_ptr, torch.cat((lab_a, lab_b)), smoothing, scale, g=s)
         ctx.meta = (kind, precision, n_a, n, d_e, d_r, dir_a, dir_b)
         ctx.save_for_backward(ent, rel, eidx_a, ridx_a, eidx_b, ridx_b, q if q is not None else s.new_empty(0), s)
+        if 2 * n_a == n:  # equal parts (1vsAll): one reduction for both sums
+            return loss_rows.view(2, n_a).sum(1) * scale
         return torch.stack((loss_rows[:n_a].sum(), loss_rows[n_a:].sum())) * scale
 
     @staticmethod
@@ -229,15 +231,21 @@ class _ScoreXent2(torch.autograd.Function):
         ent, rel, eidx_a, ridx_a, eidx_b, ridx_b, q, g = ctx.saved_tensors
         tab_w = window(kind, dir_a, ent)
         # dL/dS = gl[part] * G on each part's rows: folded into the [n, d] operands
-        row_scale = torch.cat((gl[0].expand(n_a), gl[1].expand(n - n_a)))[:, None]
         dq = L.score_dot_bwd_q(g, tab_w, None, precision)
-        dq.mul_(row_scale)
+        if 2 * n_a == n:  # equal parts: broadcast the two factors (no row-scale vector)
+            gl3 = gl.view(2, 1, 1)
+            dq.view(2, n_a, -1).mul_(gl3)
+            q_s = (q.view(2, n_a, -1) * gl3).view(n, -1)
+        else:
+            row_scale = torch.cat((gl[0].expand(n_a), gl[1].expand(n - n_a)))[:, None]
+            dq.mul_(row_scale)
+            q_s = q * row_scale
         if tab_w.shape[1] == d_e:  # the GEMM covers every column: write, do not accumulate
             d_ent = torch.empty_like(ent)
-            L.score_dot_bwd_t(g, q * row_scale, None, d_ent, precision, accumulate=False)
+            L.score_dot_bwd_t(g, q_s, None, d_ent, precision, accumulate=False)
         else:
             d_ent = torch.zeros_like(ent)
-            L.score_dot_bwd_t(g, q * row_scale, None, window(kind, dir_a, d_ent), precision)
+            L.score_dot_bwd_t(g, q_s, None, window(kind, dir_a, d_ent), precision)
         d_rel = torch.zeros_like(rel)
         L.prep_query_bwd(kind, dir_a, ent, eidx_a, rel, ridx_a, n_a, d_e, d_r, dq[:n_a], d_ent, d_rel)
         L.prep_query_bwd(kind, dir_b, ent, eidx_b, rel, ridx_b, n - n_a, d_e, d_r, dq[n_a:], d_ent, d_rel)

@@ -303,30 +303,32 @@ class TrainingJob1vsAll(TrainingJob):
         t = -time.time()
         triples = batch["triples"].to(self.device, non_blocking=True)
         bs = len(triples)
+        cols = triples.t().contiguous()  # s, p, o as contiguous index vectors (one copy)
         t += time.time()
         fused = self.config.get("engine.fused_loss") and isinstance(self.loss, KLDivWithSoftmaxKgeLoss)
         fwd = -time.time()
-        both = self.model.score_sp_po_xent(triples[:, S], triples[:, P], triples[:, O], 1.0 / bs) if fused else None
+        both = self.model.score_sp_po_xent(cols[S], cols[P], cols[O], 1.0 / bs) if fused else None
         if both is not None:  # sp_ and _po in one engine pass; one backward (same gradient sum)
             fwd += time.time()
             bwd = -time.time()
-            both.sum().backward()
+            total = both.sum()
+            total.backward()
             bwd += time.time()
-            return TrainingJob._ProcessBatchResult(both.detach().sum(), bs, t, fwd, bwd)
-        loss_sp = self.model.score_sp_xent(triples[:, S], triples[:, P], triples[:, O], 1.0 / bs) if fused else None
+            return TrainingJob._ProcessBatchResult(total.detach(), bs, t, fwd, bwd)
+        loss_sp = self.model.score_sp_xent(cols[S], cols[P], cols[O], 1.0 / bs) if fused else None
         if loss_sp is None:
-            scores_sp = self.model.score_sp(triples[:, S], triples[:, P])
-            loss_sp = self.loss(scores_sp, triples[:, O]) / bs
+            scores_sp = self.model.score_sp(cols[S], cols[P])
+            loss_sp = self.loss(scores_sp, cols[O]) / bs
             del scores_sp
         fwd += time.time()
         bwd = -time.time()
         loss_sp.backward()
         bwd += time.time()
         fwd -= time.time()
-        loss_po = self.model.score_po_xent(triples[:, P], triples[:, O], triples[:, S], 1.0 / bs) if fused else None
+        loss_po = self.model.score_po_xent(cols[P], cols[O], cols[S], 1.0 / bs) if fused else None
         if loss_po is None:
-            scores_po = self.model.score_po(triples[:, P], triples[:, O])
-            loss_po = self.loss(scores_po, triples[:, S]) / bs
+            scores_po = self.model.score_po(cols[P], cols[O])
+            loss_po = self.loss(scores_po, cols[S]) / bs
             del scores_po
         fwd += time.time()
         bwd -= time.time()
