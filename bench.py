@@ -331,6 +331,9 @@ def extras(args, model, c, E, R, device):
     res["eval_first_run_seconds"] = round(t1 - t0, 4)
     res["eval_mrr_filtered"] = tr["mean_reciprocal_rank_filtered"]
     res["eval_hits_at_10_filtered"] = tr["hits_at_10_filtered"]
+    res["eval_note"] = ("synthetic triples are drawn at random (no learnable structure), so the model trained "
+                        "for the timing steps ranks near chance; rank / MRR parity with the reference is pinned "
+                        "by the reference-captured eval fixtures (tests/test_gpu_api.py, tests/golden/eval_*.npz)")
     res.update(other_configs(device))
     if args.c5:
         res.update(c5_shard(args, device))
