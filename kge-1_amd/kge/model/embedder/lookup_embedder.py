@@ -69,6 +69,10 @@ class LookupEmbedder(KgeEmbedder):
     def _embeddings_all(self) -> Tensor:
         return self._embeddings.weight
 
+    def penalty_active(self) -> bool:
+        """Whether penalty() returns a term (lp regularisation with a non-zero weight)."""
+        return self.regularize != "" and self.get_option("regularize_weight") != 0.0
+
     def penalty(self, **kwargs) -> List:
         """Lp regularisation (lookup_embedder.py:112-158)."""
         result = super().penalty(**kwargs)

@@ -287,6 +287,11 @@ class KgeModel(KgeBase):
         self._relation_embedder.prepare_job(job, **kwargs)
 
     def penalty(self, **kwargs) -> List[Tensor]:
+        embs = (self.get_s_embedder(), self.get_p_embedder(), self.get_o_embedder())
+        if not any(getattr(e, "penalty_active", lambda: True)() for e in embs):
+            # nothing regularises (the default weight 0): skip the per-batch index upload
+            # the reference does anyway (kge_model.py:588-605 moves the batch to the device)
+            return super().penalty(**kwargs)
         if "batch" in kwargs and "triples" in kwargs["batch"]:
             triples = kwargs["batch"]["triples"].to(self.config.get("job.device"))
             return (super().penalty(**kwargs)

@@ -34,10 +34,7 @@ perm = torch.randperm(job.num_examples, generator=torch.Generator().manual_seed(
 
 
 def step(i):
-    job.optimizer.zero_grad()
-    res = job._process_batch(i, job._collate(perm[i * B:(i + 1) * B]))
-    job.optimizer.step()
-    return res
+    return job.train_step(i, job._collate(perm[i * B:(i + 1) * B]))[0]
 
 
 for i in range(5):
