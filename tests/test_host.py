@@ -125,3 +125,39 @@ def test_csr_minus():
     pb, cb = np.array([0, 1, 2, 3]), np.array([2, 9, 8])
     p, c = _csr_minus(pa, ca, pb, cb, 10)
     assert p.tolist() == [0, 2, 2, 3] and c.tolist() == [1, 3, 7]
+
+
+def test_kvsall_batch_queries_host_csr():
+    """TrainingJobKvsAll._queries (the batch's query pairs and label CSR, built on the host
+    and shipped in one copy) against the answers of each query read from the triples."""
+    from kge import Config, Dataset
+    from kge.job import TrainingJob
+
+    c = Config()
+    c.set("model", "distmult")
+    c._import("distmult")
+    c.set("job.device", "cpu")
+    c.set("lookup_embedder.dim", 8)
+    c.set("train.type", "KvsAll")
+    c.set("dataset.num_entities", 40)
+    c.set("dataset.num_relations", 5)
+    c.set("verbose", False)
+    rng = np.random.default_rng(3)
+    t = np.stack([rng.integers(0, 40, 400), rng.integers(0, 5, 400), rng.integers(0, 40, 400)], 1).astype(np.int32)
+    ds = Dataset(c, None)
+    ds._triples = {"train": torch.from_numpy(t)}
+    job = TrainingJob.create(c, ds)
+    job._prepare()
+    answers = [{}, {}]
+    for s, p, o in t.tolist():
+        answers[0].setdefault((s, p), set()).add(o)
+        answers[1].setdefault((p, o), set()).add(s)
+    for qi in range(2):
+        n_q = len(job.query_indexes[qi])
+        sel = rng.choice(n_q, size=min(n_q, 37), replace=False)
+        q, l_ptr, l_col = job._queries(qi, sel)
+        assert q.shape == (len(sel), 2) and l_ptr.shape == (len(sel) + 1,) and int(l_ptr[0]) == 0
+        for i in range(len(sel)):
+            key = tuple(q[i].tolist())
+            got = sorted(l_col[int(l_ptr[i]):int(l_ptr[i + 1])].tolist())
+            assert got == sorted(answers[qi][key]), (qi, key)
