@@ -127,6 +127,17 @@ int kge_score_dot_bwd_q(const float* g, int64_t ldg, const float* t, int64_t ldt
                         const int64_t* tidx, int64_t n, int64_t m, int d, float* dq,
                         int64_t lddq, int accumulate, int precision, void* stream);
 
+/* The same with a caller-owned workspace of ws_elems floats (16-B aligned).  When it holds
+ * kge_score_dot_bwd_q_ws_size(n, m, d, precision) floats, the bf16x3 path's K chunks write
+ * partial slabs that one pass adds in a fixed order (no float atomics: deterministic, and
+ * no zero fill of dQ); otherwise it behaves as kge_score_dot_bwd_q.  Replaces the same
+ * autograd step as kge_score_dot_bwd_q (mm backward of complex.py:36-44). */
+int64_t kge_score_dot_bwd_q_ws_size(int64_t n, int64_t m, int d, int precision);
+int kge_score_dot_bwd_q_ws(const float* g, int64_t ldg, const float* t, int64_t ldt,
+                           const int64_t* tidx, int64_t n, int64_t m, int d, float* dq,
+                           int64_t lddq, int accumulate, int precision, float* ws,
+                           int64_t ws_elems, void* stream);
+
 /* dT[row(j), k] += sum_i G[i, j] * Q[i, k]   (always accumulates; rows scattered
  * atomically when tidx != NULL) */
 int kge_score_dot_bwd_t(const float* g, int64_t ldg, const float* q, int64_t ldq,

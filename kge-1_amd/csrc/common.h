@@ -98,8 +98,10 @@ static inline int kge_num_cus() {
 }
 
 // bf16x3 backward GEMMs (gemm_bwd3.hip), dispatched from kge_score_dot_bwd_q / _t.
+int kge_bwd3_q_splits(int64_t n, int64_t m, int d, int cus);
 int kge_bwd3_q(const float* g, int64_t ldg, const float* t, int64_t ldt, const int64_t* tidx, int64_t n,
-               int64_t m, int d, float* dq, int64_t lddq, int cus, hipStream_t st);
+               int64_t m, int d, float* dq, int64_t lddq, int accumulate, float* ws, int64_t ws_elems, int cus,
+               hipStream_t st);
 int kge_bwd3_t(const float* g, int64_t ldg, const float* q, int64_t ldq, const int64_t* tidx, int64_t n,
                int64_t m, int d, float* dt, int64_t lddt, int accumulate, hipStream_t st);
 

@@ -120,19 +120,37 @@ __global__ void __launch_bounds__(NT, 2)
 
 }  // namespace
 
+extern "C" int64_t kge_score_dot_bwd_q_ws_size(int64_t n, int64_t m, int d, int precision) {
+  if (precision != KGE_PREC_BF16X3 || n <= 0 || m <= 0 || d <= 0) return 0;
+  const int splits = kge_bwd3_q_splits(n, m, d, kge_num_cus());
+  return splits > 1 ? (int64_t)splits * n * d : 0;
+}
+
 extern "C" int kge_score_dot_bwd_q(const float* g, int64_t ldg, const float* t, int64_t ldt,
                                    const int64_t* tidx, int64_t n, int64_t m, int d, float* dq,
                                    int64_t lddq, int accumulate, int precision, void* stream) {
+  return kge_score_dot_bwd_q_ws(g, ldg, t, ldt, tidx, n, m, d, dq, lddq, accumulate, precision, nullptr, 0, stream);
+}
+
+extern "C" int kge_score_dot_bwd_q_ws(const float* g, int64_t ldg, const float* t, int64_t ldt,
+                                      const int64_t* tidx, int64_t n, int64_t m, int d, float* dq,
+                                      int64_t lddq, int accumulate, int precision, float* ws, int64_t ws_elems,
+                                      void* stream) {
   KGE_REQUIRE(n >= 0 && m >= 0 && d > 0 && n < (1LL << 31) && m < (1LL << 31));
-  KGE_REQUIRE(g && t && dq && ldg >= m && ldt >= d && lddq >= d);
+  KGE_REQUIRE(g && t && dq && ldg >= m && ldt >= d && lddq >= d && ws_elems >= 0);
   KGE_REQUIRE(precision == KGE_PREC_FP32 || precision == KGE_PREC_BF16X3);
   hipStream_t st = as_stream(stream);
-  if (!accumulate && n > 0) {
+  if (m == 0 && !accumulate && n > 0) {  // empty reduction: dq = 0
     hipError_t e = hipMemset2DAsync(dq, lddq * sizeof(float), 0, d * sizeof(float), n, st);
     if (e != hipSuccess) return (int)e;
   }
   if (n == 0 || m == 0) return 0;
-  if (precision == KGE_PREC_BF16X3) return kge_bwd3_q(g, ldg, t, ldt, tidx, n, m, d, dq, lddq, kge_num_cus(), st);
+  if (precision == KGE_PREC_BF16X3)
+    return kge_bwd3_q(g, ldg, t, ldt, tidx, n, m, d, dq, lddq, accumulate, ws, ws_elems, kge_num_cus(), st);
+  if (!accumulate) {
+    hipError_t e = hipMemset2DAsync(dq, lddq * sizeof(float), 0, d * sizeof(float), n, st);
+    if (e != hipSuccess) return (int)e;
+  }
   const int gm = (int)((n + BM - 1) / BM), gn = (d + BN - 1) / BN;
   // split the long K = m reduction so that the grid fills the chip (>= ~1024 blocks)
   int splits = (int)std::max<int64_t>(1, std::min<int64_t>((m + 255) / 256, 1024 / std::max(1, gm * gn)));

@@ -201,6 +201,8 @@ __global__ void __launch_bounds__(NT, 1)
           c[(int64_t)i * ldc + j] += v;
         } else if (C_MODE == 3) {
           c[(int64_t)i * ldc + j] = v;
+        } else if (C_MODE == 4) {
+          c[((int64_t)z * M + i) * ldc + j] = v;
         } else {
           atomicAdd(c + crow[i] * ldc + j, v);
         }
@@ -442,11 +444,35 @@ __global__ void __launch_bounds__(NT, 1)
           c[(int64_t)i * ldc + j] += v;
         } else if (C_MODE == 3) {
           c[(int64_t)i * ldc + j] = v;
+        } else if (C_MODE == 4) {  // this K chunk's partial slab (summed by slab_sum_kernel)
+          c[((int64_t)z * M + i) * ldc + j] = v;
         } else {
           atomicAdd(c + crow[i] * ldc + j, v);
         }
       }
     }
+}
+
+// out[i, j] (+)= sum over z = 0 .. splits-1 of slab[z][i][j], in z order: the split-K sum of
+// the dQ GEMM without float atomics (which run at ~1.3 TB/s of added bytes chip-wide,
+// MI355X_MICROARCH.md 'Global float atomics', and sum in arrival order) -- deterministic.
+__global__ void __launch_bounds__(256) slab_sum_kernel(const float* __restrict__ slab, int splits, int64_t M, int N,
+                                                       float* __restrict__ out, int64_t ldo, int accumulate) {
+  const int n4 = N / 4;
+  const int64_t total = M * n4;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t i = e / n4;
+    const int j = (int)(e - i * n4) * 4;
+    float4 acc = accumulate ? *reinterpret_cast<const float4*>(out + i * ldo + j) : make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int z = 0; z < splits; ++z) {
+      const float4 v = *reinterpret_cast<const float4*>(slab + (z * M + i) * N + j);
+      acc.x += v.x;
+      acc.y += v.y;
+      acc.z += v.z;
+      acc.w += v.w;
+    }
+    *reinterpret_cast<float4*>(out + i * ldo + j) = acc;
+  }
 }
 
 template <bool A_T, int C_MODE, bool GATHER, bool VEC>
@@ -482,13 +508,37 @@ bool vec_ok(const float* g, int64_t ldg, int64_t m, const float* x, int64_t ldx,
 
 }  // namespace
 
-// Called from kge_score_dot_bwd_q / _t (gemm_bwd.hip) for KGE_PREC_BF16X3.
-int kge_bwd3_q(const float* g, int64_t ldg, const float* t, int64_t ldt, const int64_t* tidx, int64_t n,
-               int64_t m, int d, float* dq, int64_t lddq, int cus, hipStream_t st) {
+// K splits of the dQ GEMM: enough that the grid covers the CUs once (one wave of
+// 1-block-per-CU tiles)
+int kge_bwd3_q_splits(int64_t n, int64_t m, int d, int cus) {
   const int64_t tiles = ((n + BM - 1) / BM) * ((d + BN - 1) / BN);
-  // split K = m so that the grid covers the CUs once (one wave of 1-block-per-CU tiles)
   const int64_t by_k = std::max<int64_t>(1, (m + 8 * BK - 1) / (8 * BK));
-  const int splits = (int)std::max<int64_t>(1, std::min<int64_t>(by_k, cus / std::max<int64_t>(1, tiles)));
+  return (int)std::max<int64_t>(1, std::min<int64_t>(by_k, cus / std::max<int64_t>(1, tiles)));
+}
+
+// Called from kge_score_dot_bwd_q / _t (gemm_bwd.hip) for KGE_PREC_BF16X3.  With a workspace
+// of splits * n * d floats (and vectorisable operands) the K chunks write partial slabs that
+// slab_sum_kernel adds in a fixed order; otherwise the chunks add into dq with float atomics
+// (dq zero-filled first unless accumulating).
+int kge_bwd3_q(const float* g, int64_t ldg, const float* t, int64_t ldt, const int64_t* tidx, int64_t n,
+               int64_t m, int d, float* dq, int64_t lddq, int accumulate, float* ws, int64_t ws_elems, int cus,
+               hipStream_t st) {
+  const int splits = kge_bwd3_q_splits(n, m, d, cus);
+  if (vec_ok(g, ldg, m, t, ldt, d) && splits > 1 && ws && ws_elems >= (int64_t)splits * n * d && lddq % 4 == 0 &&
+      aligned16(dq) && aligned16(ws)) {
+    const int e = tidx ? launch<false, 4, true, true>(g, ldg, t, ldt, tidx, ws, d, nullptr, n, d, m, splits, st)
+                       : launch<false, 4, false, true>(g, ldg, t, ldt, nullptr, ws, d, nullptr, n, d, m, splits, st);
+    if (e) return e;
+    const int64_t total = n * (d / 4);
+    const int blocks = (int)std::min<int64_t>((total + 255) / 256, (int64_t)cus * 4);
+    slab_sum_kernel<<<dim3(blocks), dim3(256), 0, st>>>(ws, splits, n, d, dq, lddq, accumulate);
+    KGE_CHECK_LAUNCH();
+    return 0;
+  }
+  if (!accumulate) {
+    hipError_t e = hipMemset2DAsync(dq, lddq * sizeof(float), 0, d * sizeof(float), n, st);
+    if (e != hipSuccess) return (int)e;
+  }
   if (vec_ok(g, ldg, m, t, ldt, d)) {
     if (tidx) return launch<false, 0, true, true>(g, ldg, t, ldt, tidx, dq, lddq, nullptr, n, d, m, splits, st);
     return launch<false, 0, false, true>(g, ldg, t, ldt, nullptr, dq, lddq, nullptr, n, d, m, splits, st);

@@ -44,6 +44,8 @@ SIGNATURES = {
     "kge_split_rows": ([_P, _I64, _I64, _I, _P, _P, _I64, _P], _I),
     "kge_score_dot_split": ([_P, _P, _I64, _P, _I64, _P, _I64, _I64, _I, _P, _I64, _P], _I),
     "kge_score_dot_bwd_q": ([_P, _I64, _P, _I64, _P, _I64, _I64, _I, _P, _I64, _I, _I, _P], _I),
+    "kge_score_dot_bwd_q_ws_size": ([_I64, _I64, _I, _I], _I64),
+    "kge_score_dot_bwd_q_ws": ([_P, _I64, _P, _I64, _P, _I64, _I64, _I, _P, _I64, _I, _I, _P, _I64, _P], _I),
     "kge_score_dot_bwd_t": ([_P, _I64, _P, _I64, _P, _I64, _I64, _I, _P, _I64, _I, _P], _I),
     "kge_adagrad_step": ([_P, _P, _P, _I64, ctypes.c_float, ctypes.c_float, ctypes.c_float, _I, _P], _I),
     "kge_score_dot_bwd_t_ex": ([_P, _I64, _P, _I64, _P, _I64, _I64, _I, _P, _I64, _I, _I, _P], _I),
@@ -252,8 +254,12 @@ def score_dot_bwd_q(g, t, tidx, precision, dq=None, accumulate=False):
     if dq is None:
         dq = torch.empty(n, d, device=g.device, dtype=torch.float32)
         accumulate = False
-    _check(lib().kge_score_dot_bwd_q(ptr(g), rows(g), ptr(t), rows(t), ptr(tidx), n, m, d, ptr(dq),
-                                     rows(dq), int(accumulate), precision, stream()), "kge_score_dot_bwd_q")
+    # split-K partial slabs summed in a fixed order instead of float atomics (bf16x3)
+    ws_n = lib().kge_score_dot_bwd_q_ws_size(n, m, d, precision)
+    ws = torch.empty(ws_n, device=g.device, dtype=torch.float32) if ws_n > 0 else None
+    _check(lib().kge_score_dot_bwd_q_ws(ptr(g), rows(g), ptr(t), rows(t), ptr(tidx), n, m, d, ptr(dq),
+                                        rows(dq), int(accumulate), precision, ptr(ws), ws_n, stream()),
+           "kge_score_dot_bwd_q")
     return dq
 
 

@@ -15,7 +15,7 @@ def test_library_exports_every_header_symbol():
     from kge import _lib
 
     header = open(os.path.join(ROOT, "include", "kgescore.h")).read()
-    declared = set(re.findall(r"^\s*(?:int|const char\*)\s+(kge_\w+)\s*\(", header, re.M))
+    declared = set(re.findall(r"^\s*(?:int|int64_t|const char\*)\s+(kge_\w+)\s*\(", header, re.M))
     assert declared == set(_lib.SIGNATURES), declared ^ set(_lib.SIGNATURES)
     lib = _lib.lib()
     for name in declared:
