@@ -188,7 +188,10 @@ class _GraphStep:
     attributes, optimizer state, allocator warm-up); the third is recorded (recording runs
     nothing) and replayed, and every later full batch is copied into the recorded index
     buffer and replayed.  The optimizer's host-side step counters are advanced per replay.
-    A partial last batch, or any step the recording cannot take, runs eagerly."""
+    A partial last batch, or any step the recording cannot take, runs eagerly.  Like any
+    recorded graph it assumes the parameters and optimizer state stay where they are
+    (in-place updates such as load_state_dict are fine; re-creating the tensors is not:
+    call disable() or build a new job)."""
 
     WARMUP = 2
 
