@@ -135,3 +135,18 @@ def test_graph_step_not_used_when_unsafe():
     job = TrainingJob.create(c, ds)
     job._prepare()
     assert job._graph_step is None
+
+
+def test_graph_step_run_epoch_matches_eager():
+    """Two epochs through run_epoch (the job's own loop: pinned one-batch-late loss reads,
+    a partial last batch, the recorded step replayed from the third batch on) with and
+    without engine.graph_step: same epoch losses."""
+    traces = {}
+    for graph in (False, True):
+        job, _ = _job(graph, "fp32")
+        job.generator.manual_seed(0)
+        traces[graph] = [job.run_epoch()["avg_loss"] for _ in range(2)]
+        if graph:
+            assert job._graph_step.graph is not None
+    np.testing.assert_allclose(traces[True], traces[False], rtol=1e-5)
+    assert traces[True][1] < traces[True][0]
