@@ -301,6 +301,13 @@ int kge_rank_hist(const int64_t* greater, const int64_t* ties, int64_t n,
                   int tie_handling, int64_t* ranks, float* hist, int64_t hist_len,
                   void* stream);
 
+/* The same for several rankings in one launch: row i counts into histogram
+ * i / rows_per_hist of hist[(n / rows_per_hist) x hist_len] (the raw / filtered /
+ * filtered-with-test histograms of one eval batch direction, eval.py:148-171). */
+int kge_rank_hist_multi(const int64_t* greater, const int64_t* ties, int64_t n,
+                        int64_t rows_per_hist, int tie_handling, int64_t* ranks,
+                        float* hist, int64_t hist_len, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

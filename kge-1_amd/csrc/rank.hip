@@ -97,14 +97,15 @@ __global__ void __launch_bounds__(NT) rank_counts_kernel(const float* __restrict
   }
 }
 
+// row i counts into histogram i / rows_per_hist (hists of hist_len floats, back to back)
 __global__ void rank_hist_kernel(const int64_t* __restrict__ greater, const int64_t* __restrict__ ties, int64_t n,
-                                 int tie, int64_t* ranks, float* hist, int64_t hist_len) {
+                                 int64_t rows_per_hist, int tie, int64_t* ranks, float* hist, int64_t hist_len) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const int64_t g = greater[i], t = ties[i];
   int64_t r = tie == KGE_TIE_ROUNDED_MEAN ? g + t / 2 : (tie == KGE_TIE_BEST ? g : g + t - 1);
   if (ranks) ranks[i] = r;
-  if (hist && r >= 0 && r < hist_len) atomicAdd(hist + r, 1.0f);
+  if (hist && r >= 0 && r < hist_len) atomicAdd(hist + (i / rows_per_hist) * hist_len + r, 1.0f);
 }
 
 }  // namespace
@@ -126,10 +127,15 @@ extern "C" int kge_rank_counts(const float* s, int64_t lds, int64_t n, int64_t m
 
 extern "C" int kge_rank_hist(const int64_t* greater, const int64_t* ties, int64_t n, int tie_handling,
                              int64_t* ranks, float* hist, int64_t hist_len, void* stream) {
-  KGE_REQUIRE(n >= 0 && greater && ties && tie_handling >= 0 && tie_handling <= 2);
+  return kge_rank_hist_multi(greater, ties, n, n > 0 ? n : 1, tie_handling, ranks, hist, hist_len, stream);
+}
+
+extern "C" int kge_rank_hist_multi(const int64_t* greater, const int64_t* ties, int64_t n, int64_t rows_per_hist,
+                                   int tie_handling, int64_t* ranks, float* hist, int64_t hist_len, void* stream) {
+  KGE_REQUIRE(n >= 0 && greater && ties && tie_handling >= 0 && tie_handling <= 2 && rows_per_hist > 0);
   if (n == 0) return 0;
   rank_hist_kernel<<<dim3((unsigned)((n + 255) / 256)), dim3(256), 0, as_stream(stream)>>>(
-      greater, ties, n, tie_handling, ranks, hist, hist_len);
+      greater, ties, n, rows_per_hist, tie_handling, ranks, hist, hist_len);
   KGE_CHECK_LAUNCH();
   return 0;
 }

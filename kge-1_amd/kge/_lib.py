@@ -66,6 +66,7 @@ SIGNATURES = {
                                 _I64, _P, _I64, _P], _I),
     "kge_bucket_scatter": ([_P, _I64, _P, _P, _P], _I),
     "kge_stage_i64": ([_P, _P, _I64, _P], _I),
+    "kge_rank_hist_multi": ([_P, _P, _I64, _I64, _I, _P, _P, _I64, _P], _I),
     "kge_softmax_row_stats": ([_P, _I64, _I64, _I64, _I64, _P, _P, _P, _P, _P], _I),
     "kge_softmax_grad": ([_P, _I64, _I64, _I64, _I64, _P, _P, _F, _P, _I64, _P], _I),
 }
@@ -325,6 +326,16 @@ def rank_counts(s, c0, true_idx, true_score, f_ptr, f_col, t_ptr, t_col, greater
     _check(lib().kge_rank_counts(ptr(s), rows(s), n, m, c0, ptr(true_idx), ptr(true_score), ptr(f_ptr),
                                  ptr(f_col), ptr(t_ptr), ptr(t_col), ptr(greater), ptr(ties), stream()),
            "kge_rank_counts")
+
+
+def rank_hist_multi(greater, ties, rows_per_hist, tie_handling, ranks, hists):
+    """kge_rank_hist_multi: row i of greater / ties counts into hists[i // rows_per_hist]."""
+    greater, ties = greater.contiguous(), ties.contiguous()
+    n = greater.numel()
+    if hists.dim() != 2 or not hists.is_contiguous() or n > hists.shape[0] * rows_per_hist:
+        raise ValueError("rank_hist_multi: hists must be a contiguous [k, hist_len] tensor covering every row")
+    _check(lib().kge_rank_hist_multi(ptr(greater), ptr(ties), n, rows_per_hist, TIE[tie_handling], ptr(ranks),
+                                     ptr(hists), hists.shape[1], stream()), "kge_rank_hist_multi")
 
 
 def rank_hist(greater, ties, tie_handling, ranks, hist):

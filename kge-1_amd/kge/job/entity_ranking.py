@@ -81,6 +81,9 @@ class EntityRankingJob(EvaluationJob):
 
     def _prepare(self):
         self.model.prepare_job(self)
+        from ..model.reciprocal_relations_model import ReciprocalRelationsModel
+
+        self._two_sided = isinstance(self.model, ReciprocalRelationsModel)
         self.triples = self.dataset.split(self.eval_split).long()
         tri = self.triples.numpy()
         E = self.dataset.num_entities()
@@ -120,9 +123,12 @@ class EntityRankingJob(EvaluationJob):
             B = b1 - b0
             s, p, o = triples[b0:b1, 0], triples[b0:b1, 1], triples[b0:b1, 2]
             o_true = self.model.score_spo(s, p, o, "o").view(-1).float().contiguous()
-            s_true = self.model.score_spo(s, p, o, "s").view(-1).float().contiguous()
-            g = {d: torch.zeros(3 * B, dtype=torch.int64, device=dev) for d in "so"}
-            t = {d: torch.zeros(3 * B, dtype=torch.int64, device=dev) for d in "so"}
+            # score_spo(.., "s") is the same triple score unless the model scores the two
+            # directions differently (reciprocal relations): skip the second launch then
+            s_true = o_true if not self._two_sided else self.model.score_spo(s, p, o, "s").view(-1).float().contiguous()
+            counts = torch.zeros(4, 3 * B, dtype=torch.int64, device=dev)  # greater / ties per direction
+            g = {"o": counts[0], "s": counts[1]}
+            t = {"o": counts[2], "s": counts[3]}
             for c0 in range(0, E, chunk):
                 c1 = min(E, c0 + chunk)
                 subset = None if (c0 == 0 and c1 == E) else torch.arange(c0, c1, device=dev)
@@ -131,13 +137,12 @@ class EntityRankingJob(EvaluationJob):
                 self._count(scores[:, :C], c0, o, o_true, "sp", b0, b1, g["o"], t["o"])
                 self._count(scores[:, C:], c0, s, s_true, "po", b0, b1, g["s"], t["s"])
                 del scores
-            for ri, r in enumerate(self.rankings):
-                for d in "os":
-                    rk = torch.empty(B, dtype=torch.int64, device=dev)
-                    _lib.rank_hist(g[d][ri * B:(ri + 1) * B], t[d][ri * B:(ri + 1) * B], self.tie_handling, rk,
-                                   hists[ri])
-                    if self.capture_ranks:
-                        ranks_out[f"{d}{r}"].append(rk)
+            for d in "os":  # every ranking of one direction in one launch
+                rk = torch.empty(nrank * B, dtype=torch.int64, device=dev)
+                _lib.rank_hist_multi(g[d][:nrank * B], t[d][:nrank * B], B, self.tie_handling, rk, hists)
+                if self.capture_ranks:
+                    for ri, r in enumerate(self.rankings):
+                        ranks_out[f"{d}{r}"].append(rk[ri * B:(ri + 1) * B])
         epoch_time += time.time()
         metrics = {}
         for ri, r in enumerate(self.rankings):
