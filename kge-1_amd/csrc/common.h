@@ -4,6 +4,7 @@
 #include <stdint.h>
 
 #include <algorithm>
+#include <atomic>
 
 #include "../../include/kgescore.h"
 
@@ -85,16 +86,41 @@ __device__ __forceinline__ void split_bf16x4_pk_c(const float4& v, bf16x4& hi, b
   lo = __builtin_bit_cast(bf16x4, (uint2){l0, l1});
 }
 
-// Compute units of the current device (256 on MI355X); cached per translation unit.
+// Per-device host-side caches are indexed by the HIP device ordinal (one process may drive
+// several GPUs; function attributes and device properties belong to one device each).
+constexpr int KGE_MAX_DEVICES = 64;
+static inline int kge_device() {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= KGE_MAX_DEVICES) dev = 0;
+  return dev;
+}
+
+// Compute units of the current device (256 on MI355X); cached per device.
 static inline int kge_num_cus() {
-  static int cus = 0;
-  if (!cus) {
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess ||
-        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
-      cus = 256;
+  static std::atomic<int> cus[KGE_MAX_DEVICES];
+  const int dev = kge_device();
+  int c = cus[dev].load(std::memory_order_relaxed);
+  if (c <= 0) {
+    int real = 0;
+    if (hipGetDevice(&real) != hipSuccess ||
+        hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, real) != hipSuccess || c <= 0)
+      c = 256;
+    cus[dev].store(c, std::memory_order_relaxed);
   }
-  return cus;
+  return c;
+}
+
+// Raise a kernel's dynamic-LDS limit once per device (hipFuncSetAttribute acts on the
+// current device only).  `done` is a zero-initialised array of KGE_MAX_DEVICES flags owned by
+// the launch site; concurrent first calls both set the attribute, which is harmless.
+static inline int kge_allow_lds(const void* fn, int bytes, std::atomic<bool>* done) {
+  const int dev = kge_device();
+  if (!done[dev].load(std::memory_order_acquire)) {
+    hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+    if (e != hipSuccess) return (int)e;
+    done[dev].store(true, std::memory_order_release);
+  }
+  return 0;
 }
 
 // bf16x3 backward GEMMs (gemm_bwd3.hip), dispatched from kge_score_dot_bwd_q / _t.
