@@ -458,15 +458,11 @@ extern "C" int kge_score_cand_bwd(int model, float l_norm, int dir, const float*
     return 0;
   }
   const size_t sh = (size_t)(1 + NW) * d * sizeof(float);
-  static bool attr = false;
-  if (!attr) {
-    for (const void* f : {(const void*)cand_bwd_scalar_kernel<K_DOT>, (const void*)cand_bwd_scalar_kernel<K_TRANSE>,
-                          (const void*)cand_bwd_scalar_kernel<K_ROTATE>}) {
-      hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (1 + NW) * 3584 * 4);
-      if (e != hipSuccess) return (int)e;
-    }
-    attr = true;
-  }
+  static std::atomic<bool> lds_ok[3][KGE_MAX_DEVICES];
+  int fi = 0;
+  for (const void* f : {(const void*)cand_bwd_scalar_kernel<K_DOT>, (const void*)cand_bwd_scalar_kernel<K_TRANSE>,
+                        (const void*)cand_bwd_scalar_kernel<K_ROTATE>})
+    if (const int e = kge_allow_lds(f, (1 + NW) * 3584 * 4, lds_ok[fi++])) return e;
   if (kind == K_DOT)
     cand_bwd_scalar_kernel<K_DOT><<<grid, dim3(NT), sh, st>>>(l1, sigma, q, ldq, ent, ld_ent, cand, ldc, (int)k, d, s,
                                                               lds, g, ldg, dq, lddq, d_ent, ld_dent);

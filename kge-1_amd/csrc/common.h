@@ -131,6 +131,10 @@ int kge_bwd3_q(const float* g, int64_t ldg, const float* t, int64_t ldt, const i
 int kge_bwd3_t(const float* g, int64_t ldg, const float* q, int64_t ldq, const int64_t* tidx, int64_t n,
                int64_t m, int d, float* dt, int64_t lddt, int accumulate, hipStream_t st);
 
+// x[i, 0 .. d) = 0 for i < n by a fill kernel (gemm_bwd3.hip): unlike hipMemset*Async it may
+// be recorded into a HIP graph by a capturing caller.
+int kge_zero_rows(float* x, int64_t ldx, int64_t n, int d, hipStream_t st);
+
 // packed-VALU all-entities distance kernel (score_dist2.hip); -1 when the layout does not fit
 int kge_score_dist2(int kind, float sign, const float* q, int64_t ldq, const float* t, int64_t ldt,
                     const int64_t* tidx, int64_t n, int64_t m, int d, float* s, int64_t lds, hipStream_t st);

@@ -137,19 +137,17 @@ extern "C" int kge_score_dot_bwd_q_ws(const float* g, int64_t ldg, const float* 
                                       int64_t lddq, int accumulate, int precision, float* ws, int64_t ws_elems,
                                       void* stream) {
   KGE_REQUIRE(n >= 0 && m >= 0 && d > 0 && n < (1LL << 31) && m < (1LL << 31));
-  KGE_REQUIRE(g && t && dq && ldg >= m && ldt >= d && lddq >= d && ws_elems >= 0);
+  KGE_REQUIRE((g || m == 0) && (t || m == 0) && dq && ldg >= m && ldt >= d && lddq >= d && ws_elems >= 0);
   KGE_REQUIRE(precision == KGE_PREC_FP32 || precision == KGE_PREC_BF16X3);
   hipStream_t st = as_stream(stream);
   if (m == 0 && !accumulate && n > 0) {  // empty reduction: dq = 0
-    hipError_t e = hipMemset2DAsync(dq, lddq * sizeof(float), 0, d * sizeof(float), n, st);
-    if (e != hipSuccess) return (int)e;
+    if (const int e = kge_zero_rows(dq, lddq, n, d, st)) return e;
   }
   if (n == 0 || m == 0) return 0;
   if (precision == KGE_PREC_BF16X3)
     return kge_bwd3_q(g, ldg, t, ldt, tidx, n, m, d, dq, lddq, accumulate, ws, ws_elems, kge_num_cus(), st);
   if (!accumulate) {
-    hipError_t e = hipMemset2DAsync(dq, lddq * sizeof(float), 0, d * sizeof(float), n, st);
-    if (e != hipSuccess) return (int)e;
+    if (const int e = kge_zero_rows(dq, lddq, n, d, st)) return e;
   }
   const int gm = (int)((n + BM - 1) / BM), gn = (d + BN - 1) / BN;
   // split the long K = m reduction so that the grid fills the chip (>= ~1024 blocks)
@@ -179,8 +177,7 @@ extern "C" int kge_score_dot_bwd_t_ex(const float* g, int64_t ldg, const float* 
   if (m == 0) return 0;
   hipStream_t st = as_stream(stream);
   if (!accumulate && (n == 0 || precision == KGE_PREC_FP32)) {  // fp32 path: zero, then accumulate
-    hipError_t e = hipMemset2DAsync(dt, lddt * sizeof(float), 0, d * sizeof(float), m, st);
-    if (e != hipSuccess) return (int)e;
+    if (const int e = kge_zero_rows(dt, lddt, m, d, st)) return e;
     accumulate = 1;
   }
   if (n == 0) return 0;

@@ -475,16 +475,22 @@ __global__ void __launch_bounds__(256) slab_sum_kernel(const float* __restrict__
   }
 }
 
+// x[i, 0 .. d) = 0 for i < n (a fill kernel rather than hipMemset2DAsync, so that a caller may
+// capture the launch sequence into a HIP graph).
+__global__ void __launch_bounds__(256) zero_rows_kernel(float* __restrict__ x, int64_t ldx, int64_t n, int d) {
+  const int64_t total = n * d;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x)
+    x[(e / d) * ldx + e % d] = 0.f;
+}
+
+int zero_rows(float* x, int64_t ldx, int64_t n, int d, hipStream_t st) { return kge_zero_rows(x, ldx, n, d, st); }
+
 template <bool A_T, int C_MODE, bool GATHER, bool VEC>
 int launch(const float* a, int64_t lda, const float* b, int64_t ldb, const int64_t* brow, float* c, int64_t ldc,
            const int64_t* crow, int64_t M, int64_t N, int64_t K, int splits, hipStream_t st) {
   const void* fn = VEC ? (const void*)gemm3v_kernel<A_T, C_MODE, GATHER> : (const void*)gemm3_kernel<A_T, C_MODE, GATHER>;
-  static bool attr_set = false;
-  if (!attr_set) {
-    hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, 2 * STAGE);
-    if (e != hipSuccess) return (int)e;
-    attr_set = true;
-  }
+  static std::atomic<bool> lds_ok[KGE_MAX_DEVICES];
+  if (const int e = kge_allow_lds(fn, 2 * STAGE, lds_ok)) return e;
   const int nmt = (int)((M + BM - 1) / BM), nnt = (int)((N + BN - 1) / BN);
   int kchunk = (int)((K + splits - 1) / splits);
   kchunk = (kchunk + BK - 1) / BK * BK;
@@ -507,6 +513,14 @@ bool vec_ok(const float* g, int64_t ldg, int64_t m, const float* x, int64_t ldx,
 }
 
 }  // namespace
+
+int kge_zero_rows(float* x, int64_t ldx, int64_t n, int d, hipStream_t st) {
+  if (n <= 0 || d <= 0) return 0;
+  const int blocks = (int)std::min<int64_t>((n * d + 255) / 256, 4096);
+  zero_rows_kernel<<<dim3(blocks), dim3(256), 0, st>>>(x, ldx, n, d);
+  KGE_CHECK_LAUNCH();
+  return 0;
+}
 
 // K splits of the dQ GEMM: enough that the grid covers the CUs once (one wave of
 // 1-block-per-CU tiles)
@@ -535,9 +549,15 @@ int kge_bwd3_q(const float* g, int64_t ldg, const float* t, int64_t ldt, const i
     KGE_CHECK_LAUNCH();
     return 0;
   }
+  if (vec_ok(g, ldg, m, t, ldt, d) && splits == 1) {  // K not split: every dQ element has one owner
+    if (accumulate)
+      return tidx ? launch<false, 1, true, true>(g, ldg, t, ldt, tidx, dq, lddq, nullptr, n, d, m, 1, st)
+                  : launch<false, 1, false, true>(g, ldg, t, ldt, nullptr, dq, lddq, nullptr, n, d, m, 1, st);
+    return tidx ? launch<false, 3, true, true>(g, ldg, t, ldt, tidx, dq, lddq, nullptr, n, d, m, 1, st)
+                : launch<false, 3, false, true>(g, ldg, t, ldt, nullptr, dq, lddq, nullptr, n, d, m, 1, st);
+  }
   if (!accumulate) {
-    hipError_t e = hipMemset2DAsync(dq, lddq * sizeof(float), 0, d * sizeof(float), n, st);
-    if (e != hipSuccess) return (int)e;
+    if (const int e = zero_rows(dq, lddq, n, d, st)) return e;
   }
   if (vec_ok(g, ldg, m, t, ldt, d)) {
     if (tidx) return launch<false, 0, true, true>(g, ldg, t, ldt, tidx, dq, lddq, nullptr, n, d, m, splits, st);

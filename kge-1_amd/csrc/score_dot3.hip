@@ -299,13 +299,9 @@ int launch_persist16(const __bf16* qhi, const __bf16* qlo, int64_t ldq, const fl
   const int64_t ntiles = (int64_t)nrt * ((m + BN - 1) / BN);
   if (ntiles > 0x7fffffff) return KGE_ERR_ARG;
   const size_t shmem = 2 * C::STAGE;
-  static bool attr_set = false;
-  if (!attr_set) {
-    hipError_t e = hipFuncSetAttribute((const void*)score_dot_persist16_kernel<BM, BN, WM, WN, ABL>,
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)shmem);
-    if (e != hipSuccess) return (int)e;
-    attr_set = true;
-  }
+  static std::atomic<bool> lds_ok[KGE_MAX_DEVICES];
+  if (const int e = kge_allow_lds((const void*)score_dot_persist16_kernel<BM, BN, WM, WN, ABL>, (int)shmem, lds_ok))
+    return e;
   int grid = kge_num_cus();
   grid = (int)std::min<int64_t>(grid, (ntiles + 7) / 8 * 8);
   grid = std::max(8, grid / 8 * 8);
