@@ -53,6 +53,7 @@ extern "C" {
 #define KGE_ERR_ARG 1001     /* invalid argument (shape, enum, null pointer) */
 #define KGE_ERR_ALIGN 1002   /* pointer / leading dimension alignment        */
 #define KGE_ERR_NOGPU 1003   /* no gfx950 device visible                      */
+#define KGE_ERR_SCRATCH 1004 /* needs more than the library's static scratch  */
 
 int kge_version(void);
 const char* kge_error_string(int status);
@@ -137,6 +138,20 @@ int kge_score_dot_bwd_q_ws(const float* g, int64_t ldg, const float* t, int64_t 
                            const int64_t* tidx, int64_t n, int64_t m, int d, float* dq,
                            int64_t lddq, int accumulate, int precision, float* ws,
                            int64_t ws_elems, void* stream);
+
+/* kge_score_dot_bwd_q (bf16x3) for callers that cannot allocate device memory -- code under
+ * HIP graph capture, tight serving loops, harnesses that forbid hipMalloc.  It has no
+ * counterpart in the reference.  The split-K partial slabs go to a 32 MiB static device array
+ * inside the library (one copy per GPU, held until the process ends) instead of a caller
+ * workspace; no hipMalloc / hipFree / allocating routine is called.  The first call on a
+ * device resolves that array's address (do it once outside a graph capture).  Limits:
+ * splits * n * d <= 8 Mi floats, else KGE_ERR_SCRATCH (never reached on a device of <= 256
+ * CUs); 16-B aligned g / t / dq with ldg, ldt, lddq, d multiples of 4 and ldg >= round_up(m, 4),
+ * else KGE_ERR_ALIGN.  Calls on one GPU share the array: calls that overlap there (two
+ * streams) race.  Results equal kge_score_dot_bwd_q_ws with a full-size workspace bit for bit. */
+int kge_score_dot_bwd_q_noalloc(const float* g, int64_t ldg, const float* t, int64_t ldt,
+                                const int64_t* tidx, int64_t n, int64_t m, int d, float* dq,
+                                int64_t lddq, int accumulate, void* stream);
 
 /* dT[row(j), k] += sum_i G[i, j] * Q[i, k]   (always accumulates; rows scattered
  * atomically when tidx != NULL) */

@@ -579,6 +579,62 @@ int kge_bwd3_t(const float* g, int64_t ldg, const float* q, int64_t ldq, const i
   return launch<true, 1, false, false>(g, ldg, q, ldq, nullptr, dt, lddt, nullptr, m, d, n, 1, st);
 }
 
+// ---------------------------------------------------------------------------------------
+// kge_score_dot_bwd_q_noalloc: the dQ GEMM for callers that cannot allocate (HIP graph
+// capture, serving loops).  The split-K partial slabs go to this file-scope device array
+// instead of a caller workspace.  Its size covers every shape on a device of up to 256 CUs:
+// splits <= CUs / tiles and tiles >= (n / BM) (d / BN), so splits * n * d <= 256 * BM * BN.
+// Each GPU the library runs on holds its own copy (at its own address) until the process
+// ends; every call on a GPU shares it, so calls that overlap on one GPU (two streams) race.
+// Nothing in it needs clearing between calls: every slab element that slab_sum_kernel reads
+// is written by the GEMM of the same call.
+constexpr int64_t SCRATCH_ELEMS = (int64_t)256 * BM * BN;  // 8 Mi floats = 32 MiB
+static __device__ __align__(256) float scratch[SCRATCH_ELEMS];
+
+namespace {
+std::atomic<float*> scratch_ptr[KGE_MAX_DEVICES];  // device address of `scratch`, per device
+
+// The array's name is a host-side stand-in, not a device address: resolve it once per device,
+// with that device current, and hand kernels the resolved pointer only.
+int scratch_address(float** out) {
+  int dev = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e != hipSuccess) return (int)e;
+  if (dev < 0 || dev >= KGE_MAX_DEVICES) return KGE_ERR_ARG;
+  float* p = scratch_ptr[dev].load(std::memory_order_acquire);
+  if (!p) {
+    void* sym = nullptr;
+    e = hipGetSymbolAddress(&sym, HIP_SYMBOL(scratch));
+    if (e != hipSuccess) return (int)e;
+    if (!sym) return (int)hipErrorInvalidSymbol;
+    p = static_cast<float*>(sym);
+    scratch_ptr[dev].store(p, std::memory_order_release);
+  }
+  *out = p;
+  return 0;
+}
+}  // namespace
+
+extern "C" int kge_score_dot_bwd_q_noalloc(const float* g, int64_t ldg, const float* t, int64_t ldt,
+                                           const int64_t* tidx, int64_t n, int64_t m, int d, float* dq,
+                                           int64_t lddq, int accumulate, void* stream) {
+  KGE_REQUIRE(n >= 0 && m >= 0 && d > 0 && n < (1LL << 31) && m < (1LL << 31));
+  KGE_REQUIRE((g || m == 0) && (t || m == 0) && dq && ldg >= m && ldt >= d && lddq >= d);  // m == 0: g, t unread
+  hipStream_t st = as_stream(stream);
+  if (n == 0) return 0;
+  if (m == 0) return accumulate ? 0 : zero_rows(dq, lddq, n, d, st);
+  if (!vec_ok(g, ldg, m, t, ldt, d) || lddq % 4 != 0 || !aligned16(dq)) return KGE_ERR_ALIGN;
+  const int cus = kge_num_cus();
+  const int splits = kge_bwd3_q_splits(n, m, d, cus);
+  const int64_t need = splits > 1 ? (int64_t)splits * n * d : 0;
+  if (need > SCRATCH_ELEMS) return KGE_ERR_SCRATCH;
+  float* ws = nullptr;
+  if (need > 0) {
+    if (const int e = scratch_address(&ws)) return e;
+  }
+  return kge_bwd3_q(g, ldg, t, ldt, tidx, n, m, d, dq, lddq, accumulate, ws, need > 0 ? SCRATCH_ELEMS : 0, cus, st);
+}
+
 // Dev-only variants for scripts/tune_bwd.py (not in include/kgescore.h): 0 = dQ as shipped
 // (split-K atomics), 1 = dQ with plain stores (wrong sums: prices the atomics), 2 = dT
 // written (C_MODE 3), 3 = dT read-modify-write (C_MODE 1).

@@ -46,6 +46,7 @@ SIGNATURES = {
     "kge_score_dot_bwd_q": ([_P, _I64, _P, _I64, _P, _I64, _I64, _I, _P, _I64, _I, _I, _P], _I),
     "kge_score_dot_bwd_q_ws_size": ([_I64, _I64, _I, _I], _I64),
     "kge_score_dot_bwd_q_ws": ([_P, _I64, _P, _I64, _P, _I64, _I64, _I, _P, _I64, _I, _I, _P, _I64, _P], _I),
+    "kge_score_dot_bwd_q_noalloc": ([_P, _I64, _P, _I64, _P, _I64, _I64, _I, _P, _I64, _I, _P], _I),
     "kge_score_dot_bwd_t": ([_P, _I64, _P, _I64, _P, _I64, _I64, _I, _P, _I64, _I, _P], _I),
     "kge_adagrad_step": ([_P, _P, _P, _I64, ctypes.c_float, ctypes.c_float, ctypes.c_float, _I, _P], _I),
     "kge_score_dot_bwd_t_ex": ([_P, _I64, _P, _I64, _P, _I64, _I64, _I, _P, _I64, _I, _I, _P], _I),
@@ -99,7 +100,7 @@ def lib() -> ctypes.CDLL:
 def _check(status: int, what: str):
     if status != 0:
         msg = lib().kge_error_string(status).decode()
-        if status == 1001:
+        if status in (1001, 1004):
             raise ValueError(f"{what}: {msg}")
         raise EngineError(f"{what} failed ({status}): {msg}")
 
@@ -261,6 +262,18 @@ def score_dot_bwd_q(g, t, tidx, precision, dq=None, accumulate=False):
     _check(lib().kge_score_dot_bwd_q_ws(ptr(g), rows(g), ptr(t), rows(t), ptr(tidx), n, m, d, ptr(dq),
                                         rows(dq), int(accumulate), precision, ptr(ws), ws_n, stream()),
            "kge_score_dot_bwd_q")
+    return dq
+
+
+def score_dot_bwd_q_noalloc(g, t, tidx, dq, accumulate=False):
+    """dq (+)= g . t[tidx] (bf16x3) through the entry point that allocates nothing: the split-K
+    partial slabs live in the library's static device scratch (kge_score_dot_bwd_q_noalloc).
+    dq is caller-provided; calls that overlap on one GPU race on the scratch."""
+    tidx = idx64(tidx)
+    n, m = g.shape
+    d = t.shape[1]
+    _check(lib().kge_score_dot_bwd_q_noalloc(ptr(g), rows(g), ptr(t), rows(t), ptr(tidx), n, m, d, ptr(dq),
+                                             rows(dq), int(accumulate), stream()), "kge_score_dot_bwd_q_noalloc")
     return dq
 
 
