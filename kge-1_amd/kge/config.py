@@ -23,6 +23,15 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 _MODEL_DIRS = [os.path.join(_HERE, "model"), os.path.join(_HERE, "model", "embedder")]
 
 
+def _number_or_str(v: str):
+    for conv in (int, float):
+        try:
+            return conv(v)
+        except ValueError:
+            pass
+    return v
+
+
 def _strip_plus(d):
     if isinstance(d, dict):
         return {k: _strip_plus(v) for k, v in d.items() if k != "+++"}
@@ -74,22 +83,45 @@ class Config:
             raise e
 
     def set(self, key: str, value, create: bool = False, overwrite: bool = True, log: bool = False):
+        """Set a dotted key with the reference's checks (config.py:144-236): a key that does
+        not exist yet may only be created with create=True or under a dict that carries
+        "+++" (KeyError otherwise, so a misspelt option is not silently ignored), and a new
+        value must have the type of the value it replaces (ValueError; numeric strings are
+        converted, and an int is accepted where a float is stored)."""
         parts = key.split(".")
         node = self.options
         for i, name in enumerate(parts[:-1]):
-            if name not in node or not isinstance(node[name], dict):
-                if not (create or "+++" in node or i == 0):
-                    raise KeyError(f"{key} not present and create=False")
+            if name in node and isinstance(node[name], dict):
+                create = create or "+++" in node[name]
+            elif name in node and node[name] is not None:
+                raise KeyError(f"Key '{key}' cannot be set because '{'.'.join(parts[:i + 1])}' is not a dictionary")
+            else:
+                if not create:
+                    where = "at root level" if i == 0 else f"under key '{'.'.join(parts[:i])}'"
+                    raise KeyError(f"Key '{key}' cannot be set because key '{'.'.join(parts[:i + 1])}' does not "
+                                   f"exist and no new keys are allowed to be created {where}.")
                 node[name] = {}
             node = node[name]
         last = parts[-1]
-        if last in node:
-            old = node[last]
-            if not overwrite:
-                return old
-            # keep the reference's lenient numeric typing (int -> float ok)
+        old = node.get(last)
+        if old is None:
+            if not create:
+                where = "at root level" if len(parts) == 1 else f"under key '{'.'.join(parts[:-1])}'"
+                raise KeyError(f"Key '{key}' cannot be set because it does not exist and no new keys are "
+                               f"allowed to be created {where}.")
+            if isinstance(value, str):
+                value = _number_or_str(value)
+        else:
+            if isinstance(value, str) and isinstance(old, (int, float)) and not isinstance(old, bool):
+                conv = _number_or_str(value)
+                if not isinstance(conv, str):
+                    value = float(conv) if isinstance(old, float) else conv
             if isinstance(old, float) and isinstance(value, int) and not isinstance(value, bool):
                 value = float(value)
+            if type(value) != type(old):
+                raise ValueError(f"key '{key}' has incorrect type (expected {type(old)}, found {type(value)})")
+            if not overwrite:
+                return old
         node[last] = value
         return value
 

@@ -67,6 +67,13 @@ class EntityRankingJob(EvaluationJob):
         super().__init__(config, dataset, parent_job, model)
         self.tie_handling = config.check(
             "entity_ranking.tie_handling", ["rounded_mean_rank", "best_rank", "worst_rank"])
+        #: additional metrics per slot: "..._head" ranks the subject of (?, p, o), "..._tail" the
+        #: object of (s, p, ?) (eval.py:125-146)
+        self.head_and_tail = config.get("entity_ranking.metrics_per.head_and_tail")
+        for k in ("relation_type", "argument_frequency"):
+            if config.get("entity_ranking.metrics_per." + k):
+                raise NotImplementedError(
+                    f"entity_ranking.metrics_per.{k} (eval.py:149-224) is not implemented; set it to False")
         self.capture_ranks = False  # keep per-query ranks in self.ranks (tests / tracing)
         self.ranks: Dict[str, np.ndarray] = {}
 
@@ -106,6 +113,17 @@ class EntityRankingJob(EvaluationJob):
     # ---------------------------------------------------------------- evaluation
     @torch.no_grad()
     def _run(self) -> dict:
+        """Scores with engine.eval_precision (default fp32: ranks compare near-ties, and
+        the reference ranks fp32 scores) for the whole run, whatever precision training uses."""
+        scorer = self.model.get_scorer()
+        saved = scorer.precision_override
+        scorer.precision_override = self.config.check("engine.eval_precision", list(_lib.PRECISIONS))
+        try:
+            return self._run_ranking()
+        finally:
+            scorer.precision_override = saved
+
+    def _run_ranking(self) -> dict:
         was_training = self.model.training
         self.model.eval()
         E = self.dataset.num_entities()
@@ -113,7 +131,7 @@ class EntityRankingJob(EvaluationJob):
         nrank = len(self.rankings)
         chunk = self.config.get("entity_ranking.chunk_size")
         chunk = E if chunk is None or chunk < 0 else chunk
-        hists = torch.zeros(nrank, E, device=dev)
+        hists_d = torch.zeros(2, nrank, E, device=dev)  # per direction: tail ("o"), head ("s")
         ranks_out = {f"{d}{r}": [] for d in "so" for r in self.rankings}
         epoch_time = -time.time()
         triples = self.triples.to(dev)
@@ -137,16 +155,20 @@ class EntityRankingJob(EvaluationJob):
                 self._count(scores[:, :C], c0, o, o_true, "sp", b0, b1, g["o"], t["o"])
                 self._count(scores[:, C:], c0, s, s_true, "po", b0, b1, g["s"], t["s"])
                 del scores
-            for d in "os":  # every ranking of one direction in one launch
+            for di, d in enumerate("os"):  # every ranking of one direction in one launch
                 rk = torch.empty(nrank * B, dtype=torch.int64, device=dev)
-                _lib.rank_hist_multi(g[d][:nrank * B], t[d][:nrank * B], B, self.tie_handling, rk, hists)
+                _lib.rank_hist_multi(g[d][:nrank * B], t[d][:nrank * B], B, self.tie_handling, rk, hists_d[di])
                 if self.capture_ranks:
                     for ri, r in enumerate(self.rankings):
                         ranks_out[f"{d}{r}"].append(rk[ri * B:(ri + 1) * B])
         epoch_time += time.time()
         metrics = {}
+        hists = hists_d.sum(0)  # counts are small integers: the fp32 sum is exact
         for ri, r in enumerate(self.rankings):
             metrics.update(self._compute_metrics(hists[ri], RANKING_SUFFIX[r]))
+            if self.head_and_tail:  # entity_ranking.py:376-387 (suffix order: ranking, then slot)
+                metrics.update(self._compute_metrics(hists_d[1, ri], RANKING_SUFFIX[r] + "_head"))
+                metrics.update(self._compute_metrics(hists_d[0, ri], RANKING_SUFFIX[r] + "_tail"))
         if self.capture_ranks:
             self.ranks = {k: torch.cat(v).cpu().numpy() if v else np.zeros(0, np.int64)
                           for k, v in ranks_out.items()}

@@ -85,8 +85,12 @@ class TrainingJobNegativeSampling(TrainingJob):
         prepare = -time.time()
         triples = batch["triples"].to(self.device, non_blocking=True)
         bs = len(triples)
-        negs = [self._sampler.sample(triples, slot) if self._sampler.num_samples[slot] > 0 else None
-                for slot in (S, P, O)]
+        if "negative_samples" in batch:  # drawn by the caller (the reference's collate output)
+            negs = [ns.to(self.device).long() if self._sampler.num_samples[slot] > 0 else None
+                    for slot, ns in zip((S, P, O), batch["negative_samples"])]
+        else:
+            negs = [self._sampler.sample(triples, slot) if self._sampler.num_samples[slot] > 0 else None
+                    for slot in (S, P, O)]
         prepare += time.time()
         fwd = bwd = 0.0
         total = torch.zeros((), device=self.device)

@@ -55,6 +55,11 @@ class TrainingJob(Job):
         self.pre_batch_hooks = []
         self.post_batch_trace_hooks = []
         self.post_epoch_trace_hooks = []
+        self.post_epoch_hooks = []
+        self.post_valid_hooks = []
+        self.valid_job = None
+        self.valid_trace = []
+        self.best_state = None
         self.generator = torch.Generator()
         seed = config.get("random_seed.torch")
         if seed >= 0:
@@ -78,11 +83,60 @@ class TrainingJob(Job):
         self.model.prepare_job(self)
 
     def _run(self):
+        """The epoch loop of train.py:136-250: train an epoch, validate every valid.every
+        epochs (EvaluationJob on valid.split sharing this model), step the LR scheduler
+        (metric-based schedulers on the validation metric), stop early when the metric has
+        not improved for valid.early_stopping.patience validations or misses its minimum
+        threshold.  Checkpoint files are outside the scoring path: the best epoch is kept in
+        memory (self.best_state) instead of being written.  Returns the epoch traces."""
+        cfg = self.config
+        metric_name = cfg.get("valid.metric")
+        patience = cfg.get("valid.early_stopping.patience")
         traces = []
-        for _ in range(self.config.get("train.max_epochs")):
+        while True:
+            if self.valid_trace and self.valid_trace[-1]["epoch"] == self.epoch:
+                best = max(range(len(self.valid_trace)), key=lambda i: self.valid_trace[i][metric_name])
+                if best == len(self.valid_trace) - 1:
+                    self.best_state = {k: v.detach().clone() for k, v in self.model.state_dict().items()}
+                if patience > 0 and len(self.valid_trace) > patience and best < len(self.valid_trace) - patience:
+                    cfg.log(f"Stopping early ({metric_name} did not improve over best result in the last "
+                            f"{patience} validation runs).")
+                    break
+                if (self.epoch > cfg.get("valid.early_stopping.min_threshold.epochs")
+                        and self.valid_trace[best][metric_name]
+                        < cfg.get("valid.early_stopping.min_threshold.metric_value")):
+                    cfg.log(f"Stopping early ({metric_name} did not achieve min treshold after {self.epoch} epochs")
+                    break
+            if self.epoch >= cfg.get("train.max_epochs"):
+                break
             self.epoch += 1
-            traces.append(self.run_epoch())
+            trace = self.run_epoch()
+            traces.append(trace)
+            for f in self.post_epoch_hooks:
+                f(self, trace)
+            every = cfg.get("valid.every")
+            if every > 0 and self.epoch % every == 0:
+                vtrace = self._validate()
+                self.valid_trace.append(vtrace)
+                for f in self.post_valid_hooks:
+                    f(self, vtrace)
+                self.kge_lr_scheduler.step(vtrace[metric_name])
+            else:
+                self.kge_lr_scheduler.step()
         return traces
+
+    def _validate(self) -> Dict[str, Any]:
+        """Run the validation job (created on first use, train.py:77-84) on this model."""
+        if self.valid_job is None:
+            from .entity_ranking import EvaluationJob
+
+            valid_conf = self.config.clone()
+            valid_conf.set("job.type", "eval")
+            if self.config.get("valid.split") != "":
+                valid_conf.set("eval.split", self.config.get("valid.split"))
+            self.valid_job = EvaluationJob.create(valid_conf, self.dataset, parent_job=self, model=self.model)
+        self.valid_job.epoch = self.epoch
+        return self.valid_job.run()
 
     def _batches(self):
         perm = torch.randperm(self.num_examples, generator=self.generator)
@@ -141,8 +195,12 @@ class TrainingJob(Job):
             settle(pending)
         epoch_time += time.time()
         trace = dict(type=self.type_str, scope="epoch", epoch=self.epoch, split=self.train_split,
-                     batches=n_batches, size=self.num_examples, avg_loss=sum_loss / max(1, self.num_examples),
-                     avg_penalty=sum_penalty / max(1, n_batches), epoch_time=epoch_time, prepare_time=prep,
+                     batches=n_batches, size=self.num_examples,
+                     lr=[group["lr"] for group in self.optimizer.param_groups],
+                     avg_loss=sum_loss / max(1, self.num_examples),
+                     avg_penalty=sum_penalty / max(1, n_batches),
+                     avg_cost=sum_loss / max(1, self.num_examples) + sum_penalty / max(1, n_batches),
+                     epoch_time=epoch_time, prepare_time=prep,
                      forward_time=fwd, backward_time=bwd, optimizer_time=opt_t, event="epoch_completed")
         for f in self.post_epoch_trace_hooks:
             f(self, trace)
@@ -292,6 +350,7 @@ class TrainingJob1vsAll(TrainingJob):
                 and torch.device(self.device).type == "cuda"
                 and hasattr(opt, "graph_safe") and opt.graph_safe()
                 and self.kge_lr_scheduler._lr_scheduler is None
+                and not self.pre_batch_hooks  # e.g. the embedding normaliser re-creates the weights
                 and self.model._lookup_tables() is not None):
             self._graph_step = _GraphStep(self)
 

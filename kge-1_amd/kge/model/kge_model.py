@@ -61,6 +61,12 @@ class RelationalScorer(KgeBase):
 
     engine_kind: Optional[int] = None
 
+    #: The reference's TransE and RESCAL scorers pass the generic "s_o" result through their
+    #: own ``out.view(p_emb.size(0), -1)`` (transe.py:22-24, rescal.py:51-53): the [n_s, n_p]
+    #: score matrix leaves reinterpreted (not transposed) as [n_p, n_s].  Scorers that set
+    #: this flag reproduce that layout, so callers see what the reference returns.
+    s_o_viewed_by_relation_count = False
+
     def __init__(self, config: Config, dataset, configuration_key: str):
         super().__init__(config, dataset, configuration_key)
 
@@ -68,10 +74,17 @@ class RelationalScorer(KgeBase):
     def l_norm(self) -> float:
         return 1.0
 
+    #: set by a job for the duration of a run to score with another precision than
+    #: engine.precision (EntityRankingJob applies engine.eval_precision this way)
+    precision_override: Optional[str] = None
+
     def precision(self) -> int:
         from .. import _lib
 
-        return _lib.PRECISIONS[self.config.get("engine.precision")]
+        name = self.precision_override or self.config.get("engine.precision")
+        if name not in _lib.PRECISIONS:
+            raise ValueError(f"engine precision {name!r}: expected one of {sorted(_lib.PRECISIONS)}")
+        return _lib.PRECISIONS[name]
 
     def score_emb_spo(self, s_emb: Tensor, p_emb: Tensor, o_emb: Tensor) -> Tensor:
         return self.score_emb(s_emb, p_emb, o_emb, "spo")
@@ -116,6 +129,8 @@ class RelationalScorer(KgeBase):
             n_p = p_emb.size(0)
             out = self.score_emb_spo(s_emb.repeat_interleave(n_p, 0), p_emb.repeat((n, 1)),
                                      o_emb.repeat_interleave(n_p, 0))
+            if self.s_o_viewed_by_relation_count:
+                n = n_p
         else:
             raise ValueError('cannot handle combine="{}".format(combine)')
         return out.view(n, -1)

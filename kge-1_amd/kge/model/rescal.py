@@ -6,6 +6,7 @@ from .kge_model import KgeModel, RelationalScorer
 
 class RescalScorer(RelationalScorer):
     engine_kind = _lib.RESCAL
+    s_o_viewed_by_relation_count = True  # the reference reshapes "s_o" scores this way
 
 
 class Rescal(KgeModel):

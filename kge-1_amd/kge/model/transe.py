@@ -7,6 +7,7 @@ from .kge_model import KgeModel, RelationalScorer
 
 class TransEScorer(RelationalScorer):
     engine_kind = _lib.TRANSE
+    s_o_viewed_by_relation_count = True  # the reference reshapes "s_o" scores this way
 
     def __init__(self, config, dataset, configuration_key=None):
         super().__init__(config, dataset, configuration_key)

@@ -28,7 +28,21 @@ Fixtures written (see tests/golden/README.md for the schema):
   EntityRankingJob, unchunked and with entity_ranking.chunk_size = ceil(E / 8);
 * ``train1vsall_complex.npz`` -- F4: three 1vsAll batches (sp + po, KL/CE, Adagrad)
   with per-batch losses and the final tables;
-* ``shapes.npz`` -- F5: config-derived relation dims (RotatE d/2, RESCAL d^2).
+* ``shapes.npz`` -- F5: config-derived relation dims (RotatE d/2, RESCAL d^2);
+* ``eval_fullsize_normal.npz`` -- F6: the reference EntityRankingJob at the FB15K-237 entity
+  count (E = 14,541, R = 237, ComplEx-512, N(0, 0.1) tables regenerated from a recorded numpy
+  seed -- the 30 MB tables themselves are not stored, a checksum is), 512 evaluation triples
+  filtered against 30,000 training triples, with test filtering;
+* ``train_kvsall_distmult.npz`` -- F7: three KvsAll batches (DistMult, sp_ and _po queries,
+  label smoothing, KL, Adagrad) with the queries / labels of each batch, the per-batch loss
+  the reference reports and the final tables;
+* ``train_ns_<model>.npz`` -- F8: two negative-sampling batches (implementation "triple",
+  KL) with the reference sampler's negatives recorded, so they can be injected;
+* ``train_toy_complex.npz`` -- F9: the options of examples/toy-complex-train.yaml as the
+  BASELINE config words them (1vsAll, dim 128, Adagrad 0.2, ReduceLROnPlateau, lp penalty
+  0.8e-7, N(0, 0.1)) run through the reference's TrainingJob._run on a small synthetic
+  dataset with the batch order recorded: per-epoch loss / penalty / lr and every validation;
+* ``score_so.npz`` -- the "s_o" combine (KgeModel.score_so, all relations and a subset).
 
 Run:  PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden.py [case,case,...]
 """
@@ -257,12 +271,12 @@ def ds_config(model, dim, folder, E, R, extra=None):
     return config
 
 
-def run_eval(config, folder, ent, rel, chunk_size):
+def run_eval(config, folder, ent, rel, chunk_size, batch_size=64):
     from kge.job import EvaluationJob
     from kge.job.eval import hist_all
 
     config.set("entity_ranking.chunk_size", chunk_size)
-    config.set("eval.batch_size", 64)
+    config.set("eval.batch_size", batch_size)
     config.set("eval.split", "valid")
     config.set("entity_ranking.filter_splits", ["train", "valid"])
     config.set("entity_ranking.filter_with_test", True)
@@ -366,6 +380,270 @@ def gen_train_fixture():
     return fn
 
 
+def synth_triples_fast(rng, E, R, n):
+    """Unique random triples, skewed entity distribution, vectorised (large E)."""
+    w = 1.0 / np.arange(1, E + 1) ** 0.6
+    cdf = np.cumsum(w / w.sum())
+    uniq = np.zeros(0, np.int64)
+    while len(uniq) < n:
+        k = int((n - len(uniq)) * 1.3) + 1024
+        s = np.minimum(np.searchsorted(cdf, rng.random(k)), E - 1)
+        o = np.minimum(np.searchsorted(cdf, rng.random(k)), E - 1)
+        p = rng.integers(0, R, k)
+        code = (s * R + p) * E + o
+        allc = np.concatenate([uniq, code])
+        _, first = np.unique(allc, return_index=True)
+        uniq = allc[np.sort(first)]
+    uniq = uniq[:n]
+    o = uniq % E
+    sp = uniq // E
+    return np.stack([sp // R, sp % R, o], 1).astype(np.int64)
+
+
+def seeded_tables(seed, E, R, d_e, d_r, std=0.1):
+    """N(0, std) tables from numpy's PCG64 stream (regenerated, not stored, by the tests)."""
+    rng = np.random.default_rng(seed)
+    ent = (rng.standard_normal((E, d_e), dtype=np.float32) * np.float32(std)).astype(np.float32)
+    rel = (rng.standard_normal((R, d_r), dtype=np.float32) * np.float32(std)).astype(np.float32)
+    return ent, rel
+
+
+def table_checksum(x):
+    return [float(x.astype(np.float64).sum()), float(np.abs(x.astype(np.float64)).sum()),
+            float(x[0, 0]), float(x[-1, -1])]
+
+
+def gen_eval_fullsize():
+    E, R, dim = 14541, 237, 512
+    n_train, n_valid, n_test = 30000, 512, 512
+    rng = np.random.default_rng(3)
+    allt = synth_triples_fast(rng, E, R, n_train + n_valid + n_test)
+    splits = dict(train=allt[:n_train], valid=allt[n_train:n_train + n_valid], test=allt[n_train + n_valid:])
+    folder = os.path.join(TMP, "ds_eval_fullsize")
+    write_dataset(folder, E, R, splits)
+    seed = 2024
+    ent, rel = seeded_tables(seed, E, R, dim, dim)
+    config = ds_config("complex", dim, folder, E, R)
+    ranks, metrics = run_eval(config, folder, torch.from_numpy(ent), torch.from_numpy(rel), -1, batch_size=128)
+    out = {f"tri_{k}": v.astype(np.int32) for k, v in splits.items()}
+    out.update({f"full_{k}": v for k, v in ranks.items()})
+    out["metrics"] = np.array(json.dumps({"full": metrics}))
+    out["meta"] = np.array(json.dumps(dict(
+        E=E, R=R, dim=dim, model="complex", eval_split="valid", filter_splits=["train", "valid"],
+        filter_with_test=True, batch_size=128, tie_handling="rounded_mean_rank", table_seed=seed, std=0.1,
+        ent_checksum=table_checksum(ent), rel_checksum=table_checksum(rel), torch=torch.__version__,
+        numpy=np.__version__)))
+    fn = os.path.join(OUT, "eval_fullsize_normal.npz")
+    np.savez_compressed(fn, **out)
+    return fn
+
+
+def gen_kvsall_fixture():
+    from kge.job import TrainingJob
+
+    E, R, splits = make_dataset_splits()
+    folder = os.path.join(TMP, "ds_kvsall")
+    write_dataset(folder, E, R, splits)
+    dim, bs, nb = 32, 64, 3
+    config = ds_config("distmult", dim, folder, E, R, {
+        "train.type": "KvsAll", "train.optimizer": "Adagrad", "train.optimizer_args": {"lr": 0.2},
+        "train.loss": "kl", "train.batch_size": bs, "KvsAll.label_smoothing": 0.1,
+    })
+    ds = Dataset.create(config, folder=folder)
+    gen = torch.Generator().manual_seed(12)
+    ent = torch.randn(E, dim, generator=gen) * 0.1
+    rel = torch.randn(R, dim, generator=gen) * 0.1
+    job = TrainingJob.create(config, ds)
+    set_tables(job.model, ent, rel)
+    job._prepare()
+    collate = job._get_collate_fun()
+    perm = torch.randperm(job.num_examples, generator=gen)[:nb * bs].tolist()
+    out = dict(ent0=ent.numpy(), rel0=rel.numpy(), tri_train=splits["train"].astype(np.int32))
+    losses = []
+    for b in range(nb):
+        batch = collate(perm[b * bs:(b + 1) * bs])
+        out[f"queries_{b}"] = batch["queries"].numpy()
+        out[f"qtype_{b}"] = batch["query_type_indexes"].numpy()
+        out[f"label_coords_{b}"] = batch["label_coords"].numpy()
+        # tables before the batch and the gradients its backward leaves (before the step)
+        out[f"ent_before_{b}"] = job.model._entity_embedder._embeddings.weight.detach().clone().numpy()
+        out[f"rel_before_{b}"] = job.model._relation_embedder._embeddings.weight.detach().clone().numpy()
+        job.optimizer.zero_grad()
+        res = job._process_batch(b, batch)
+        out[f"g_ent_{b}"] = job.model._entity_embedder._embeddings.weight.grad.detach().clone().numpy()
+        out[f"g_rel_{b}"] = job.model._relation_embedder._embeddings.weight.grad.detach().clone().numpy()
+        job.optimizer.step()
+        losses.append(res.avg_loss)
+    out["losses"] = np.array(losses, dtype=np.float64)
+    out["ent1"] = job.model._entity_embedder._embeddings.weight.detach().numpy()
+    out["rel1"] = job.model._relation_embedder._embeddings.weight.detach().numpy()
+    out["meta"] = np.array(json.dumps(dict(
+        E=E, R=R, dim=dim, model="distmult", lr=0.2, optimizer="Adagrad", loss="kl", batch_size=bs,
+        label_smoothing=0.1, query_types=job.query_types, num_batches=nb, torch=torch.__version__)))
+    fn = os.path.join(OUT, "train_kvsall_distmult.npz")
+    np.savez_compressed(fn, **out)
+    return fn
+
+
+def gen_ns_fixture(model_key):
+    from kge.job import TrainingJob
+
+    E, R, splits = make_dataset_splits()
+    folder = os.path.join(TMP, f"ds_ns_{model_key}")
+    write_dataset(folder, E, R, splits)
+    dim, bs, nb, nneg = 32, 64, 2, 8
+    config = ds_config(model_key, dim, folder, E, R, {
+        "train.type": "negative_sampling", "train.optimizer": "Adagrad", "train.optimizer_args": {"lr": 0.1},
+        "train.loss": "kl", "train.batch_size": bs, "negative_sampling.num_samples.s": nneg,
+        "negative_sampling.num_samples.o": -1, "negative_sampling.num_samples.p": 0,
+        "negative_sampling.implementation": "triple", "negative_sampling.filtering.implementation": "standard",
+    })
+    ds = Dataset.create(config, folder=folder)
+    gen = torch.Generator().manual_seed(13)
+    job = TrainingJob.create(config, ds)
+    d_e, d_r = job.model._entity_embedder.dim, job.model._relation_embedder.dim
+    ent = torch.randn(E, d_e, generator=gen) * 0.1
+    rel = torch.randn(R, d_r, generator=gen) * 0.1
+    if model_key == "rotate":
+        rel = (torch.rand(R, d_r, generator=gen) * 2 - 1) * math.pi
+    set_tables(job.model, ent, rel)
+    job._prepare()
+    collate = job._get_collate_fun()
+    torch.manual_seed(99)  # the reference sampler draws from torch's global stream
+    perm = torch.randperm(job.num_examples, generator=gen)[:nb * bs].tolist()
+    out = dict(ent0=ent.numpy(), rel0=rel.numpy(), tri_train=splits["train"].astype(np.int32))
+    losses = []
+    for b in range(nb):
+        batch = collate(perm[b * bs:(b + 1) * bs])
+        out[f"triples_{b}"] = batch["triples"].numpy()
+        out[f"neg_s_{b}"] = batch["negative_samples"][0].numpy()
+        out[f"neg_o_{b}"] = batch["negative_samples"][2].numpy()
+        # tables before the batch and the gradients its backward leaves (before the step)
+        out[f"ent_before_{b}"] = job.model._entity_embedder._embeddings.weight.detach().clone().numpy()
+        out[f"rel_before_{b}"] = job.model._relation_embedder._embeddings.weight.detach().clone().numpy()
+        job.optimizer.zero_grad()
+        res = job._process_batch(b, batch)
+        out[f"g_ent_{b}"] = job.model._entity_embedder._embeddings.weight.grad.detach().clone().numpy()
+        out[f"g_rel_{b}"] = job.model._relation_embedder._embeddings.weight.grad.detach().clone().numpy()
+        job.optimizer.step()
+        losses.append(res.avg_loss)
+    out["losses"] = np.array(losses, dtype=np.float64)
+    out["ent1"] = job.model._entity_embedder._embeddings.weight.detach().numpy()
+    out["rel1"] = job.model._relation_embedder._embeddings.weight.detach().numpy()
+    out["meta"] = np.array(json.dumps(dict(
+        E=E, R=R, dim=dim, d_e=d_e, d_r=d_r, model=model_key, lr=0.1, optimizer="Adagrad", loss="kl",
+        batch_size=bs, num_negatives=nneg, implementation="triple", num_batches=nb,
+        l_norm=config.get(model_key + ".l_norm") if model_key in ("rotate", "transe") else None,
+        torch=torch.__version__)))
+    fn = os.path.join(OUT, f"train_ns_{model_key}.npz")
+    np.savez_compressed(fn, **out)
+    return fn
+
+
+class _FixedLoader:
+    """Stands in for the reference job's shuffling DataLoader: yields the batches of one
+    recorded permutation per epoch (the reference iterates `self.loader` and calls len())."""
+
+    def __init__(self, triples, perms, batch_size):
+        self.triples, self.perms, self.bs, self.epoch = triples, perms, batch_size, 0
+
+    def __len__(self):
+        return math.ceil(self.perms.shape[1] / self.bs)
+
+    def __iter__(self):
+        perm = self.perms[self.epoch]
+        self.epoch += 1
+        for b in range(0, len(perm), self.bs):
+            yield {"triples": self.triples[perm[b:b + self.bs], :].long()}
+
+
+def gen_toy_fixture():
+    from kge.job import TrainingJob
+
+    E, R, splits = make_dataset_splits(seed=5, E=400, R=10, n_train=2000, n_valid=200, n_test=200)
+    folder = os.path.join(TMP, "ds_toy")
+    write_dataset(folder, E, R, splits)
+    dim, bs, epochs = 128, 100, 6
+    config = ds_config("complex", dim, folder, E, R, {
+        # examples/toy-complex-train.yaml, with train.type / dim as BASELINE configs[0] words them
+        "train.type": "1vsAll", "train.optimizer": "Adagrad", "train.optimizer_args": {"lr": 0.2},
+        "train.lr_scheduler": "ReduceLROnPlateau",
+        "train.lr_scheduler_args": {"mode": "max", "patience": 0, "factor": 0.5},
+        "lookup_embedder.regularize_weight": 0.8e-7,
+        "lookup_embedder.initialize": "normal_",
+        "train.batch_size": bs, "train.max_epochs": epochs, "valid.every": 1,
+        "train.checkpoint.every": 0, "valid.early_stopping.patience": 0,
+    })
+    config.set("lookup_embedder.initialize_args.normal_.mean", 0.0)
+    config.set("lookup_embedder.initialize_args.normal_.std", 0.1)
+    ds = Dataset.create(config, folder=folder)
+    gen = torch.Generator().manual_seed(14)
+    ent = torch.randn(E, dim, generator=gen) * 0.1
+    rel = torch.randn(R, dim, generator=gen) * 0.1
+    job = TrainingJob.create(config, ds)
+    set_tables(job.model, ent, rel)
+    job._prepare()
+    job._is_prepared = True
+    n = job.num_examples
+    perms = np.stack([torch.randperm(n, generator=gen).numpy() for _ in range(epochs)])
+    job.loader = _FixedLoader(ds.split("train"), perms, bs)
+    epoch_traces, valid_traces = [], []
+    job.post_epoch_hooks.append(lambda j, t: epoch_traces.append(dict(t)))
+    job.post_valid_hooks.append(lambda j, t: valid_traces.append(dict(t)))
+    job.run()
+    keep_e = ("epoch", "avg_loss", "avg_penalty", "avg_cost", "lr", "batches", "size")
+    ep = [{k: t[k] for k in keep_e} for t in epoch_traces]
+    va = [{k: v for k, v in t.items() if isinstance(v, (int, float)) and ("rank" in k or "hits" in k or k == "epoch")}
+          for t in valid_traces]
+    fn = os.path.join(OUT, "train_toy_complex.npz")
+    np.savez_compressed(
+        fn, ent0=ent.numpy(), rel0=rel.numpy(), perms=perms.astype(np.int32),
+        **{f"tri_{k}": v.astype(np.int32) for k, v in splits.items()},
+        ent1=job.model._entity_embedder._embeddings.weight.detach().numpy(),
+        rel1=job.model._relation_embedder._embeddings.weight.detach().numpy(),
+        epochs=np.array(json.dumps(ep)), valids=np.array(json.dumps(va)),
+        final_lr=np.array([g["lr"] for g in job.optimizer.param_groups]),
+        meta=np.array(json.dumps(dict(
+            E=E, R=R, dim=dim, model="complex", train_type="1vsAll", lr=0.2, optimizer="Adagrad",
+            lr_scheduler="ReduceLROnPlateau", lr_scheduler_args={"mode": "max", "patience": 0, "factor": 0.5},
+            regularize_weight=0.8e-7, batch_size=bs, max_epochs=epochs, valid_every=1,
+            valid_metric=config.get("valid.metric"), eval_batch_size=config.get("eval.batch_size"),
+            torch=torch.__version__))))
+    return fn
+
+
+def gen_score_so_fixture():
+    out = {}
+    names = []
+    for name, key, dim, extra in [("complex", "complex", 32, {}), ("distmult", "distmult", 32, {}),
+                                  ("transe_l1", "transe", 32, {"transe.l_norm": 1.0}),
+                                  ("rotate_l1", "rotate", 32, {"rotate.l_norm": 1.0})]:
+        E, R, n, m = 40, 9, 12, 5
+        config = make_config(key, dim, E, R, extra)
+        model = KgeModel.create(config, Dataset(config, None))
+        d_e, d_r = model._entity_embedder.dim, model._relation_embedder.dim
+        gen = torch.Generator().manual_seed(31 + len(names))
+        ent = torch.randn(E, d_e, generator=gen) * 0.1
+        rel = torch.randn(R, d_r, generator=gen) * 0.1
+        if key == "rotate":
+            rel = (torch.rand(R, d_r, generator=gen) * 2 - 1) * math.pi
+        set_tables(model, ent, rel)
+        s = torch.randint(0, E, (n,), generator=gen)
+        o = torch.randint(0, E, (n,), generator=gen)
+        psub = torch.randperm(R, generator=gen)[:m]
+        with torch.no_grad():
+            so_all = model.score_so(s, o)
+            so_sub = model.score_so(s, o, psub)
+        for k, v in dict(ent=ent, rel=rel, s=s, o=o, psub=psub, so_all=so_all, so_sub=so_sub).items():
+            out[f"{name}_{k}"] = v.numpy()
+        names.append(dict(name=name, model=key, d_e=d_e, d_r=d_r,
+                          l_norm=extra.get("transe.l_norm", extra.get("rotate.l_norm"))))
+    out["meta"] = np.array(json.dumps(dict(cases=names, torch=torch.__version__)))
+    fn = os.path.join(OUT, "score_so.npz")
+    np.savez_compressed(fn, **out)
+    return fn
+
+
 def gen_shapes():
     rows = []
     for model, d in [("rotate", 64), ("rotate", 1024), ("rescal", 16), ("rescal", 32),
@@ -394,6 +672,12 @@ def main():
             written.append(gen_eval_fixture(regime))
         written.append(gen_train_fixture())
         written.append(gen_shapes())
+    extra = {"eval_fullsize": gen_eval_fullsize, "kvsall": gen_kvsall_fixture,
+             "ns_rotate": lambda: gen_ns_fixture("rotate"), "ns_complex": lambda: gen_ns_fixture("complex"),
+             "toy": gen_toy_fixture, "score_so": gen_score_so_fixture}
+    for name, fn in extra.items():
+        if only is None or name in only:
+            written.append(fn())
     shutil.rmtree(TMP, ignore_errors=True)
     for fn in written:
         print(os.path.relpath(fn, OUT), os.path.getsize(fn))

@@ -148,6 +148,7 @@ def eval_job(f, tag, precision):
     c.set("job.device", "cuda")
     c.set("lookup_embedder.dim", meta["dim"])
     c.set("engine.precision", precision)
+    c.set("engine.eval_precision", precision)
     c.set("eval.batch_size", meta["batch_size"])
     c.set("eval.split", "valid")
     c.set("entity_ranking.chunk_size", -1 if tag == "full" else meta["chunk8"])
@@ -177,16 +178,25 @@ def test_entity_ranking_vs_golden(regime, precision, tag):
 
 
 def test_entity_ranking_bf16x3_normal_near_ties_only():
-    """bf16x3 on real-valued data: a rank may only move where a competitor lies within
-    the 1e-4 score tolerance of the true score."""
+    """bf16x3 scoring on real-valued data: a rank may differ from the reference's only where
+    unfiltered competitors lie within the score tolerance of the true score -- asserted per
+    moved rank against exact (float64) score rows, with |rank change| bounded by the number
+    of such competitors (test_gpu_configs.assert_rank_moves_are_near_ties)."""
+    from test_gpu_configs import assert_rank_moves_are_near_ties
+
     f = np.load(os.path.join(GOLDEN, "eval_normal.npz"))
     ref_metrics = json.loads(str(f["metrics"]))["full"]
     job, trace = eval_job(f, "full", "bf16x3")
-    diff = sum(int((job.ranks[k] != f["full_" + k]).sum()) for k in job.ranks)
-    total = sum(len(v) for v in job.ranks.values())
-    assert diff <= 0.02 * total
+    ref = {k: f["full_" + k] for k in job.ranks}
+    splits = {k: f["tri_" + k].astype(np.int64) for k in ("train", "valid", "test")}
+    moved, worst = assert_rank_moves_are_near_ties(job.ranks, ref, f["ent"], f["rel"], splits["valid"], splits,
+                                                   3e-5, "bf16x3")
+    n_q = 2 * len(splits["valid"])
+    for k, v in ref_metrics.items():
+        if k.startswith("hits_at"):
+            assert abs(trace[k] - v) <= moved / n_q + 1e-7, k
     assert trace["mean_reciprocal_rank_filtered"] == pytest.approx(ref_metrics["mean_reciprocal_rank_filtered"],
-                                                                   rel=1e-3)
+                                                                   rel=1e-3 if moved else 1e-6)
 
 
 @pytest.mark.parametrize("fused", [True, False], ids=["fused_xent", "torch_ce"])

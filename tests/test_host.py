@@ -43,6 +43,30 @@ def test_config_defaults_and_imports():
         c.check("entity_ranking.tie_handling", ["best_rank"])
 
 
+def test_config_set_rejects_unknown_keys_and_wrong_types():
+    """Config.set with the reference's checks (config.py:144-236): a misspelt key raises
+    instead of being stored and ignored; a value of another type raises."""
+    from kge import Config
+
+    c = Config()
+    c.set("model", "complex")
+    c._import("complex")
+    with pytest.raises(KeyError):
+        c.set("trian.batch_size", 64)            # unknown at root level
+    with pytest.raises(KeyError):
+        c.set("train.batchsize", 64)             # unknown under an existing key
+    with pytest.raises(ValueError):
+        c.set("train.batch_size", "many")        # int expected
+    with pytest.raises(ValueError):
+        c.set("engine.fused_loss", 1)            # bool expected
+    assert c.set("train.batch_size", "64") == 64  # numeric strings convert (CLI values)
+    assert c.set("lookup_embedder.regularize_weight", 1) == 1.0  # int accepted for a float
+    c.set("train.optimizer_args.lr", 0.5)        # "+++" dictionaries take new keys
+    c.set("brand_new.key", 3, create=True)
+    assert c.get("train.optimizer_args.lr") == 0.5 and c.get("brand_new.key") == 3
+    assert c.get("engine.eval_precision") == "fp32"
+
+
 def test_model_dims_match_reference_shapes():
     from kge import Config, Dataset, KgeModel
 
@@ -50,6 +74,7 @@ def test_model_dims_match_reference_shapes():
     for model, d, d_e, d_r in rows:
         c = Config()
         c.set("model", model)
+        c._import(model)
         c.set("job.device", "cpu")
         c.set("dataset.num_entities", 10)
         c.set("dataset.num_relations", 3)
@@ -66,6 +91,7 @@ def test_scoring_on_cpu_raises_no_fallback():
 
     c = Config()
     c.set("model", "complex")
+    c._import("complex")
     c.set("job.device", "cpu")
     c.set("dataset.num_entities", 10)
     c.set("dataset.num_relations", 3)
