@@ -62,17 +62,17 @@ const char* kge_error_string(int status);
  * Q[i, :] = prep(model, dir, ent[eidx[i]], rel[ridx[i]])      i in [0, n)
  * eidx / ridx may be NULL (row i is then taken as row i: score_emb on embeddings).
  *   dir = SP: complex cmul(s, r)            complex.py:31-38
- *             distmult s*r                  distmult.py:83
- *             rescal   s^T M_r              rescal.py:145-151
- *             transe   s + r                transe.py:223
- *             rotate   s * rot(r)           rotate.py:288-297
+ *             distmult s*r                  distmult.py:20
+ *             rescal   s^T M_r              rescal.py:37-43
+ *             transe   s + r                transe.py:19
+ *             rotate   s * rot(r)           rotate.py:41-50
  *             cp       s_h * r              cp.py:23  (Q has d_e/2 columns)
  *             simple   [s_t*r_b | s_h*r_f]/2   simple.py:24-26,34
  *   dir = PO: complex conj(r)*o             complex.py:40
- *             distmult o*r                  distmult.py:85
- *             rescal   M_r o                rescal.py:152-157
- *             transe   o - r                transe.py:225
- *             rotate   o * conj(rot(r))     rotate.py:298-307 (|e*rot - o| = |e - o*conj(rot)|)
+ *             distmult o*r                  distmult.py:22
+ *             rescal   M_r o                rescal.py:44-49
+ *             transe   o - r                transe.py:21
+ *             rotate   o * conj(rot(r))     rotate.py:51-60 (|e*rot - o| = |e - o*conj(rot)|)
  *             cp       o_t * r              cp.py:25  (Q has d_e/2 columns)
  *             simple   [o_t*r_f | o_h*r_b]/2   simple.py:28-30,34
  * (x_h / x_t: first / second half of an entity row; r_f / r_b: of a relation row.)
@@ -103,7 +103,7 @@ int kge_prep_query_bwd(int model, int dir, const float* ent, int64_t ld_ent,
 /* ---- all-entities contraction (bilinear models) --------------------------------
  * S[i, j] = sum_k Q[i, k] * T[row(j), k],  row(j) = tidx ? tidx[j] : j
  * i in [0, n), j in [0, m), k in [0, d).  Output leading dim lds.
- * Replaces the mm in complex.py:38,40 / distmult.py:83,85 / rescal.py:150,156.
+ * Replaces the mm in complex.py:38,40 / distmult.py:20,22 / rescal.py:42,48.
  */
 int kge_score_dot(const float* q, int64_t ldq, const float* t, int64_t ldt,
                   const int64_t* tidx, int64_t n, int64_t m, int d, float* s,
@@ -168,7 +168,7 @@ int kge_score_dot_bwd_t_ex(const float* g, int64_t ldg, const float* q, int64_t 
 
 /* ---- all-entities distance scoring (TransE, RotatE; VALU, no MFMA) -------------
  * S[i, j] = sign * dist_kind(Q[i, :], T[row(j), :])
- * Replaces torch.cdist in transe.py:223,225 and the pairwise tensors of rotate.py:288-307.
+ * Replaces torch.cdist in transe.py:19,21 and the pairwise tensors of rotate.py:41-60.
  */
 int kge_score_dist(int kind, float sign, const float* q, int64_t ldq, const float* t,
                    int64_t ldt, const int64_t* tidx, int64_t n, int64_t m, int d,
@@ -183,7 +183,7 @@ int kge_score_dist_bwd(int kind, float sign, const float* g, int64_t ldg,
 /* ---- row-wise triple scores ------------------------------------------------------
  * out[i] = score(ent[sidx[i]], rel[pidx[i]], ent[oidx[i]])      (combine="spo")
  * Replaces KgeModel.score_spo (kge_model.py:620-637) for the five scorers.  TransE uses
- * F.pairwise_distance semantics (|s+p-o+1e-6|, transe.py:221).
+ * F.pairwise_distance semantics (|s+p-o+1e-6|, transe.py:17).
  */
 int kge_score_spo(int model, float l_norm, const float* ent, int64_t ld_ent,
                   const int64_t* sidx, const float* rel, int64_t ld_rel,
@@ -239,7 +239,7 @@ int kge_softmax_grad(const float* s, int64_t lds, int64_t n, int64_t m, int64_t 
  *   ComplEx / DistMult / RESCAL / CP / SimplE: <q, e>   (Q from kge_prep_query, either
  *            direction; for CP, ent / d are the entity-row window of width d_e/2)
  *   TransE : -|| sigma (q - e) + 1e-6 ||_p, sigma = +1 (dir SP: s+p-o') / -1 (dir PO: s'+p-o)
- *            (F.pairwise_distance, transe.py:221)
+ *            (F.pairwise_distance, transe.py:17)
  *   RotatE : sum_k |q_k - e_k|_C (p = 1) or its L2 form; (s o rot(p)) - o' / s' o rot(p) - o
  *            via |s' - o conj(rot(p))| = |s' o rot(p) - o|  (rotate.py:18-50)
  * Replaces the B x (1 + N) triple construction + score_spo of TrainingJobNegativeSampling's

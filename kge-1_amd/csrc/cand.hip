@@ -5,7 +5,7 @@
 //   out[i, c] = score(q_i, ent[cand[i, c]])
 //     dot models : <q_i, e>                                   (q = prep(s, r) / prep(r, o))
 //     TransE     : -|| sigma (q_i - e) + 1e-6 ||_p            (F.pairwise_distance,
-//                  sigma = +1 for sp_ queries (s+p-o'), -1 for _po (s'+p-o), transe.py:221)
+//                  sigma = +1 for sp_ queries (s+p-o'), -1 for _po (s'+p-o), transe.py:17)
 //     RotatE     : + sum_k |q_ik - e_k|_C  (p=1) / sqrt(sum |.|^2) (p=2)   (rotate.py:18-50)
 // Nothing is shared between rows, so the kernel is a gather: one workgroup per query row,
 // the query staged in LDS, each wave streams whole candidate rows (float4 per lane, two

@@ -635,7 +635,8 @@ extern "C" int kge_score_dot_bwd_q_noalloc(const float* g, int64_t ldg, const fl
   return kge_bwd3_q(g, ldg, t, ldt, tidx, n, m, d, dq, lddq, accumulate, ws, need > 0 ? SCRATCH_ELEMS : 0, cus, st);
 }
 
-// Dev-only variants for scripts/tune_bwd.py (not in include/kgescore.h): 0 = dQ as shipped
+#ifdef KGE_DEV_BUILD  // libkgescore_dev.so only
+// Dev-only variants for scripts/dev/tune_bwd.py (not in include/kgescore.h): 0 = dQ as shipped
 // (split-K atomics), 1 = dQ with plain stores (wrong sums: prices the atomics), 2 = dT
 // written (C_MODE 3), 3 = dT read-modify-write (C_MODE 1).
 extern "C" int kge_dev_bwd3(int variant, const float* g, int64_t ldg, const float* x, int64_t ldx, int64_t n,
@@ -650,3 +651,4 @@ extern "C" int kge_dev_bwd3(int variant, const float* g, int64_t ldg, const floa
     default: return KGE_ERR_ARG;
   }
 }
+#endif  // KGE_DEV_BUILD

@@ -74,7 +74,7 @@ __global__ void __launch_bounds__(256) prep_elementwise(const float* __restrict_
         c = rw.r[k];
         s = rw.r[k + h];
       } else {
-        sincosf(rw.r[k], &s, &c);  // rotate.py:273 (radians -> unit complex)
+        sincosf(rw.r[k], &s, &c);  // rotate.py:26 (radians -> unit complex)
       }
       if (DIR == KGE_DIR_SP) {  // a * (c + i s)
         out.put(i, k, a_re * c - a_im * s);
@@ -148,7 +148,7 @@ __global__ void __launch_bounds__(256) prep_elementwise_vec(const float* __restr
         c = *reinterpret_cast<const float4*>(rw.r + k);
         s = *reinterpret_cast<const float4*>(rw.r + k + h);
       } else {
-        const float4 ph = *reinterpret_cast<const float4*>(rw.r + k);  // rotate.py:273
+        const float4 ph = *reinterpret_cast<const float4*>(rw.r + k);  // rotate.py:26
         sincosf(ph.x, &s.x, &c.x);
         sincosf(ph.y, &s.y, &c.y);
         sincosf(ph.z, &s.z, &c.z);

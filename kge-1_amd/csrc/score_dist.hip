@@ -1,8 +1,8 @@
 // All-entities distance scoring for TransE and RotatE: VALU
 // work with no MFMA.  S[i, j] = sign * dist(Q[i], T[row(j)]).
 //
-// The reference materialises the pairwise difference tensor (rotate.py:288-307:
-// n x m x d/2 floats, several times) or goes through torch.cdist (transe.py:223-225).
+// The reference materialises the pairwise difference tensor (rotate.py:41-60:
+// n x m x d/2 floats, several times) or goes through torch.cdist (transe.py:19-21).
 // Here a 64 x 64 output tile is register-blocked 4 x 4 per thread and the K dimension is
 // streamed through LDS in K-major chunks, so nothing pairwise ever leaves registers.
 //   L1      : sum_k |q_k - e_k|
@@ -259,13 +259,16 @@ __global__ void __launch_bounds__(NT) score_dist_bwd_kernel(float sign, const fl
 
 }  // namespace
 
-static int g_dist_impl = 2;  // 2: packed kernel when applicable, 1: this file's kernel (dev A/B)
-
+#ifdef KGE_DEV_BUILD  // libkgescore_dev.so only: A/B switch between the two kernels
+static int g_dist_impl = 2;  // 2: register-tiled kernel when applicable, 1: this file's kernel
 extern "C" int kge_dev_dist_impl(int impl) {
   const int old = g_dist_impl;
   if (impl == 1 || impl == 2) g_dist_impl = impl;
   return old;
 }
+#else
+constexpr int g_dist_impl = 2;
+#endif
 
 extern "C" int kge_score_dist(int kind, float sign, const float* q, int64_t ldq, const float* t, int64_t ldt,
                               const int64_t* tidx, int64_t n, int64_t m, int d, float* s, int64_t lds,
@@ -277,7 +280,7 @@ extern "C" int kge_score_dist(int kind, float sign, const float* q, int64_t ldq,
   if (n == 0 || m == 0) return 0;
   KGE_REQUIRE((n + TM - 1) / TM < 65536);
   hipStream_t st = as_stream(stream);
-  if (g_dist_impl == 2) {  // packed-VALU kernel (score_dist2.hip) when the layout allows
+  if (g_dist_impl == 2) {  // register-tiled kernel (score_dist2.hip) when the layout allows
     const int r = kge_score_dist2(kind, sign, q, ldq, t, ldt, tidx, n, m, d, s, lds, st);
     if (r >= 0) return r;
   }

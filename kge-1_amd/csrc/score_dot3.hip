@@ -352,6 +352,7 @@ extern "C" int kge_score_dot_split(const void* qhi, const void* qlo, int64_t ldq
   return launch_persist16<128, 256, 2, 4>(h, l, ldq, t, ldt, tidx, n, m, d, s, lds, st);
 }
 
+#ifdef KGE_DEV_BUILD  // libkgescore_dev.so only: ablation / probe variants for scripts/dev
 extern "C" int kge_dev_score_dot_persist(int variant, const void* qhi, const void* qlo, int64_t ldq,
                                          const float* t, int64_t ldt, const int64_t* tidx, int64_t n, int64_t m,
                                          int d, float* s, int64_t lds, void* stream) {
@@ -373,3 +374,4 @@ extern "C" int kge_dev_score_dot_persist(int variant, const void* qhi, const voi
     default: return KGE_ERR_ARG;
   }
 }
+#endif  // KGE_DEV_BUILD

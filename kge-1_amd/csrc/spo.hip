@@ -21,7 +21,7 @@ __device__ __forceinline__ Trip rows_of(const float* ent, int64_t ld_ent, const 
 
 // value of the per-element "difference" of the distance models
 __device__ __forceinline__ float transe_diff(float s, float p, float o) {
-  return ((s + p) - o) + 1e-6f;  // F.pairwise_distance: ||x1 - x2 + eps|| (transe.py:221)
+  return ((s + p) - o) + 1e-6f;  // F.pairwise_distance: ||x1 - x2 + eps|| (transe.py:17)
 }
 
 template <int MODEL>

@@ -13,7 +13,9 @@ from typing import Optional
 import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libkgescore.so")
+#: KGE_LIBRARY points development scripts at another build of the same ABI (the dev library
+#: with the kge_dev_* probes, kge-1_amd/csrc `make dev`); unset, the in-tree product library.
+LIB_PATH = os.environ.get("KGE_LIBRARY") or os.path.join(_HERE, "libkgescore.so")
 
 # enums (kgescore.h)
 COMPLEX, DISTMULT, RESCAL, TRANSE, ROTATE, CP, SIMPLE = range(7)

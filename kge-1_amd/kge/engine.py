@@ -50,8 +50,8 @@ def _timed(fn, *args, **kwargs):
 
 
 def dist_kind(kind: int, l_norm: float):
-    """(kernel distance kind, sign) for TransE (-dist, transe.py:220-225) and RotatE
-    (+dist, quirk Q1, rotate.py:275-307)."""
+    """(kernel distance kind, sign) for TransE (-dist, transe.py:16-21) and RotatE
+    (+dist, quirk Q1, rotate.py:28-60)."""
     if l_norm not in (1.0, 2.0):
         raise ValueError(f"l_norm={l_norm} not supported (1 or 2)")
     if kind == L.TRANSE:

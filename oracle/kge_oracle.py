@@ -66,8 +66,8 @@ def prep_sp(model: str, s: np.ndarray, r: np.ndarray) -> np.ndarray:
     complex  -- complex.py:31-38: (s_all * r_all) @ o_all^T with
                s_all=[s_re,s_im,s_re,s_im], r_all=[r_re,r_re,r_im,-r_im],
                o_all=[o_re,o_im,o_im,o_re]  ==  cmul(s, r) . [e_re | e_im].
-    distmult -- distmult.py:83: (s * p) @ o^T.
-    rescal   -- rescal.py:145-151: s^T M_r, M_r = p.view(d, d) (row-major).
+    distmult -- distmult.py:20: (s * p) @ o^T.
+    rescal   -- rescal.py:37-43: s^T M_r, M_r = p.view(d, d) (row-major).
     cp       -- cp.py:23: (s_h * p) @ o_t^T.
     simple   -- simple.py:24-26,34: ((s_h * p_f) @ o_t^T + (s_t * p_b) @ o_h^T) / 2
                == 0.5 [s_t * p_b | s_h * p_f] . [e_h | e_t].
@@ -95,8 +95,8 @@ def prep_po(model: str, r: np.ndarray, o: np.ndarray) -> np.ndarray:
     """Query vector q such that score(e, r, o) = q . e for every entity e.
 
     complex  -- complex.py:40: (r_all * o_all) @ s_all^T == conj(r) * o.
-    distmult -- distmult.py:85: (o * p) @ s^T.
-    rescal   -- rescal.py:152-157: M_r o.
+    distmult -- distmult.py:22: (o * p) @ s^T.
+    rescal   -- rescal.py:44-49: M_r o.
     cp       -- cp.py:25: (o_t * p) @ s_h^T.
     simple   -- simple.py:28-30,34: ((o_t * p_f) @ s_h^T + (o_h * p_b) @ s_t^T) / 2
                == 0.5 [o_t * p_f | o_h * p_b] . [e_h | e_t].
@@ -121,11 +121,11 @@ def prep_po(model: str, r: np.ndarray, o: np.ndarray) -> np.ndarray:
 
 
 def _rot(r):
-    return np.cos(r), np.sin(r)  # rotate.py:273
+    return np.cos(r), np.sin(r)  # rotate.py:26
 
 
 def rotate_q_sp(s, r):
-    """s * rot(r) -- rotate.py:290-292 (hadamard_complex, rotate.py:365-369)."""
+    """s * rot(r) -- rotate.py:43-45 (hadamard_complex, rotate.py:118-122)."""
     s_re, s_im = _halves(s)
     c, si = _rot(r)
     return _cat(s_re * c - s_im * si, s_re * si + s_im * c)
@@ -148,7 +148,7 @@ def score_emb(model: str, s, p, o, combine: str, l_norm: float = 1.0) -> np.ndar
         if combine == "_po":
             return prep_po(model, p, o) @ window(model, "_po", s).T
     elif model == "transe":
-        # transe.py:220-225: spo uses F.pairwise_distance (adds eps to the difference),
+        # transe.py:16-21: spo uses F.pairwise_distance (adds eps to the difference),
         # sp_/_po use torch.cdist (no eps).  Scores are NEGATED distances.
         if combine == "spo":
             return -_lp((s + p) - o + PAIRWISE_EPS, l_norm)
@@ -157,7 +157,7 @@ def score_emb(model: str, s, p, o, combine: str, l_norm: float = 1.0) -> np.ndar
         if combine == "_po":
             return -_lp((o - p)[:, None, :] - s[None, :, :], l_norm)
     elif model == "rotate":
-        # rotate.py:275-307.  Scores are POSITIVE distances (quirk Q1).
+        # rotate.py:28-60.  Scores are POSITIVE distances (quirk Q1).
         if combine == "spo":
             q = rotate_q_sp(s, p)
             d_re, d_im = _halves(q - o)
@@ -170,7 +170,7 @@ def score_emb(model: str, s, p, o, combine: str, l_norm: float = 1.0) -> np.ndar
             d_im = q_im[:, None, :] - o_im[None]
             return _lp(np.sqrt(d_re ** 2 + d_im ** 2), l_norm)
         if combine == "_po":
-            # pairwise_hadamard_complex(s, rot(p)) - o, norm, transpose (rotate.py:298-307)
+            # pairwise_hadamard_complex(s, rot(p)) - o, norm, transpose (rotate.py:51-60)
             s_re, s_im = _halves(s)
             c, si = _rot(p)
             o_re, o_im = _halves(o)
@@ -588,7 +588,7 @@ def train_1vsall(model, ent, rel, batches: Sequence[np.ndarray], lr=0.2, eps=1e-
 
 
 def relation_dim(model: str, d_e: int, d_r: int = -1) -> int:
-    """Config-derived relation dims: rotate.py:329-334 (d/2), rescal.py:187-204 (d^2)."""
+    """Config-derived relation dims: rotate.py:82-87 (d/2), rescal.py:79-96 (d^2)."""
     if d_r >= 0:
         return d_r
     if model == "rotate":

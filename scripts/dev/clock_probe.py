@@ -1,6 +1,7 @@
 """Dev probe: per-workgroup shader clocks vs 100-MHz real-time ticks inside the contraction kernel."""
 import ctypes, sys
-sys.path.insert(0, '.'); sys.path.insert(0, 'kge-1_amd')
+sys.path.insert(0, '.'); sys.path.insert(0, 'kge-1_amd')  # run from the repository root
+import os; os.environ.setdefault('KGE_LIBRARY', 'kge-1_amd/csrc/build_dev/libkgescore_dev.so')  # `make dev`: has the kge_dev_* probes
 import numpy as np, torch
 from kge import _lib as L
 lib = L.lib()

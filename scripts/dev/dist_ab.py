@@ -1,7 +1,8 @@
 """Dev A/B: packed distance kernel (score_dist2.hip) vs the scalar one (score_dist.hip) at
 B=1024, E=14,541, d=512 for TransE L1/L2 and RotatE L1/L2 (interleaved, one process)."""
 import ctypes, sys
-sys.path.insert(0, '.'); sys.path.insert(0, 'kge-1_amd')
+sys.path.insert(0, '.'); sys.path.insert(0, 'kge-1_amd')  # run from the repository root
+import os; os.environ.setdefault('KGE_LIBRARY', 'kge-1_amd/csrc/build_dev/libkgescore_dev.so')  # `make dev`: has the kge_dev_* probes
 import numpy as np, torch
 from kge import _lib as L
 lib = L.lib()

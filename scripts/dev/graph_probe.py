@@ -1,7 +1,7 @@
 """Dev probe: the recorded 1vsAll step (C2 shape) -- replay alone, pinned copy + replay, and
 job.train_step, each 50x without host syncs."""
 import os, sys, time
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, ROOT); sys.path.insert(0, os.path.join(ROOT, "kge-1_amd"))
 import torch
 from kge import Config, Dataset

@@ -9,6 +9,6 @@ cd /tmp
 i=0
 for set in "SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES GRBM_GUI_ACTIVE" "SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES" "SQ_INSTS_VALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS" "SQ_INSTS_MFMA SQ_VALU_MFMA_COEXEC_CYCLES SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS" "SQ_LDS_IDX_ACTIVE SQ_INST_LEVEL_VMEM SQ_ACTIVE_INST_VMEM SQ_VMEM_TA_CMD_FIFO_FULL" "FETCH_SIZE" "WRITE_SIZE" "TCC_HIT_sum TCC_MISS_sum TCC_EA0_RDREQ_sum"; do
   i=$((i+1))
-  timeout -s KILL 60 rocprofv3 --pmc $set --kernel-trace --output-format csv -d $GRAFT_REPO_ROOT/gpurun_out/pmc/p$i -o run -- python3 $GRAFT_REPO_ROOT/scripts/tune_one.py $V > /dev/null 2> $GRAFT_REPO_ROOT/gpurun_out/pmc/err$i.txt || { echo "pass $i failed"; tail -3 $GRAFT_REPO_ROOT/gpurun_out/pmc/err$i.txt; exit 1; }
+  timeout -s KILL 60 rocprofv3 --pmc $set --kernel-trace --output-format csv -d $GRAFT_REPO_ROOT/gpurun_out/pmc/p$i -o run -- python3 $GRAFT_REPO_ROOT/scripts/dev/tune_one.py $V > /dev/null 2> $GRAFT_REPO_ROOT/gpurun_out/pmc/err$i.txt || { echo "pass $i failed"; tail -3 $GRAFT_REPO_ROOT/gpurun_out/pmc/err$i.txt; exit 1; }
 done
 echo done

@@ -1,6 +1,6 @@
 """Dev probe: filtered entity-ranking eval of the synthetic FB15K-237 test split (C2 model)."""
 import os, sys, time, cProfile, pstats
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, ROOT); sys.path.insert(0, os.path.join(ROOT, "kge-1_amd"))
 import torch
 from kge import Config, Dataset, KgeModel

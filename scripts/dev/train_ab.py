@@ -1,7 +1,7 @@
 """Dev A/B: the bench's 1vsAll training step (C2 shape, job.train_step), eager vs recorded
 HIP graph, in one process."""
 import os, sys, time
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, ROOT); sys.path.insert(0, os.path.join(ROOT, "kge-1_amd"))
 import torch
 from kge import Config, Dataset

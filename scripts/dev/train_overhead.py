@@ -1,6 +1,6 @@
 """Dev probe: host (issue) time vs device time of the 1vsAll training step (C2 shape)."""
 import os, sys, time
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, ROOT); sys.path.insert(0, os.path.join(ROOT, "kge-1_amd"))
 import torch
 from kge import Config, Dataset

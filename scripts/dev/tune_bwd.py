@@ -1,7 +1,7 @@
 """Dev sweep of the backward GEMM variants at the stacked C2 shape (2048 queries x 14541
 entities x 512): interleaved rounds in one process (kge_dev_bwd3 / the shipped entries)."""
 import ctypes, sys
-import os as _os; _R = _os.path.dirname(_os.path.dirname(_os.path.abspath(__file__))); sys.path.insert(0, _R); sys.path.insert(0, _os.path.join(_R, 'kge-1_amd'))
+import os as _os; _os.environ.setdefault('KGE_LIBRARY', _os.path.join(_os.path.dirname(_os.path.dirname(_os.path.dirname(_os.path.abspath(__file__)))), 'kge-1_amd', 'csrc', 'build_dev', 'libkgescore_dev.so')); _R = _os.path.dirname(_os.path.dirname(_os.path.dirname(_os.path.abspath(__file__)))); sys.path.insert(0, _R); sys.path.insert(0, _os.path.join(_R, 'kge-1_amd'))
 import numpy as np, torch
 from kge import _lib as L
 lib = L.lib()

@@ -1,6 +1,6 @@
 """Sweep score_dot variants at the C2 shape on one GPU (interleaved rounds, one process)."""
 import ctypes, sys, time
-import os as _os; _R = _os.path.dirname(_os.path.dirname(_os.path.abspath(__file__))); sys.path.insert(0, _R); sys.path.insert(0, _os.path.join(_R, 'kge-1_amd'))
+import os as _os; _os.environ.setdefault('KGE_LIBRARY', _os.path.join(_os.path.dirname(_os.path.dirname(_os.path.dirname(_os.path.abspath(__file__)))), 'kge-1_amd', 'csrc', 'build_dev', 'libkgescore_dev.so')); _R = _os.path.dirname(_os.path.dirname(_os.path.dirname(_os.path.abspath(__file__)))); sys.path.insert(0, _R); sys.path.insert(0, _os.path.join(_R, 'kge-1_amd'))
 import numpy as np, torch
 from kge import _lib as L
 lib = L.lib()

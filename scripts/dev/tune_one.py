@@ -1,7 +1,7 @@
 """Run one contraction variant a few times at the C2 shape (for rocprofv3 PMC passes):
-python scripts/tune_one.py <variant of kge_dev_score_dot_persist>."""
+python scripts/dev/tune_one.py <variant of kge_dev_score_dot_persist>."""
 import ctypes, os, sys
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, ROOT); sys.path.insert(0, os.path.join(ROOT, 'kge-1_amd'))
 import torch
 from kge import _lib as L

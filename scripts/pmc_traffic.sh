@@ -39,4 +39,4 @@ out = {"kernel": name, "dispatches": {k: len(v) for k, v in vals.items()},
 json.dump(out, open(dst, "w"), indent=1)
 print(json.dumps(out))
 EOF
-cp $OUT/pmc_traffic.json $GRAFT_REPO_ROOT/profiles/r01/pmc_traffic.json
+cp $OUT/pmc_traffic.json $GRAFT_REPO_ROOT/profiles/r02/pmc_traffic.json

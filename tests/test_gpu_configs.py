@@ -448,7 +448,7 @@ def test_c3_kvsall_step_at_wn18rr_size_vs_float64():
         loss = torch.nn.functional.kl_div(torch.log_softmax(scores, 1),
                                           torch.nn.functional.normalize(labels, p=1, dim=1), reduction="sum") / 512
         loss.backward()
-        last = float(loss)
+        last = float(loss.detach())
     assert float(res.avg_loss) == pytest.approx(last, rel=1e-5)
     for got, ref, name in ((g_ent, ent.grad, "entity"), (g_rel, rel.grad, "relation")):
         err = float((got - ref).abs().max() / ref.abs().max())

@@ -262,25 +262,23 @@ def test_score_dot_split_multitile(L):
 
 @pytest.mark.parametrize("kind", [0, 1, 2, 3])
 @pytest.mark.parametrize("d", [64, 512, 30])
-def test_score_dist_packed_vs_scalar(L, kind, d):
-    """The packed-VALU distance kernel (score_dist2.hip) against the scalar one
-    (score_dist.hip, selected with kge_dev_dist_impl) and float64; d = 30 (RotatE 15
-    complex components) takes the scalar kernel in both cases (layout fallback)."""
-    import ctypes
-    lib = L.lib()
-    lib.kge_dev_dist_impl.argtypes = [ctypes.c_int]
+def test_score_dist_tiled_and_generic_kernels(L, kind, d):
+    """Both all-entities distance kernels against float64 and against each other: the
+    register-tiled kernel (score_dist2.hip) takes 16-B-aligned rows with a component count
+    that is a multiple of 4; any other layout -- here rows with an odd leading dimension, and
+    d = 30 (RotatE: 15 complex components) -- takes the generic kernel (score_dist.hip)."""
     g = torch.Generator().manual_seed(kind * 100 + d)
     n, m = 100, 501
     q = (torch.randn(n, d, generator=g) * 0.1).cuda()
     t = (torch.randn(m + 7, d, generator=g) * 0.1).cuda()
     sub = torch.randint(0, m + 7, (m,), generator=g).cuda()
-    outs = {}
-    try:
-        for impl in (1, 2):
-            lib.kge_dev_dist_impl(impl)
-            outs[impl] = (L.score_dist(kind, -1.0, q, t, None), L.score_dist(kind, -1.0, q, t, sub))
-    finally:
-        lib.kge_dev_dist_impl(2)
+    # the same values in rows that are only 4-B aligned (leading dimension d + 1)
+    q_odd = torch.zeros(n, d + 1, device="cuda")[:, :d]
+    q_odd.copy_(q)
+    t_odd = torch.zeros(m + 7, d + 1, device="cuda")[:, :d]
+    t_odd.copy_(t)
+    outs = {2: (L.score_dist(kind, -1.0, q, t, None), L.score_dist(kind, -1.0, q, t, sub)),
+            1: (L.score_dist(kind, -1.0, q_odd, t_odd, None), L.score_dist(kind, -1.0, q_odd, t_odd, sub))}
     qq, tt = q.double().cpu(), t.double().cpu()
     if kind < 2:
         diff = qq[:, None, :] - tt[None, :, :]

@@ -21,6 +21,12 @@ def test_library_exports_every_header_symbol():
     for name in declared:
         assert hasattr(lib, name), name
     assert lib.kge_version() >= 100
+    # development probes (kge_dev_*, `make dev`) are not part of the product library
+    import subprocess
+    syms = subprocess.run(["nm", "-D", "--defined-only", _lib.LIB_PATH], capture_output=True, text=True).stdout
+    assert "kge_dev_" not in syms
+    exported = {ln.split()[-1] for ln in syms.splitlines() if " T kge_" in ln}
+    assert exported == declared, exported ^ declared
     assert lib.kge_error_string(1001).decode().startswith("kgescore: invalid argument")
 
 
