@@ -74,6 +74,8 @@ class EntityRankingJob(EvaluationJob):
             if config.get("entity_ranking.metrics_per." + k):
                 raise NotImplementedError(
                     f"entity_ranking.metrics_per.{k} (eval.py:149-224) is not implemented; set it to False")
+        #: compute ops of the row-sharded path; None: the engine (kge.sharded.EngineOps)
+        self.sharded_ops = None
         self.capture_ranks = False  # keep per-query ranks in self.ranks (tests / tracing)
         self.ranks: Dict[str, np.ndarray] = {}
 
@@ -123,12 +125,28 @@ class EntityRankingJob(EvaluationJob):
         finally:
             scorer.precision_override = saved
 
+    def _sharded_scorer(self):
+        """RowShardedScorer over this rank's rows of the model's entity table when the job
+        runs in a torch.distributed world (engine.row_sharded), else None."""
+        from ..sharded import RowShardedScorer, engine_ops_for, shard_bounds, sharding_enabled
+        import torch.distributed as dist
+
+        if not sharding_enabled(self.config):
+            return None
+        world = dist.get_world_size()
+        ent = self.model.get_s_embedder()._embeddings.weight.detach()
+        rel = self.model.get_p_embedder()._embeddings.weight.detach()
+        lo, hi = shard_bounds(ent.shape[0], world, dist.get_rank())
+        ops = self.sharded_ops if self.sharded_ops is not None else engine_ops_for(self.model)
+        return RowShardedScorer(ent[lo:hi], lo, hi, ent.shape[0], rel, ops)
+
     def _run_ranking(self) -> dict:
         was_training = self.model.training
         self.model.eval()
         E = self.dataset.num_entities()
         dev = self.device
         nrank = len(self.rankings)
+        sharded = self._sharded_scorer()
         chunk = self.config.get("entity_ranking.chunk_size")
         chunk = E if chunk is None or chunk < 0 else chunk
         hists_d = torch.zeros(2, nrank, E, device=dev)  # per direction: tail ("o"), head ("s")
@@ -140,6 +158,23 @@ class EntityRankingJob(EvaluationJob):
             b1 = min(N, b0 + self.batch_size)
             B = b1 - b0
             s, p, o = triples[b0:b1, 0], triples[b0:b1, 1], triples[b0:b1, 2]
+            if sharded is not None:
+                # each rank counts over its own rows; one all_reduce of the int64 counts makes
+                # them global (the reference's chunk_size decomposition, entity_ranking.py:153-216)
+                tf = self._t
+                counts = sharded.rank_counts(
+                    s, p, o, (self._f["sp"][0][b0:], self._f["sp"][1]), (self._f["po"][0][b0:], self._f["po"][1]),
+                    (tf["sp"][0][b0:], tf["sp"][1]) if tf is not None else None,
+                    (tf["po"][0][b0:], tf["po"][1]) if tf is not None else None,
+                    p_inverse=(p + self.dataset.num_relations()) if self._two_sided else None)
+                for di, d in enumerate("os"):
+                    rk = torch.empty(nrank * B, dtype=torch.int64, device=dev)
+                    sharded.ops.rank_hist_multi(counts[di, 0, :nrank * B], counts[di, 1, :nrank * B], B,
+                                                self.tie_handling, rk, hists_d[di])
+                    if self.capture_ranks:
+                        for ri, r in enumerate(self.rankings):
+                            ranks_out[f"{d}{r}"].append(rk[ri * B:(ri + 1) * B])
+                continue
             o_true = self.model.score_spo(s, p, o, "o").view(-1).float().contiguous()
             # score_spo(.., "s") is the same triple score unless the model scores the two
             # directions differently (reciprocal relations): skip the second launch then

@@ -135,11 +135,16 @@ class TrainingJob(Job):
             if self.config.get("valid.split") != "":
                 valid_conf.set("eval.split", self.config.get("valid.split"))
             self.valid_job = EvaluationJob.create(valid_conf, self.dataset, parent_job=self, model=self.model)
+            if getattr(self, "sharded_ops", None) is not None:
+                self.valid_job.sharded_ops = self.sharded_ops
         self.valid_job.epoch = self.epoch
         return self.valid_job.run()
 
     def _batches(self):
         perm = torch.randperm(self.num_examples, generator=self.generator)
+        sharded = getattr(self, "_sharded", None)
+        if sharded is not None:  # every rank steps through the same global batches
+            perm = sharded.broadcast(perm)
         for b in range(0, self.num_examples, self.batch_size):
             yield perm[b:b + self.batch_size]
 
@@ -340,10 +345,19 @@ class TrainingJob1vsAll(TrainingJob):
         super().__init__(config, dataset, parent_job, model=model)
         self.type_str = "1vsAll"
         self._graph_step = None
+        self._sharded = None
+        #: compute ops of the row-sharded path; None: the engine (kge.sharded.EngineOps).
+        #: Tests inject CPU ops here to run the exchange logic over gloo.
+        self.sharded_ops = None
 
     def _prepare(self):
         super()._prepare()
         self.num_examples = self.dataset.split(self.train_split).size(0)
+        from ..sharded import sharding_enabled
+
+        if sharding_enabled(self.config):
+            self._sharded = ShardedTraining1vsAll(self)
+            return
         opt = self.optimizer
         if (self.config.get("engine.graph_step") and self.config.get("engine.fused_loss")
                 and isinstance(self.loss, KLDivWithSoftmaxKgeLoss)
@@ -362,6 +376,8 @@ class TrainingJob1vsAll(TrainingJob):
         engine.fused_loss and the kl loss, scoring + cross entropy + its gradient of both
         directions run as one engine op (KgeModel.score_sp_po_xent; per direction with
         score_sp_xent / score_po_xent when the scorer cannot share one contraction)."""
+        if self._sharded is not None:
+            return self._sharded.process_batch(batch)
         t = -time.time()
         triples = batch["triples"].to(self.device, non_blocking=True)
         bs = len(triples)
@@ -397,6 +413,76 @@ class TrainingJob1vsAll(TrainingJob):
         loss_po.backward()
         bwd += time.time()
         return TrainingJob._ProcessBatchResult(loss_sp.detach() + loss_po.detach(), bs, t, fwd, bwd)
+
+
+class ShardedTraining1vsAll:
+    """TrainingJob1vsAll over an entity table row-sharded across the processes of a
+    torch.distributed world (one per GPU; kge.sharded.RowShardedScorer.train_1vsall_global):
+    vocab-parallel softmax cross entropy, no score or gradient matrix on the link.
+
+    Every rank steps through the same global batches (the batch order is broadcast from
+    rank 0) and owns rows [lo, hi) of the entity table: its slice of the model's weight is the
+    live copy (scored, updated by this rank's optimizer, whose Adagrad state covers only
+    these rows); rows outside the slice go stale until ``sync_model`` all-gathers the shards.
+    The relation table is replicated: every rank applies the same all-reduced gradient.  The
+    objective and its gradients equal the unsharded job's (train.py:1032-1062)."""
+
+    def __init__(self, job: "TrainingJob1vsAll"):
+        import torch.distributed as dist
+
+        from ..sharded import RowShardedScorer, engine_ops_for, shard_bounds
+
+        if not isinstance(job.loss, KLDivWithSoftmaxKgeLoss):
+            raise NotImplementedError("row-sharded 1vsAll training supports train.loss kl only")
+        emb = (job.model.get_s_embedder(), job.model.get_p_embedder())
+        if any(getattr(e, "penalty_active", lambda: False)() for e in emb):
+            raise NotImplementedError("row-sharded training does not support embedding penalties")
+        if job.model._lookup_tables() is None and job.sharded_ops is None:
+            raise NotImplementedError("row-sharded training needs plain lookup embedders and an engine scorer")
+        self.job = job
+        self.world, self.rank = dist.get_world_size(), dist.get_rank()
+        ent_w = job.model.get_s_embedder()._embeddings.weight
+        rel_w = job.model.get_p_embedder()._embeddings.weight
+        E = ent_w.shape[0]
+        self.lo, self.hi = shard_bounds(E, self.world, self.rank)
+        # the shard is a view of the model's own table: updates land in the model
+        self.ent_param = torch.nn.Parameter(ent_w.data[self.lo:self.hi])
+        self.rel_param = rel_w
+        ops = job.sharded_ops if job.sharded_ops is not None else engine_ops_for(job.model)
+        self.scorer = RowShardedScorer(self.ent_param.data, self.lo, self.hi, E, rel_w.data, ops)
+        job.optimizer = KgeOptimizer.create(job.config, params=[self.ent_param, self.rel_param])
+        job.kge_lr_scheduler = KgeLRScheduler(job.config, job.optimizer)
+
+    def broadcast(self, cpu_tensor: torch.Tensor) -> torch.Tensor:
+        """rank 0's value of a CPU tensor on every rank (staged through the job's device when
+        the backend moves device memory only)."""
+        import torch.distributed as dist
+
+        if dist.get_backend() == "gloo":
+            t = cpu_tensor.clone()
+            dist.broadcast(t, src=0)
+            return t
+        t = cpu_tensor.to(self.job.device)
+        dist.broadcast(t, src=0)
+        return t.cpu()
+
+    def process_batch(self, batch) -> "TrainingJob._ProcessBatchResult":
+        t = -time.time()
+        triples = batch["triples"].to(self.job.device).long()
+        t += time.time()
+        fwd = -time.time()
+        loss, d_ent, d_rel = self.scorer.train_1vsall_global(triples)
+        fwd += time.time()
+        self.ent_param.grad = d_ent
+        self.rel_param.grad = d_rel
+        return TrainingJob._ProcessBatchResult(loss, len(triples), t, fwd, 0.0)
+
+    def sync_model(self):
+        """All-gather the shards into every rank's full entity table (before unsharded
+        scoring, or to save the model)."""
+        full = self.scorer.all_gather_table()
+        with torch.no_grad():
+            self.job.model.get_s_embedder()._embeddings.weight.copy_(full)
 
 
 class TrainingJobKvsAll(TrainingJob):

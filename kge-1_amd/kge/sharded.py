@@ -85,6 +85,34 @@ class EngineOps:
     def rank_counts(self, s, c0, true_idx, true_score, fp, fc, tp, tc, greater, ties):
         self.L.rank_counts(s, c0, true_idx, true_score, fp, fc, tp, tc, greater, ties)
 
+    def rank_hist_multi(self, greater, ties, rows_per_hist, tie_handling, ranks, hists):
+        self.L.rank_hist_multi(greater, ties, rows_per_hist, tie_handling, ranks, hists)
+
+
+def sharding_enabled(config) -> bool:
+    """Whether jobs run entity-row-sharded: engine.row_sharded "auto" shards whenever a
+    torch.distributed world larger than one process exists (one process per GPU, as torchrun
+    starts them); "on" demands an initialised process group and shards over it whatever its
+    size (a world of one is the degenerate single-shard case); "off" never shards."""
+    mode = config.check("engine.row_sharded", ["auto", "on", "off"])
+    if mode == "off":
+        return False
+    ready = dist.is_available() and dist.is_initialized()
+    if mode == "on":
+        if not ready:
+            raise RuntimeError("engine.row_sharded is 'on' but torch.distributed is not initialised "
+                               "(start one process per GPU with torchrun)")
+        return True
+    return ready and dist.get_world_size() > 1
+
+
+def engine_ops_for(model):
+    """EngineOps of a KgeModel's scorer (its engine kernel kind, precision and norm)."""
+    scorer = model.get_scorer()
+    if scorer.engine_kind is None:
+        raise NotImplementedError(f"{type(scorer).__name__} has no engine kernels: row sharding is not available")
+    return EngineOps(scorer.engine_kind, scorer.precision(), scorer.l_norm())
+
 
 def shard_bounds(num_entities: int, world: int, rank: int):
     per = math.ceil(num_entities / world)
@@ -192,9 +220,16 @@ class RowShardedScorer:
           -> dQ = sum_k G_k E_k (all_reduce, W*B x d) ; dE_k = G_k^T Q stays local
           -> prep backward for the queries this rank owns.
         The relation gradient is all_reduced once (each query's at its owner).
-        Returns (loss, d_ent for this rank's shard, d_rel) -- identical loss on every rank."""
+        Returns (loss as a float, d_ent for this rank's shard, d_rel) -- identical loss on
+        every rank."""
         tr = torch.stack([s, p, o], 1)
-        tr_all = self._all_gather_1d(tr.reshape(-1)).view(-1, 3)
+        loss, d_ent, d_rel = self.train_1vsall_global(self._all_gather_1d(tr.reshape(-1)).view(-1, 3))
+        return float(loss), d_ent, d_rel
+
+    def train_1vsall_global(self, tr_all: torch.Tensor):
+        """train_1vsall_grads for a global batch [n, 3] that every rank already holds
+        identically (the index batch is tiny, so a job hands every rank the whole batch
+        instead of gathering slices): no triple exchange, everything else as above."""
         n = tr_all.shape[0]
         scale = 1.0 / n
         E_k = self.hi - self.lo
@@ -224,23 +259,40 @@ class RowShardedScorer:
             dq = torch.where(owned[:, None], dq, torch.zeros_like(dq))
             self.ops.prep_bwd(direction, self.ent, local, self.rel, p_all, dq, d_ent, d_rel)
         dist.all_reduce(d_rel, group=self.group)
-        return float(loss), d_ent, d_rel
+        return loss, d_ent, d_rel  # loss: a 0-dim float64 tensor on the table's device (no host sync)
 
     # ---------------------------------------------------------------- eval
-    def rank_counts(self, s, p, o, f_sp, f_po, t_sp=None, t_po=None):
+    def rank_counts(self, s, p, o, f_sp, f_po, t_sp=None, t_po=None, p_inverse=None):
         """Global greater/tie counts of the true o (sp_) and s (_po) for a batch that
         every rank holds identically (s, p, o [B]); CSR filter lists as in
-        EntityRankingJob.  Returns greater/ties [2 directions, 3 rankings, B] summed over
-        shards with one all_reduce."""
+        EntityRankingJob.  Returns greater/ties [2 directions, 2 (greater, ties), 3 rankings x B]
+        summed over shards with one all_reduce.  p_inverse: the relation ids p + R of a
+        reciprocal-relations model, whose (?, p, o) side is scored as (o, p + R, ?) -- both
+        its queries and its true score (reciprocal_relations_model.py:57-74)."""
         B = s.numel()
         rows = self.gather_rows(torch.cat([s, o]))  # full s rows then o rows, on every rank
         ar = torch.arange(B, device=s.device)
-        true = self.ops.spo(rows[:B], self.rel, p, rows[B:])
+        true_o = self.ops.spo(rows[:B], self.rel, p, rows[B:])
+        if p_inverse is None:
+            sides = ((ar, 0, p, o, true_o, f_sp, t_sp), (ar + B, 1, p, s, true_o, f_po, t_po))
+        else:
+            true_s = self.ops.spo(rows[B:], self.rel, p_inverse, rows[:B])
+            sides = ((ar, 0, p, o, true_o, f_sp, t_sp), (ar + B, 0, p_inverse, s, true_s, f_po, t_po))
         counts = torch.zeros(2, 2, 3 * B, dtype=torch.int64, device=s.device)
-        for di, (eidx, direction, tgt, f, t) in enumerate(((ar, 0, o, f_sp, t_sp), (ar + B, 1, s, f_po, t_po))):
-            q = self.ops.prep(direction, rows, eidx, self.rel, p)
+        for di, (eidx, direction, rel_ids, tgt, true, f, t) in enumerate(sides):
+            q = self.ops.prep(direction, rows, eidx, self.rel, rel_ids)
             sc = self.ops.score(q, self._win(direction, self.ent))
             self.ops.rank_counts(sc, self.lo, tgt, true, f[0], f[1], t[0] if t is not None else None,
                                  t[1] if t is not None else None, counts[di, 0], counts[di, 1])
         dist.all_reduce(counts, group=self.group)
         return counts
+
+    def all_gather_table(self) -> torch.Tensor:
+        """The full [E, d] entity table assembled from every rank's shard (checkpoints, or
+        handing a sharded-trained model to unsharded code)."""
+        per = math.ceil(self.E / self.world)
+        mine = torch.zeros(per, self.ent.shape[1], dtype=self.ent.dtype, device=self.ent.device)
+        mine[:self.hi - self.lo] = self.ent
+        parts = [torch.empty_like(mine) for _ in range(self.world)]
+        dist.all_gather(parts, mine, group=self.group)
+        return torch.cat(parts)[:self.E]

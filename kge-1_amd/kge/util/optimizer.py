@@ -73,9 +73,12 @@ class FusedAdagrad(torch.optim.Adagrad):
 
 class KgeOptimizer:
     @staticmethod
-    def create(config, model):
+    def create(config, model=None, params=None):
+        """The optimizer of train.optimizer over a model's trainable parameters, or over an
+        explicit parameter list (a row-sharded job steps its shard of the entity table)."""
         name = config.get("train.optimizer")
-        params = [p for p in model.parameters() if p.requires_grad]
+        if params is None:
+            params = [p for p in model.parameters() if p.requires_grad]
         args = config.get("train.optimizer_args")
         if name == "Adagrad" and config.get("engine.fused_optimizer"):
             return FusedAdagrad(params, **args)

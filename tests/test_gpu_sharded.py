@@ -86,3 +86,56 @@ def test_train_1vsall_grads_world1_matches_fused(L, prec):
         assert (d_rel - rel.grad).abs().max() <= tol * rel.grad.abs().max()
     finally:
         dist.destroy_process_group()
+
+
+def test_sharded_jobs_world1_rccl_match_unsharded_jobs(L):
+    """TrainingJob1vsAll and EntityRankingJob with engine.row_sharded on, over an RCCL world
+    of one process (the degenerate single shard, EngineOps = the HIP kernels): the same loss
+    trajectory, tables and ranks as the unsharded jobs from the same start."""
+    from kge import Config, Dataset
+    from kge.job import EntityRankingJob, TrainingJob
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()))
+    dist.init_process_group("nccl", rank=0, world_size=1)
+    try:
+        runs = {}
+        for mode in ("off", "on"):
+            c = Config()
+            c.set("model", "complex")
+            c._import("complex")
+            c.set("job.device", "cuda")
+            c.set("verbose", False)
+            c.set("lookup_embedder.dim", 64)
+            c.set("lookup_embedder.initialize_args", {"mean": 0.0, "std": 0.1})
+            c.set("train.type", "1vsAll")
+            c.set("train.batch_size", 256)
+            c.set("train.max_epochs", 2)
+            c.set("train.optimizer_args", {"lr": 0.1})
+            c.set("valid.every", 0)
+            c.set("eval.batch_size", 100)
+            c.set("random_seed.torch", 3)
+            c.set("engine.precision", "fp32")
+            c.set("engine.graph_step", False)
+            c.set("engine.row_sharded", mode)
+            ds = Dataset.synthetic(c, "toy", seed=1, num_entities=700, num_relations=9, sizes=(2000, 150, 150))
+            torch.manual_seed(11)
+            job = TrainingJob.create(c, ds)
+            traces = job.run()
+            assert (job._sharded is not None) == (mode == "on")
+            ev = EntityRankingJob(c, ds, model=job.model)
+            ev.capture_ranks = True
+            et = ev.run()
+            runs[mode] = ([t["avg_loss"] for t in traces],
+                          job.model._entity_embedder._embeddings.weight.detach().cpu().numpy(),
+                          job.model._relation_embedder._embeddings.weight.detach().cpu().numpy(), ev.ranks,
+                          et["mean_reciprocal_rank_filtered_with_test"])
+        np.testing.assert_allclose(runs["on"][0], runs["off"][0], rtol=1e-5)
+        for i in (1, 2):  # tables after 16 Adagrad steps: all but a handful of ill-conditioned elements
+            diff = np.abs(runs["on"][i] - runs["off"][i])
+            assert int((diff > 1e-4).sum()) <= max(4, 1e-3 * diff.size) and float(diff.mean()) < 1e-5
+        same = sum(int((runs["on"][3][k] == runs["off"][3][k]).sum()) for k in runs["on"][3])
+        total = sum(len(v) for v in runs["on"][3].values())
+        assert same >= 0.99 * total  # two fp32 trajectories: a rare near-tie may sit on another side
+        assert runs["on"][4] == pytest.approx(runs["off"][4], rel=1e-2)
+    finally:
+        dist.destroy_process_group()

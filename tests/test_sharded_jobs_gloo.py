@@ -1,0 +1,249 @@
+"""World-size-2 gloo test (CPU) of the JOBS over a row-sharded entity table:
+TrainingJob1vsAll (engine.row_sharded: vocab-parallel 1vsAll through
+RowShardedScorer.train_1vsall_global, Adagrad state on each rank's rows, validation after
+every epoch) and EntityRankingJob (per-shard rank counts, one all_reduce).
+
+The jobs, the exchange logic and the optimizer wiring are the product code; only the per-shard
+compute is injected (torch / numpy CPU ops restating the engine kernels), as this container
+has no GPU.  Compared with the UNSHARDED objective computed independently here: torch
+autograd of  sum_dir CE(Q E^T, target) / B  with torch.optim.Adagrad over the same batches
+(train.py:1032-1062), and the CPU oracle's entity ranking (entity_ranking.py:79-577)."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from oracle import kge_oracle as K
+from test_sharded_gloo import OracleOps
+from test_sharded_train_gloo import TorchOps, _prep
+
+E, R, D, BS, EPOCHS, SEED = 41, 4, 8, 16, 2, 5
+
+
+class JobOps(TorchOps):
+    """TorchOps (training) + float64 eval ops."""
+
+    def score(self, q, tab, out=None):
+        s = (q.double() @ tab.double().T).float()
+        if out is not None:
+            out.copy_(s)
+            return out
+        return s
+
+    spo = OracleOps.spo
+    rank_counts = OracleOps.rank_counts
+
+    def rank_hist_multi(self, greater, ties, rows_per_hist, tie_handling, ranks, hists):
+        assert tie_handling == "rounded_mean_rank"
+        r = greater + ties // 2
+        ranks.copy_(r)
+        for h in range(hists.shape[0]):
+            part = r[h * rows_per_hist:(h + 1) * rows_per_hist]
+            hists[h] += torch.bincount(part, minlength=hists.shape[1]).float()
+
+
+def _splits():
+    rng = np.random.default_rng(1)
+    seen, out = set(), []
+    while len(out) < 120:
+        t = (int(rng.integers(E)), int(rng.integers(R)), int(rng.integers(E)))
+        if t not in seen:
+            seen.add(t)
+            out.append(t)
+    t = np.array(out, dtype=np.int64)
+    return {"train": t[:80], "valid": t[80:100], "test": t[100:]}
+
+
+def _tables():
+    g = torch.Generator().manual_seed(3)
+    return torch.randn(E, D, generator=g) * 0.5, torch.randn(R, D, generator=g) * 0.5
+
+
+def _config():
+    from kge import Config
+
+    c = Config()
+    c.set("model", "complex")
+    c._import("complex")
+    c.set("job.device", "cpu")
+    c.set("verbose", False)
+    c.set("dataset.num_entities", E)
+    c.set("dataset.num_relations", R)
+    c.set("lookup_embedder.dim", D)
+    c.set("train.type", "1vsAll")
+    c.set("train.batch_size", BS)
+    c.set("train.max_epochs", EPOCHS)
+    c.set("train.optimizer", "Adagrad")
+    c.set("train.optimizer_args", {"lr": 0.1})
+    c.set("valid.every", 1)
+    c.set("valid.early_stopping.patience", 0)
+    c.set("eval.batch_size", 7)
+    c.set("random_seed.torch", SEED)
+    return c
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank, world, port, out_q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from kge import Dataset
+        from kge.job import EntityRankingJob, TrainingJob
+
+        c = _config()
+        ds = Dataset(c, None)
+        ds._triples = {k: torch.from_numpy(v.astype(np.int32)) for k, v in _splits().items()}
+        job = TrainingJob.create(c, ds)
+        ent0, rel0 = _tables()
+        with torch.no_grad():
+            job.model._entity_embedder._embeddings.weight.copy_(ent0)
+            job.model._relation_embedder._embeddings.weight.copy_(rel0)
+        job.sharded_ops = JobOps()
+        traces = job.run()
+        assert job._sharded is not None and job._sharded.world == world
+        lo, hi = job._sharded.lo, job._sharded.hi
+        state_rows = [tuple(st["sum"].shape) for st in job.optimizer.state.values()]
+        job._sharded.sync_model()
+        ev = EntityRankingJob(c, ds, model=job.model)
+        ev.sharded_ops = JobOps()
+        ev.capture_ranks = True
+        etrace = ev.run()
+        out_q.put((rank, lo, hi, [t["avg_loss"] for t in traces],
+                   [v["mean_reciprocal_rank_filtered_with_test"] for v in job.valid_trace], state_rows,
+                   job.model._entity_embedder._embeddings.weight.detach().numpy().copy(),
+                   job.model._relation_embedder._embeddings.weight.detach().numpy().copy(),
+                   {k: v.copy() for k, v in ev.ranks.items()},
+                   {k: v for k, v in etrace.items() if isinstance(v, float)}))
+    finally:
+        dist.destroy_process_group()
+
+
+def _unsharded_reference():
+    """The same training run without any sharding, by torch autograd."""
+    splits = _splits()
+    ent0, rel0 = _tables()
+    ent = ent0.clone().requires_grad_(True)
+    rel = rel0.clone().requires_grad_(True)
+    opt = torch.optim.Adagrad([ent, rel], lr=0.1)
+    gen = torch.Generator().manual_seed(SEED)
+    train = torch.from_numpy(splits["train"])
+    losses, valid_mrr = [], []
+    for _ in range(EPOCHS):
+        perm = torch.randperm(len(train), generator=gen)
+        tot = 0.0
+        for b in range(0, len(train), BS):
+            tr = train[perm[b:b + BS]]
+            opt.zero_grad()
+            loss = 0.0
+            for direction, e_col, lab_col in ((0, 0, 2), (1, 2, 0)):
+                q = _prep(direction, ent, tr[:, e_col], rel, tr[:, 1])
+                loss = loss + torch.nn.functional.cross_entropy(q @ ent.T, tr[:, lab_col], reduction="sum") / len(tr)
+            loss.backward()
+            opt.step()
+            tot += float(loss.detach()) * len(tr)
+        losses.append(tot / len(train))
+        _, m = K.entity_ranking("complex", ent.detach().double().numpy(), rel.detach().double().numpy(), splits,
+                                eval_split="valid", filter_splits=("train", "valid"), batch_size=7)
+        valid_mrr.append(m["mean_reciprocal_rank_filtered_with_test"])
+    return losses, valid_mrr, ent.detach().numpy(), rel.detach().numpy()
+
+
+def test_sharded_training_and_eval_jobs_world2_match_unsharded():
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for pr in procs:
+        pr.start()
+    res = sorted([q.get(timeout=240) for _ in range(world)], key=lambda x: x[0])
+    for pr in procs:
+        pr.join(timeout=60)
+        assert pr.exitcode == 0
+    ref_losses, ref_mrr, ref_ent, ref_rel = _unsharded_reference()
+    splits = _splits()
+    per = -(-E // world)
+    for rank, lo, hi, losses, mrr, state_rows, ent, rel, ranks, metrics in res:
+        assert (lo, hi) == (rank * per, min(E, (rank + 1) * per))
+        # the optimizer state covers this rank's rows only (and the replicated relation table)
+        assert sorted(state_rows) == sorted([(hi - lo, D), (R, D)])
+        np.testing.assert_allclose(losses, ref_losses, rtol=1e-5)
+        np.testing.assert_allclose(mrr, ref_mrr, rtol=1e-5)
+        # after sync_model every rank holds the whole trained table
+        np.testing.assert_allclose(ent, ref_ent, atol=2e-5)
+        np.testing.assert_allclose(rel, ref_rel, atol=2e-5)
+    # the sharded evaluation job on the trained model vs the oracle on the same tables
+    oranks, ometrics = K.entity_ranking("complex", res[0][6].astype(np.float64), res[0][7].astype(np.float64),
+                                        splits, eval_split="valid", filter_splits=("train", "valid"), batch_size=7)
+    for rank, *_, ranks, metrics in res:
+        assert set(ranks) == set(oranks)
+        for k, v in oranks.items():
+            np.testing.assert_array_equal(ranks[k], v, err_msg=k)
+        for k, v in ometrics.items():
+            assert metrics[k] == pytest.approx(v, rel=1e-5, abs=1e-9), k
+
+
+def _worker_reciprocal(rank, world, port, out_q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from kge.sharded import RowShardedScorer, shard_bounds
+
+        g = torch.Generator().manual_seed(0)
+        ent = torch.randn(E, D, generator=g)
+        rel = torch.randn(2 * R, D, generator=g)  # reciprocal model: relations r and r + R
+        lo, hi = shard_bounds(E, world, rank)
+        sc = RowShardedScorer(ent[lo:hi].clone(), lo, hi, E, rel, OracleOps())
+        ge = torch.Generator().manual_seed(7)
+        B = 9
+        es, ep, eo = (torch.randint(0, n, (B,), generator=ge) for n in (E, R, E))
+        f_ptr = torch.arange(0, 2 * B + 1, 2)
+        f_col = torch.randint(0, E, (2 * B,), generator=ge)
+        counts = sc.rank_counts(es, ep, eo, (f_ptr, f_col), (f_ptr, f_col), p_inverse=ep + R)
+        out_q.put((rank, counts.numpy(), [x.numpy() for x in (es, ep, eo, f_ptr, f_col)]))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_sharded_rank_counts_reciprocal_relations_world2():
+    """The (?, p, o) side of a reciprocal-relations model is the sp_ score of (o, p + R, ?),
+    queries and true score alike (reciprocal_relations_model.py:57-74): sharded counts vs
+    the unsharded computation."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_reciprocal, args=(r, world, port, q)) for r in range(world)]
+    for pr in procs:
+        pr.start()
+    res = sorted([q.get(timeout=120) for _ in range(world)], key=lambda x: x[0])
+    for pr in procs:
+        pr.join(timeout=60)
+        assert pr.exitcode == 0
+    g = torch.Generator().manual_seed(0)
+    ent = torch.randn(E, D, generator=g)
+    rel = torch.randn(2 * R, D, generator=g)
+    es, ep, eo, f_ptr, f_col = (torch.from_numpy(x) for x in res[0][2])
+    B = len(es)
+    ops = OracleOps()
+    ref = np.zeros((2, 2, 3 * B), np.int64)
+    sides = ((es, ep, eo, ops.spo(ent[es], rel, ep, ent[eo])), (eo, ep + R, es, ops.spo(ent[eo], rel, ep + R, ent[es])))
+    for di, (e_idx, rel_ids, tgt, true) in enumerate(sides):
+        scores = ops.score(ops.prep(0, ent, e_idx, rel, rel_ids), ent)
+        gr = torch.zeros(3 * B, dtype=torch.int64)
+        ti = torch.zeros(3 * B, dtype=torch.int64)
+        ops.rank_counts(scores, 0, tgt, true, f_ptr, f_col, None, None, gr, ti)
+        ref[di, 0], ref[di, 1] = gr.numpy(), ti.numpy()
+    for _, counts, _ in res:
+        np.testing.assert_array_equal(counts[:, :, :2 * B], ref[:, :, :2 * B])
+    # and the two sides really differ (an undirected true score would be wrong here)
+    assert not np.array_equal(ref[0], ref[1])
