@@ -1,29 +1,35 @@
 #!/usr/bin/env python
 """Headline benchmark: 1vsAll scoring throughput, ComplEx-512 on FB15K-237 (synthetic,
-published shape), batch 1024 -- BASELINE.json configs[1] at N=1.
+published shape), batch 1024 -- BASELINE.json configs[1].
 
-A step is one pass of the hot path over one batch of 1024 fresh (s, p) queries:
+A step is one pass of the hot path over one batch of 1024 fresh (s, p) queries per GPU:
 KgeModel.score_sp(s, p) -> fused LookupEmbedder gather + ComplEx query prep + the
-all-entities contraction against the 14,541-row entity table (libkgescore, gfx950).
+all-entities contraction against the entity table (libkgescore, gfx950).
 value = scored triples / s = (queries x entities) / step time, all ranks.
 
-N > 1 (torchrun, one process per GPU): the scored triples are partitioned by query -- every
-rank scores its own 1024 queries against the entity table, replicated at setup -- so the
-step has no data-path collective and per-GPU work is constant (weak scaling).  The
-entity-row-sharded exchange over RCCL (kge.sharded: query rows all_gathered, global batch
-scored against each rank's shard) is timed after the headline loop and reported as
-"row_sharded", together with the cost of its all_gather alone.
+N = 1: the whole 14,541-row table on the one GPU.
 
-Also reported (rank 0): the contraction kernel's roofline from HIP events on the launch stream
-(100 back-to-back launches after the timed region), score_po, a full 1vsAll training step
-(sp + po forward/backward + CE + Adagrad), the filtered eval MRR on the synthetic test
-split, and the reference CPU path (oracle/refseq.py: the reference's exact ATen op
-sequence, verified bit-exact against it) timed on this host's cores.
+N > 1 (torchrun, one process per GPU): the entity table is ROW-SHARDED over the ranks
+(kge.sharded.RowShardedScorer, RCCL over xGMI): every rank contributes its own 1024 queries
+(subjects it owns), prepares their query rows, the rows are all-gathered (W x 1024 x 512 fp32),
+and every rank scores the global batch against its E / W rows -- per-GPU work is constant
+(weak scaling), W x 1024 x 14,541 triples are scored per step.  The exchange of batch i + 1 is
+issued asynchronously while batch i is scored (a loader knows the next batch), the figure
+without that overlap and the replicated-table data-parallel figure (no collective at all)
+are reported next to it, and so is the same step at the Wikidata5M shape (configs[4]).
+
+Also reported (rank 0, N = 1): the contraction kernel's roofline from HIP events on the launch
+stream (bf16x3 production kernel and the exact-fp32 kernel), score_po, a full 1vsAll training
+step, filtered entity ranking, the other BASELINE configs' training steps, and the reference
+CPU path (oracle/refseq.py: the reference's exact ATen op sequence, pinned bit-exact / rank
+for rank against reference-captured fixtures) timed on this host's cores: score_sp, the
+1vsAll training step at both initialisations, and filtered entity ranking with its MRR
+beside the GPU job's MRR on the same tables and triples.
 """
 import argparse
 import json
-import math
 import os
+import platform
 import sys
 import time
 
@@ -38,6 +44,7 @@ import torch.distributed as dist  # noqa: E402
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
 BF16_DENSE_TFLOPS = 2500.0  # dense bf16 MFMA (spec, no sparsity)
 FP32_MFMA_TFLOPS = 157.3
+PROFILE_ROUND = "r02"
 
 
 def parse():
@@ -49,10 +56,11 @@ def parse():
     ap.add_argument("--dim", type=int, default=512)
     ap.add_argument("--dataset", default="fb15k-237")
     ap.add_argument("--precision", default="bf16x3", choices=["bf16x3", "fp32"])
-    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--cpu-seconds", type=float, default=8.0)
     ap.add_argument("--no-extras", action="store_true")
     ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--c5", action="store_true", help="also time one rank's Wikidata5M shard (configs[4])")
+    ap.add_argument("--c5", action="store_true", help="N = 1: also time one rank's Wikidata5M shard (configs[4])")
+    ap.add_argument("--no-c5", action="store_true", help="N > 1: skip the row-sharded Wikidata5M step")
     return ap.parse_args()
 
 
@@ -67,6 +75,7 @@ def make_config(args, device):
     c.set("lookup_embedder.initialize", "normal_")
     c.set("lookup_embedder.initialize_args", {"mean": 0.0, "std": 0.1})  # examples/toy-complex-train.yaml
     c.set("engine.precision", args.precision)
+    c.set("engine.row_sharded", "off")  # the bench builds its sharded scorer itself
     c.set("verbose", False)
     return c
 
@@ -86,29 +95,142 @@ def timed_loop(fn, steps, warmup, world):
     return (time.perf_counter() - t0) / steps
 
 
-def cpu_baseline(args, E, R, seconds):
-    """Reference CPU path: refseq replica of KgeModel.score_sp (ComplEx) on host cores."""
+def max_over_ranks(values, device, world):
+    if world <= 1:
+        return [float(v) for v in values]
+    from kge.sharded import all_reduce
+
+    t = torch.tensor(values, device=device, dtype=torch.float64)
+    all_reduce(t, op=dist.ReduceOp.MAX)
+    return [float(v) for v in t]
+
+
+def kernel_time_ms(kern, reps=100, settle=20):
+    """Average duration of back-to-back launches between two HIP events on the launch stream
+    (torch's current stream is the stream the kernel is launched on)."""
+    for _ in range(settle):  # the clock settles under sustained MFMA load
+        kern()
+    a = torch.cuda.Event(enable_timing=True)
+    b = torch.cuda.Event(enable_timing=True)
+    a.record()
+    for _ in range(reps):
+        kern()
+    b.record()
+    torch.cuda.synchronize()
+    return a.elapsed_time(b) / reps
+
+
+# --------------------------------------------------------------------------------- CPU baseline
+
+
+def host_info():
+    model = "unknown"
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    try:
+        affinity = len(os.sched_getaffinity(0))
+    except AttributeError:
+        affinity = os.cpu_count() or 1
+    mkl = "unknown"
+    for line in torch.__config__.show().splitlines():
+        if "Math Kernel Library" in line or "MKL" in line:
+            mkl = line.strip(" -")
+            break
+    return {"cpu_model": model, "cpus_visible": os.cpu_count(), "cpus_in_affinity_mask": affinity,
+            "omp_num_threads_env": os.environ.get("OMP_NUM_THREADS"), "torch": torch.__version__, "blas": mkl,
+            "python": platform.python_version()}
+
+
+def cpu_threads():
+    """Threads for the CPU baseline: every core this job is granted -- the scheduler affinity
+    mask, narrowed by OMP_NUM_THREADS when the box sets it (a one-GPU box grants a CPU share of
+    the host; os.cpu_count() shows the whole machine, which the job may not use)."""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:
+        n = os.cpu_count() or 1
+    env = os.environ.get("OMP_NUM_THREADS")
+    if env and env.isdigit() and int(env) > 0:
+        n = min(n, int(env))
+    return max(1, n)
+
+
+def cpu_baseline(args, E, R, seconds, eval_ctx=None):
+    """The reference CPU path on this host: oracle/refseq.py replays the reference's ATen op
+    sequences (KgeModel.score_sp, one TrainingJob1vsAll batch incl. Adagrad, EntityRankingJob)."""
     from oracle import refseq
 
-    torch.set_num_threads(max(1, min(os.cpu_count() or 1, 16)))
+    threads = cpu_threads()
+    torch.set_num_threads(threads)
+    B, d = args.batch, args.dim
     g = torch.Generator().manual_seed(0)
-    ent = torch.randn(E, args.dim, generator=g) * 0.1
-    rel = torch.randn(R, args.dim, generator=g) * 0.1
+    ent = torch.randn(E, d, generator=g) * 0.1
+    rel = torch.randn(R, d, generator=g) * 0.1
     times = []
     t_end = time.perf_counter() + seconds
-    i = 0
-    while (time.perf_counter() < t_end or len(times) < 3) and len(times) < 200:
-        s = torch.randint(0, E, (args.batch,), generator=g)
-        p = torch.randint(0, R, (args.batch,), generator=g)
+    while (time.perf_counter() < t_end or len(times) < 5) and len(times) < 200:
+        s = torch.randint(0, E, (B,), generator=g)
+        p = torch.randint(0, R, (B,), generator=g)
         t0 = time.perf_counter()
         refseq.complex_score_sp(ent, rel, s, p)
         times.append(time.perf_counter() - t0)
-        i += 1
     med = float(np.median(times))
-    return {"value": args.batch * E / med, "unit": "scored triples/s", "cores": torch.get_num_threads(),
-            "kind": "port", "ms_per_step": med * 1e3,
-            "sample": f"{len(times)} x score_sp (B={args.batch}, E={E}, d={args.dim}, N(0,0.1)), "
-                      f"reference ATen op sequence (oracle/refseq.py) on CPU, median"}
+    out = {"value": B * E / med, "unit": "scored triples/s", "cores": threads, "kind": "port",
+           "ms_per_step": med * 1e3,
+           "sample": f"median of {len(times)} x score_sp (B={B}, E={E}, d={d}, N(0,0.1)): the reference's ATen op "
+                     f"sequence (oracle/refseq.py, bit-exact vs reference-captured outputs) on the CPU",
+           "host": host_info(),
+           "flush_denormal": "unset (left as the reference leaves it; torch.set_flush_denormal is not called)"}
+    # one TrainingJob1vsAll batch (sp + po forward / backward, CE, Adagrad) at both initialisations
+    train = {}
+    for name, std in (("normal_0.1", 0.1), ("normal_1.0", 1.0)):
+        gen = torch.Generator().manual_seed(1)
+        e = torch.nn.Parameter(torch.randn(E, d, generator=gen) * std)
+        r = torch.nn.Parameter(torch.randn(R, d, generator=gen) * std)
+        opt = torch.optim.Adagrad([e, r], lr=0.2)
+        ts = []
+        for i in range(6):  # 1 warm-up + 5 timed
+            tr = torch.stack([torch.randint(0, E, (B,), generator=gen), torch.randint(0, R, (B,), generator=gen),
+                              torch.randint(0, E, (B,), generator=gen)], 1)
+            t0 = time.perf_counter()
+            refseq.train_step_1vsall(e, r, opt, tr)
+            ts.append(time.perf_counter() - t0)
+        m = float(np.median(ts[1:]))
+        train[name] = {"ms_per_step": m * 1e3, "scored_triples_per_s": 2 * B * E / m, "train_triples_per_s": B / m,
+                       "runs": len(ts) - 1}
+    out["train_step_1vsall"] = train
+    out["train_step_note"] = ("N(0,1) is the reference's default init (lookup_embedder.yaml); its softmax gradients "
+                              "are denormal-laden, which slows the CPU backward GEMMs")
+    if eval_ctx is not None:  # filtered entity ranking on the same tables / triples as the GPU job
+        ent_c, rel_c, splits, bs = eval_ctx
+        t0 = time.perf_counter()
+        job = refseq.EntityRankingCPU(ent_c, rel_c, splits, eval_split="test", filter_splits=("train", "valid"),
+                                      batch_size=bs)
+        build = time.perf_counter() - t0
+        ts, metrics = [], None
+        for _ in range(5):
+            t0 = time.perf_counter()
+            _, metrics = job.run()
+            ts.append(time.perf_counter() - t0)
+        m = float(np.median(ts))
+        n = len(splits["test"])
+        out["eval"] = {"triples": n, "seconds": m, "triples_per_s": n / m, "index_build_seconds": build, "runs": 5,
+                       "mrr_filtered": metrics["mean_reciprocal_rank_filtered"],
+                       "hits_at_10_filtered": metrics["hits_at_10_filtered"],
+                       "extrapolated_seconds_full_test_split_20466": 20466 * m / n,
+                       "sample": f"first {n} triples of the synthetic FB15K-237 test split, filtered against "
+                                 f"train + valid + test, batch {bs}: the reference's EntityRankingJob op sequence "
+                                 f"(refseq.EntityRankingCPU, rank for rank vs reference-captured fixtures)"}
+    return out
+
+
+# --------------------------------------------------------------------------------- main
 
 
 def main():
@@ -139,91 +261,48 @@ def main():
     rel = model._relation_embedder._embeddings.weight
     steps, warmup = args.steps, args.warmup
     g = torch.Generator(device=device).manual_seed(1 + rank)
-    s_all = torch.randint(0, E, (steps + warmup, B), device=device, generator=g)
-    p_all = torch.randint(0, R, (steps + warmup, B), device=device, generator=g)
+    s_all = torch.randint(0, E, (steps + warmup + 1, B), device=device, generator=g)
+    p_all = torch.randint(0, R, (steps + warmup + 1, B), device=device, generator=g)
     prec = _lib.PRECISIONS[args.precision]
 
-    # Every rank scores its own 1024 queries against the entity table (30 MB, replicated at
-    # setup): the scored triples are partitioned by query and the step has no data-path
-    # collective.  The entity-row-sharded exchange (kge.sharded: the design for eval top-k,
-    # vocab-parallel training and tables too large to replicate) is timed after the headline
-    # loop and reported in "row_sharded".
-    def step(i):
+    def step_full_table(i):  # every query of this rank against the whole table (model API)
         with torch.no_grad():
             return model.score_sp(s_all[i], p_all[i])
+
+    extra_n = {}
+    if world == 1:
+        sec = timed_loop(step_full_table, steps, warmup, world)
+        rows_q, cols = B, E
+        parallelism = "single GPU"
+    else:
+        sec, rows_q, cols, extra_n = sharded_headline(args, world, rank, device, ent, rel, prec, s_all, p_all,
+                                                      step_full_table)
+        parallelism = (f"entity table row-sharded x{world} (RCCL over xGMI): {B} queries per rank, query rows "
+                       f"all-gathered, global batch of {world * B} scored against each rank's {cols} rows")
     scored_per_step = world * B * E
 
-    # timed region: K steps bracketed by barrier + synchronize, nothing else inside
-    sec = timed_loop(step, steps, warmup, world)
-    # instrumented re-run of the same steps: HIP events around every contraction launch
-    engine.KERNEL_EVENTS = []
-    for i in range(min(steps, 20)):
-        step(warmup + i)
-    torch.cuda.synchronize()
-    events = engine.KERNEL_EVENTS
-    engine.KERNEL_EVENTS = None
-    row_sharded = None
-    if world > 1:
-        from kge.sharded import EngineOps, RowShardedScorer, shard_bounds
-
-        lo, hi = shard_bounds(E, world, rank)
-        sharded = RowShardedScorer(ent.detach()[lo:hi].contiguous(), lo, hi, E, rel.detach(),
-                                   EngineOps(_lib.COMPLEX, prec))
-        # shard-affine loader: rank k's queries have their subject in shard k
-        s_aff = torch.randint(lo, hi, (steps + warmup, B), device=device, generator=g)
-
-        def step_sharded(i):
-            with torch.no_grad():
-                return sharded.score_sp_local(s_aff[i], p_all[i])
-
-        sec_sh = timed_loop(step_sharded, steps, warmup, world)
-        q_loc = torch.randn(B, d, device=device)
-
-        def gather_only(i):
-            out = torch.empty(world * B, d, device=device)
-            dist.all_gather_into_tensor(out, q_loc)
-        sec_ag = timed_loop(gather_only, steps, warmup, world)
-        t = torch.tensor([sec_sh, sec_ag], device=device, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        sec_sh, sec_ag = float(t[0]), float(t[1])
-        row_sharded = {"ms_per_step": sec_sh * 1e3, "value": world * B * E / sec_sh,
-                       "q_all_gather_ms": sec_ag * 1e3,
-                       "what": f"entity table row-sharded x{world}; each rank's 1024 queries (subjects in its "
-                               f"shard) -> query rows all_gathered ({world * B * d * 4 / 1e6:.0f} MB) -> global "
-                               f"batch scored against every shard (kge.sharded.score_sp_local)"}
-    launch_ms = float(np.mean([a.elapsed_time(b) for a, b in events])) if events else float("nan")
-    # back-to-back launches of the same contraction between two HIP events on the launch
-    # stream: the kernel's average duration without per-launch event overhead (this is the
-    # figure the rocprofv3 kernel-trace average is compared with)
+    # ---- roofline of the dominant kernel (the contraction at this rank's shape), per launch, per GPU
     with torch.no_grad():
-        q = _lib.prep_query(_lib.COMPLEX, _lib.DIR_SP, ent.detach(), s_all[0], rel.detach(), p_all[0], B, d, d)
-        tab = ent.detach()
-        out_buf = torch.empty(q.shape[0], tab.shape[0], device=device)
-        if prec == _lib.PREC_BF16X3:  # the production path: pre-split Q planes + persistent kernel
-            qh, ql = _lib.split_rows(q)
-            kern = lambda: _lib.score_dot_split(qh, ql, tab, None, d, out=out_buf)  # noqa: E731
-        else:
-            kern = lambda: _lib.score_dot(q, tab, None, prec, out=out_buf)  # noqa: E731
-        for _ in range(20):  # the clock settles under sustained MFMA load
-            kern()
-        a = torch.cuda.Event(enable_timing=True)
-        b = torch.cuda.Event(enable_timing=True)
-        reps = 100
-        a.record()
-        for _ in range(reps):
-            kern()
-        b.record()
-        torch.cuda.synchronize()
-        kern_ms = a.elapsed_time(b) / reps
+        q = _lib.prep_query(_lib.COMPLEX, _lib.DIR_SP, ent.detach(), s_all[0].repeat(rows_q // B), rel.detach(),
+                            p_all[0].repeat(rows_q // B), rows_q, d, d)
+        tab = ent.detach()[:cols]
+        out_buf = torch.empty(rows_q, cols, device=device)
+        qh, ql = _lib.split_rows(q)
+        k3_ms = kernel_time_ms(lambda: _lib.score_dot_split(qh, ql, tab, None, d, out=out_buf))
+        k32_ms = kernel_time_ms(lambda: _lib.score_dot(q, tab, None, _lib.PREC_FP32, out=out_buf), reps=30, settle=5)
         del out_buf
-    if world > 1:
-        t = torch.tensor([sec, kern_ms, launch_ms], device=device, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        sec, kern_ms, launch_ms = float(t[0]), float(t[1]), float(t[2])
+    # instrumented steps: HIP events around every contraction launch of the model API
+    launch_ms = float("nan")
+    if world == 1:
+        engine.KERNEL_EVENTS = []
+        for i in range(min(steps, 20)):
+            step_full_table(warmup + i)
+        torch.cuda.synchronize()
+        events, engine.KERNEL_EVENTS = engine.KERNEL_EVENTS, None
+        launch_ms = float(np.mean([a.elapsed_time(b) for a, b in events])) if events else float("nan")
+    sec, k3_ms, k32_ms = max_over_ranks([sec, k3_ms, k32_ms], device, world)
+    kern_ms = k3_ms if args.precision == "bf16x3" else k32_ms
 
-    # roofline of the dominant kernel (the contraction) -- per launch, per GPU
-    rows_q = B
-    cols = E
     alg_flops = 2.0 * rows_q * cols * d
     alg_bytes = 4.0 * (rows_q * d + cols * d + rows_q * cols)
     k_s = kern_ms / 1e3
@@ -235,43 +314,49 @@ def main():
         note = "fp32-input MFMA (v_mfma_f32_32x32x2_f32); peak = 157.3 TF"
     achieved = alg_flops / k_s / 1e12
     # HBM bytes per launch from the PMC passes of scripts/pmc_traffic.sh (same kernel, same
-    # shape at N=1), committed under profiles/; null when absent or for another shape.
+    # shape, N = 1), committed under profiles/; null when absent or for another shape.
     traffic, traffic_src = None, None
-    pmc = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r01", "pmc_traffic.json")
-    if args.precision == "bf16x3" and os.path.exists(pmc):  # same per-GPU launch at every N
-        with open(pmc) as f:
-            t = json.load(f)
-        traffic = int(t["traffic_bytes"])
-        traffic_src = ("profiles/r01/pmc_traffic.json: 2 x FETCH_SIZE + WRITE_SIZE per dispatch "
-                       f"(read {t['read_bytes'] / 1e6:.1f} MB, write {t['write_bytes'] / 1e6:.1f} MB)")
+    for rnd in (PROFILE_ROUND, "r01"):
+        pmc = os.path.join(ROOT, "profiles", rnd, "pmc_traffic.json")
+        if args.precision == "bf16x3" and world == 1 and os.path.exists(pmc):
+            with open(pmc) as f:
+                t = json.load(f)
+            traffic = int(t["traffic_bytes"])
+            traffic_src = (f"profiles/{rnd}/pmc_traffic.json: 2 x FETCH_SIZE + WRITE_SIZE per dispatch "
+                           f"(read {t['read_bytes'] / 1e6:.1f} MB, write {t['write_bytes'] / 1e6:.1f} MB)")
+            break
     roofline = {"bound": "mfma", "achieved": round(achieved, 1), "peak": round(peak, 1), "unit": "TFLOP/s",
                 "frac": round(achieved / peak, 4), "traffic": traffic, "traffic_source": traffic_src,
-                "kernel": "score_dot_persist16_kernel" if args.precision == "bf16x3" else "score_dot_kernel", "kernel_us": round(kern_ms * 1e3, 2),
+                "kernel": "score_dot_persist16_kernel" if args.precision == "bf16x3" else "score_dot_kernel",
+                "kernel_shape": [rows_q, cols, d],
+                "kernel_us": round(kern_ms * 1e3, 2),
                 "kernel_us_per_launch_events": round(launch_ms * 1e3, 2),
                 "hbm_achieved_GBs": round(alg_bytes / k_s / 1e9, 1),
                 "hbm_frac": round(alg_bytes / k_s / 1e9 / HBM_PEAK_GBS, 4),
-                "alg_bytes_per_launch": int(alg_bytes), "alg_flops_per_launch": int(alg_flops), "note": note}
+                "alg_bytes_per_launch": int(alg_bytes), "alg_flops_per_launch": int(alg_flops), "note": note,
+                "exact_fp32_kernel_us": round(k32_ms * 1e3, 2),
+                "exact_fp32_kernel_frac_of_fp32_mfma_peak": round(alg_flops / (k32_ms / 1e3) / 1e12 / FP32_MFMA_TFLOPS, 4)}
 
     value = scored_per_step / sec
-    out = {"metric": "1vsAll scored triples/sec (score_sp, ComplEx-512, FB15K-237 shape, B=1024)",
+    out = {"metric": "1vsAll scored triples/sec (score_sp, ComplEx-512, FB15K-237 shape, B=1024 per GPU)",
            "value": value, "unit": "scored triples/s", "n_gpus": world, "steps": steps, "warmup": warmup,
            "ms_per_step": sec * 1e3, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
            "dtype": "f32 (bf16x3 MFMA)" if args.precision == "bf16x3" else "f32",
            "data": "synthetic (FB15K-237 shape: 14,541 entities / 237 relations), N(0,0.1) random-init tables",
            "config": {"workload": "configs[1]: ComplEx dim=512 1vsAll FB15K-237, batch 1024, score_sp per step",
-                      "model": "complex", "dim": d, "global_batch": B * world, "entities": E,
-                      "parallelism": "single GPU" if world == 1 else
-                      f"dp{world}: queries partitioned over ranks (1024 each), entity table replicated, "
-                      f"no collective in the step",
+                      "dim": d, "global_batch": B * world, "entities": E, "parallelism": parallelism,
                       "precision": args.precision},
            "roofline": roofline}
-    if row_sharded is not None:
-        out["row_sharded"] = row_sharded
+    out.update(extra_n)
 
     if rank == 0 and world == 1 and not args.no_extras:
-        out["extras"] = extras(args, model, c, E, R, device)
+        out["extras"], eval_ctx = extras(args, model, c, E, R, device)
+    else:
+        eval_ctx = None
     if rank == 0 and world == 1 and not args.no_cpu:
-        cb = cpu_baseline(args, E, R, args.cpu_seconds)
+        cb = cpu_baseline(args, E, R, args.cpu_seconds, eval_ctx)
+        if eval_ctx is not None and "eval" in cb:
+            cb["eval"]["mrr_filtered_gpu_same_input"] = out["extras"]["eval_subset_mrr_filtered"]
         out["cpu_baseline"] = cb
         out["speedup_vs_cpu"] = round(value / cb["value"], 1)
     if rank == 0:
@@ -280,8 +365,102 @@ def main():
         dist.destroy_process_group()
 
 
+def sharded_headline(args, world, rank, device, ent, rel, prec, s_all, p_all, step_full_table):
+    """N > 1.  Returns (seconds per step of the row-sharded score_sp, rows, columns of this
+    rank's contraction, extra report entries)."""
+    from kge import _lib
+    from kge.sharded import EngineOps, RowShardedScorer, shard_bounds
+
+    E = ent.shape[0]
+    B, d = args.batch, args.dim
+    steps, warmup = args.steps, args.warmup
+    lo, hi = shard_bounds(E, world, rank)
+    sharded = RowShardedScorer(ent.detach()[lo:hi].contiguous(), lo, hi, E, rel.detach(),
+                               EngineOps(_lib.COMPLEX, prec))
+    g = torch.Generator(device=device).manual_seed(101 + rank)
+    # shard-affine loader: rank k's queries have their subject in shard k
+    s_aff = torch.randint(lo, hi, (steps + warmup + 1, B), device=device, generator=g)
+    tickets = []
+
+    def step_pipelined(i):  # exchange of batch i + 1 in flight while batch i is scored
+        with torch.no_grad():
+            if not tickets:
+                tickets.append(sharded.submit_queries_local(s_aff[i], p_all[i]))
+            tickets.append(sharded.submit_queries_local(s_aff[i + 1], p_all[i + 1]))
+            return sharded.score_submitted(tickets.pop(0))
+
+    def step_serial(i):  # prep -> all_gather -> contraction, nothing overlapped
+        with torch.no_grad():
+            return sharded.score_submitted(sharded.submit_queries_local(s_aff[i], p_all[i]))
+
+    sec_pipe = timed_loop(step_pipelined, steps, warmup, world)
+    tickets.clear()
+    torch.cuda.synchronize()
+    sec_serial = timed_loop(step_serial, steps, warmup, world)
+    sec_dp = timed_loop(step_full_table, steps, warmup, world)
+    q_loc = torch.randn(B, d, device=device)
+    from kge.sharded import all_gather_into_tensor
+
+    def gather_only(i):
+        out = torch.empty(world * B, d, device=device)
+        all_gather_into_tensor(out, q_loc)
+    sec_ag = timed_loop(gather_only, steps, warmup, world)
+    sec_pipe, sec_serial, sec_dp, sec_ag = max_over_ranks([sec_pipe, sec_serial, sec_dp, sec_ag], device, world)
+    extra = {
+        "row_sharded": {"ms_per_step_pipelined": sec_pipe * 1e3, "ms_per_step_serial": sec_serial * 1e3,
+                        "value_serial": world * B * E / sec_serial, "q_all_gather_ms": sec_ag * 1e3,
+                        "q_all_gather_bytes": world * B * d * 4,
+                        "what": "headline = pipelined: the all_gather of batch i+1's query rows runs while batch i "
+                                "is scored; serial = prep -> all_gather -> contraction back to back"},
+        "replicated_dp": {"ms_per_step": sec_dp * 1e3, "value": world * B * E / sec_dp,
+                          "what": f"every rank scores its {B} queries against a replica of the whole table "
+                                  f"(KgeModel.score_sp); no collective in the step"}}
+    if not args.no_c5:
+        extra["row_sharded_c5"] = sharded_c5(args, world, rank, device, prec)
+    return sec_pipe, world * B, hi - lo, extra
+
+
+def sharded_c5(args, world, rank, device, prec):
+    """BASELINE configs[4]: ComplEx-512 score_sp on the Wikidata5M shape (4,594,485 entities)
+    with the table row-sharded over the ranks -- the same pipelined step as the headline."""
+    from kge import _lib
+    from kge.dataset import SHAPES
+    from kge.sharded import EngineOps, RowShardedScorer, shard_bounds
+
+    E, R, _ = SHAPES["wikidata5m"]
+    B, d = args.batch, args.dim
+    lo, hi = shard_bounds(E, world, rank)
+    g = torch.Generator(device=device).manual_seed(7 + rank)
+    ent = torch.randn(hi - lo, d, device=device, generator=g) * 0.1
+    rel = torch.randn(R, d, device=device, generator=g) * 0.1
+    sharded = RowShardedScorer(ent, lo, hi, E, rel, EngineOps(_lib.COMPLEX, prec))
+    n = 8
+    s = torch.randint(lo, hi, (n + 1, B), device=device, generator=g)
+    p = torch.randint(0, R, (n + 1, B), device=device, generator=g)
+    tickets = []
+
+    def step(i):
+        with torch.no_grad():
+            if not tickets:
+                tickets.append(sharded.submit_queries_local(s[i % n], p[i % n]))
+            tickets.append(sharded.submit_queries_local(s[(i + 1) % n], p[(i + 1) % n]))
+            out = sharded.score_submitted(tickets.pop(0))
+            del out
+    sec = timed_loop(step, 6, 2, world)
+    (sec,) = max_over_ranks([sec], device, world)
+    rows, cols = world * B, hi - lo
+    flops = 2.0 * rows * cols * d
+    res = {"entities": E, "rows_per_rank": cols, "global_batch": rows, "ms_per_step": sec * 1e3,
+           "value": rows * E / sec, "unit": "scored triples/s",
+           "per_gpu_tflops": round(flops / sec / 1e12, 1),
+           "per_gpu_mfma_frac": round(flops / sec / 1e12 / (BF16_DENSE_TFLOPS / 3.0), 4)}
+    del sharded, ent
+    torch.cuda.empty_cache()
+    return res
+
+
 def extras(args, model, c, E, R, device):
-    """Secondary numbers: score_po, 1vsAll train step, eval MRR (synthetic test split)."""
+    """Secondary numbers: score_po, 1vsAll train step, eval (synthetic test split)."""
     from kge import Dataset
     from kge.job import EntityRankingJob, TrainingJob
 
@@ -293,13 +472,59 @@ def extras(args, model, c, E, R, device):
     with torch.no_grad():
         sec = timed_loop(lambda i: model.score_po(p[i], o[i]), 30, 10, 1)
     res["score_po_ms"] = round(sec * 1e3, 4)
-    # 1vsAll training step (sp + po, fwd + bwd + CE + Adagrad), train_step_ms
     c2 = c.clone()
+    ds = Dataset.synthetic(c2, args.dataset, seed=0)
+    # filtered eval BEFORE any training step, on the N(0, 0.1) tables the CPU replica also gets:
+    # the first 1,024 test triples (the CPU leg's bounded sample), then the whole test split
+    tables = (model._entity_embedder._embeddings.weight.detach().cpu().clone(),
+              model._relation_embedder._embeddings.weight.detach().cpu().clone())
+    c3 = c.clone()
+    c3.set("eval.split", "test")
+    c3.set("eval.batch_size", B)
+    sub = Dataset(c3, None)
+    sub._triples = dict(ds._triples)
+    sub._triples["test"] = ds._triples["test"][:1024].clone()
+    model.eval()
+    ej = EntityRankingJob(c3, sub, model=model)
+    tr = ej.run()
+    res["eval_subset_mrr_filtered"] = tr["mean_reciprocal_rank_filtered"]
+    res["eval_subset_hits_at_10_filtered"] = tr["hits_at_10_filtered"]
+    # the splits exactly as that GPU job saw them (test = the 1,024-triple sample)
+    splits = {k: sub.split(k).long().numpy() for k in ("train", "valid", "test")}
+    eval_ctx = (tables[0], tables[1], splits, B)
+    for prec in ("fp32", "bf16x3"):
+        c4 = c3.clone()
+        c4.set("engine.eval_precision", prec)
+        ej = EntityRankingJob(c4, ds, model=model)
+        ej._prepare()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        ej._run()  # first run: lazily built filter indexes and allocator warm-up
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        ts = []
+        for _ in range(5):
+            t2 = time.perf_counter()
+            tr = ej._run()
+            torch.cuda.synchronize()
+            ts.append(time.perf_counter() - t2)
+        key = "eval" if prec == "fp32" else "eval_bf16x3"
+        res[key + "_seconds"] = round(float(np.median(ts)), 4)
+        if prec == "fp32":
+            res["eval_test_triples"] = int(len(ds.split("test")))
+            res["eval_first_run_seconds"] = round(t1 - t0, 4)
+            res["eval_precision"] = "fp32 (engine.eval_precision default)"
+        res[key + "_mrr_filtered"] = tr["mean_reciprocal_rank_filtered"]
+        res[key + "_hits_at_10_filtered"] = tr["hits_at_10_filtered"]
+    res["eval_note"] = ("synthetic triples are drawn at random (no learnable structure), so a random-init model "
+                        "ranks near chance; rank / MRR parity with the reference is pinned by the reference-captured "
+                        "eval fixtures (tests/golden/eval_*.npz, full size: eval_fullsize_normal.npz) and, in this "
+                        "run, by cpu_baseline.eval on the same tables and triples")
+    # 1vsAll training step (sp + po, fwd + bwd + CE + Adagrad), train_step_ms
     c2.set("train.type", "1vsAll")
     c2.set("train.optimizer", "Adagrad")
     c2.set("train.optimizer_args", {"lr": 0.2})
     c2.set("train.batch_size", B)
-    ds = Dataset.synthetic(c2, args.dataset, seed=0)
     job = TrainingJob.create(c2, ds, model=model)
     job._prepare()
     job.model.train()
@@ -312,32 +537,10 @@ def extras(args, model, c, E, R, device):
     res["train_step_ms"] = round(sec * 1e3, 3)
     res["train_scored_triples_per_s"] = 2 * B * E / sec
     res["train_triples_per_s"] = B / sec
-    # filtered eval (test split, batch 1024)
-    c3 = c.clone()
-    c3.set("eval.split", "test")
-    c3.set("eval.batch_size", B)
-    job.model.eval()
-    ej = EntityRankingJob(c3, ds, model=job.model)
-    ej._prepare()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    ej._run()  # first run: lazily built filter indexes and allocator warm-up
-    torch.cuda.synchronize()
-    t1 = time.perf_counter()
-    tr = ej._run()
-    torch.cuda.synchronize()
-    res["eval_test_triples"] = int(len(ds.split("test")))
-    res["eval_seconds"] = round(time.perf_counter() - t1, 4)
-    res["eval_first_run_seconds"] = round(t1 - t0, 4)
-    res["eval_mrr_filtered"] = tr["mean_reciprocal_rank_filtered"]
-    res["eval_hits_at_10_filtered"] = tr["hits_at_10_filtered"]
-    res["eval_note"] = ("synthetic triples are drawn at random (no learnable structure), so the model trained "
-                        "for the timing steps ranks near chance; rank / MRR parity with the reference is pinned "
-                        "by the reference-captured eval fixtures (tests/test_gpu_api.py, tests/golden/eval_*.npz)")
     res.update(other_configs(device))
     if args.c5:
         res.update(c5_shard(args, device))
-    return res
+    return res, eval_ctx
 
 
 def c5_shard(args, device):
@@ -374,16 +577,7 @@ def c5_shard(args, device):
         q = _lib.prep_query(_lib.COMPLEX, _lib.DIR_SP, ent, s[0], rel, p[0], B, d, d)
         qh, ql = _lib.split_rows(q)
         buf = torch.empty(B, E, device=device)
-        for _ in range(3):
-            _lib.score_dot_split(qh, ql, ent, None, d, out=buf)
-        a = torch.cuda.Event(enable_timing=True)
-        b = torch.cuda.Event(enable_timing=True)
-        a.record()
-        for _ in range(10):
-            _lib.score_dot_split(qh, ql, ent, None, d, out=buf)
-        b.record()
-        torch.cuda.synchronize()
-    k_s = a.elapsed_time(b) / 10 / 1e3
+        k_s = kernel_time_ms(lambda: _lib.score_dot_split(qh, ql, ent, None, d, out=buf), reps=10, settle=3) / 1e3
     flops = 2.0 * B * E * d
     nbytes = 4.0 * (B * d + E * d + B * E)
     out["c5_shard_kernel_us"] = round(k_s * 1e6, 1)
@@ -426,6 +620,7 @@ def other_configs(device):
     c.set("train.optimizer", "Adagrad")
     c.set("train.optimizer_args", {"lr": 0.2})
     c.set("train.batch_size", 512)
+    c.set("engine.row_sharded", "off")
     c.set("verbose", False)
     sec, ds = _job_step_time(c, "wn18rr", 512)
     E = ds.num_entities()
@@ -444,6 +639,7 @@ def other_configs(device):
     c.set("train.optimizer", "Adagrad")
     c.set("train.optimizer_args", {"lr": 0.1})
     c.set("train.batch_size", 512)
+    c.set("engine.row_sharded", "off")
     c.set("verbose", False)
     sec, _ = _job_step_time(c, "fb15k-237", 512)
     res["c4_ns_rotate1024_fb15k237_b512_n1024_step_ms"] = round(sec * 1e3, 3)

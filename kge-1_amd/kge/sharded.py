@@ -29,6 +29,47 @@ import torch
 import torch.distributed as dist
 
 
+# ---- collectives.  RCCL ("nccl") moves device memory directly.  gloo is given CPU tensors
+# only: device tensors are staged through host memory with synchronous copies (rehearsing
+# several ranks on one GPU; gloo collectives on device tensors are not used).
+
+
+def _staged(t: torch.Tensor, group) -> bool:
+    return t.is_cuda and dist.get_backend(group) == "gloo"
+
+
+def all_reduce(t: torch.Tensor, op=None, group=None):
+    op = dist.ReduceOp.SUM if op is None else op
+    if _staged(t, group):
+        h = t.cpu()
+        dist.all_reduce(h, op=op, group=group)
+        t.copy_(h)
+    else:
+        dist.all_reduce(t, op=op, group=group)
+    return t
+
+
+def all_gather(outs, t: torch.Tensor, group=None):
+    if _staged(t, group):
+        hs = [torch.empty(o.shape, dtype=o.dtype) for o in outs]
+        dist.all_gather(hs, t.cpu(), group=group)
+        for o, h in zip(outs, hs):
+            o.copy_(h)
+    else:
+        dist.all_gather(outs, t, group=group)
+    return outs
+
+
+def all_gather_into_tensor(out: torch.Tensor, t: torch.Tensor, group=None, async_op: bool = False):
+    """Returns a work handle when async_op (None when the call completed synchronously)."""
+    if _staged(t, group):
+        h = torch.empty(out.shape, dtype=out.dtype)
+        dist.all_gather_into_tensor(h, t.cpu(), group=group)
+        out.copy_(h)
+        return None
+    return dist.all_gather_into_tensor(out, t, group=group, async_op=async_op)
+
+
 class EngineOps:
     """Default compute: libkgescore."""
 
@@ -142,7 +183,7 @@ class RowShardedScorer:
 
     def _all_gather_1d(self, x: torch.Tensor) -> torch.Tensor:
         out = [torch.empty_like(x) for _ in range(self.world)]
-        dist.all_gather(out, x.contiguous(), group=self.group)
+        all_gather(out, x.contiguous(), group=self.group)
         return torch.cat(out)
 
     def _owned_rows(self, ids: torch.Tensor):
@@ -155,7 +196,7 @@ class RowShardedScorer:
         owned, local = self._owned_rows(ids)
         rows = self.ent[local]
         rows = torch.where(owned[:, None], rows, torch.zeros_like(rows))
-        dist.all_reduce(rows, group=self.group)
+        all_reduce(rows, group=self.group)
         return rows
 
     def queries(self, e: torch.Tensor, p: torch.Tensor, direction: int):
@@ -165,7 +206,7 @@ class RowShardedScorer:
         owned, local = self._owned_rows(e_all)
         q = self.ops.prep(direction, self.ent, local, self.rel, p_all)
         q = torch.where(owned[:, None], q, torch.zeros_like(q))
-        dist.all_reduce(q, group=self.group)
+        all_reduce(q, group=self.group)
         return q, e_all, p_all
 
     # ---------------------------------------------------------------- scoring
@@ -184,12 +225,30 @@ class RowShardedScorer:
             raise ValueError("queries_local needs every query entity in this rank's shard")
         q = self.ops.prep(direction, self.ent, local, self.rel, p)
         out = torch.empty((self.world * q.shape[0], q.shape[1]), dtype=q.dtype, device=q.device)
-        dist.all_gather_into_tensor(out, q.contiguous(), group=self.group)
+        all_gather_into_tensor(out, q.contiguous(), group=self.group)
         return out
 
     def score_sp_local(self, s: torch.Tensor, p: torch.Tensor, direction: int = 0) -> torch.Tensor:
         """score_sp for shard-affine batches: [W*B, hi - lo] local slice of the scores."""
         return self.ops.score(self.queries_local(s, p, direction), self._win(direction, self.ent))
+
+    def submit_queries_local(self, e: torch.Tensor, p: torch.Tensor, direction: int = 0):
+        """Start the exchange of a shard-affine batch (queries_local) without waiting for it:
+        the query rows are prepared on the current stream and their all_gather is issued
+        asynchronously (RCCL runs it on its own stream), so the caller can score the previous
+        batch meanwhile.  Returns a ticket for ``score_submitted``."""
+        owned, local = self._owned_rows(e)
+        q = self.ops.prep(direction, self.ent, local, self.rel, p)
+        out = torch.empty((self.world * q.shape[0], q.shape[1]), dtype=q.dtype, device=q.device)
+        work = all_gather_into_tensor(out, q.contiguous(), group=self.group, async_op=True)
+        return (work, out, q, direction)  # q is kept alive until the gather has read it
+
+    def score_submitted(self, ticket) -> torch.Tensor:
+        """Local slice [W*B, hi - lo] of the scores of a batch started by submit_queries_local."""
+        work, q_all, _, direction = ticket
+        if work is not None:
+            work.wait()  # the current stream waits for the gather; the host does not block
+        return self.ops.score(q_all, self._win(direction, self.ent))
 
     def topk(self, scores_local: torch.Tensor, k: int):
         """All-gather of per-shard top-k (score, global entity id), merged on every rank."""
@@ -202,8 +261,8 @@ class RowShardedScorer:
             i = torch.cat([i, torch.full((i.shape[0], pad), -1, device=i.device, dtype=i.dtype)], 1)
         vs = [torch.empty_like(v) for _ in range(self.world)]
         is_ = [torch.empty_like(i) for _ in range(self.world)]
-        dist.all_gather(vs, v.contiguous(), group=self.group)
-        dist.all_gather(is_, i.contiguous(), group=self.group)
+        all_gather(vs, v.contiguous(), group=self.group)
+        all_gather(is_, i.contiguous(), group=self.group)
         V, I = torch.cat(vs, 1), torch.cat(is_, 1)
         tv, ti = torch.topk(V, k, dim=1)
         return tv, torch.gather(I, 1, ti)
@@ -241,24 +300,24 @@ class RowShardedScorer:
             owned, local = self._owned_rows(e_all)
             q = self.ops.prep(direction, self.ent, local, self.rel, p_all)
             q = torch.where(owned[:, None], q, torch.zeros_like(q))
-            dist.all_reduce(q, group=self.group)
+            all_reduce(q, group=self.group)
             buf = torch.empty(n, (E_k + 3) // 4 * 4, device=q.device, dtype=torch.float32)
             logits = self.ops.score(q, self._win(direction, self.ent), out=buf[:, :E_k])
             mx, sm, tg = self.ops.row_stats(logits, self.lo, labels)
             M = mx.clone()
-            dist.all_reduce(M, op=dist.ReduceOp.MAX, group=self.group)
+            all_reduce(M, op=dist.ReduceOp.MAX, group=self.group)
             z = torch.where(mx == -math.inf, torch.zeros_like(sm), sm * torch.exp(mx - M))
-            dist.all_reduce(z, group=self.group)
-            dist.all_reduce(tg, group=self.group)
+            all_reduce(z, group=self.group)
+            all_reduce(tg, group=self.group)
             lse = M + torch.log(z)
             loss += ((lse - tg).double().sum() * scale)
             g = self.ops.softmax_grad(logits, self.lo, labels, lse, scale, logits)
             dq = torch.empty_like(q)
             self.ops.score_bwd(g, q, self._win(direction, self.ent), dq, self._win(direction, d_ent))
-            dist.all_reduce(dq, group=self.group)
+            all_reduce(dq, group=self.group)
             dq = torch.where(owned[:, None], dq, torch.zeros_like(dq))
             self.ops.prep_bwd(direction, self.ent, local, self.rel, p_all, dq, d_ent, d_rel)
-        dist.all_reduce(d_rel, group=self.group)
+        all_reduce(d_rel, group=self.group)
         return loss, d_ent, d_rel  # loss: a 0-dim float64 tensor on the table's device (no host sync)
 
     # ---------------------------------------------------------------- eval
@@ -284,7 +343,7 @@ class RowShardedScorer:
             sc = self.ops.score(q, self._win(direction, self.ent))
             self.ops.rank_counts(sc, self.lo, tgt, true, f[0], f[1], t[0] if t is not None else None,
                                  t[1] if t is not None else None, counts[di, 0], counts[di, 1])
-        dist.all_reduce(counts, group=self.group)
+        all_reduce(counts, group=self.group)
         return counts
 
     def all_gather_table(self) -> torch.Tensor:
@@ -294,5 +353,5 @@ class RowShardedScorer:
         mine = torch.zeros(per, self.ent.shape[1], dtype=self.ent.dtype, device=self.ent.device)
         mine[:self.hi - self.lo] = self.ent
         parts = [torch.empty_like(mine) for _ in range(self.world)]
-        dist.all_gather(parts, mine, group=self.group)
+        all_gather(parts, mine, group=self.group)
         return torch.cat(parts)[:self.E]

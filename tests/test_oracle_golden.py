@@ -95,3 +95,43 @@ def test_refseq_bitwise(name, regime):
     torch.set_num_threads(4)
     np.testing.assert_array_equal(refseq.complex_score_sp(ent, rel, s, p).numpy(), f["sp_all"])
     np.testing.assert_array_equal(refseq.complex_score_po(ent, rel, p, o).numpy(), f["po_all"])
+
+
+@pytest.mark.parametrize("regime", ["dyadic", "normal"])
+def test_refseq_entity_ranking_reproduces_reference_ranks(regime):
+    """The CPU eval replica (refseq.EntityRankingCPU, bench.py's cpu_baseline eval leg) against
+    the reference-captured ranks and metrics: identical ranks, metrics to fp32 rounding."""
+    import torch
+    from oracle import refseq
+
+    f = np.load(os.path.join(GOLDEN, f"eval_{regime}.npz"))
+    meta = json.loads(str(f["meta"]))
+    torch.set_num_threads(4)
+    splits = {k: f["tri_" + k].astype(np.int64) for k in ("train", "valid", "test")}
+    job = refseq.EntityRankingCPU(torch.from_numpy(f["ent"]), torch.from_numpy(f["rel"]), splits,
+                                  eval_split=meta["eval_split"], filter_splits=meta["filter_splits"],
+                                  filter_with_test=meta["filter_with_test"], batch_size=meta["batch_size"])
+    ranks, metrics = job.run()
+    for k, v in ranks.items():
+        np.testing.assert_array_equal(v, f["full_" + k], err_msg=k)
+    ref = json.loads(str(f["metrics"]))["full"]
+    for k, v in ref.items():
+        assert metrics[k] == pytest.approx(v, rel=1e-6, abs=1e-9), k
+
+
+def test_refseq_train_step_reproduces_reference_trajectory():
+    """The CPU training-step replica (refseq.train_step_1vsall, bench.py's cpu_baseline train
+    leg) against the reference-captured three-batch 1vsAll trajectory."""
+    import torch
+    from oracle import refseq
+
+    f = np.load(os.path.join(GOLDEN, "train1vsall_complex.npz"))
+    meta = json.loads(str(f["meta"]))
+    torch.set_num_threads(4)
+    ent = torch.nn.Parameter(torch.from_numpy(f["ent0"]).clone())
+    rel = torch.nn.Parameter(torch.from_numpy(f["rel0"]).clone())
+    opt = torch.optim.Adagrad([ent, rel], lr=meta["lr"])
+    losses = [refseq.train_step_1vsall(ent, rel, opt, torch.from_numpy(b)) for b in f["batches"]]
+    np.testing.assert_allclose(losses, f["losses"], rtol=1e-6)
+    np.testing.assert_allclose(ent.detach().numpy(), f["ent1"], atol=1e-6)
+    np.testing.assert_allclose(rel.detach().numpy(), f["rel1"], atol=1e-6)
