@@ -153,6 +153,26 @@ int kge_score_dot_bwd_q_noalloc(const float* g, int64_t ldg, const float* t, int
                                 const int64_t* tidx, int64_t n, int64_t m, int d, float* dq,
                                 int64_t lddq, int accumulate, void* stream);
 
+/* The backward GEMMs on pre-split operand planes (bf16x3; mm backward of complex.py:36-44 /
+ * distmult.py:20-22 / rescal.py:42,48, as kge_score_dot_bwd_q / _t):
+ *   dQ[i, k] (+)= gscale * sum_j G[i, j] * T[j, k]          i < n, j < m, k < d
+ *   dT[j, k] (+)= gscale * sum_i G[i, j] * Q[i, k]
+ * g_hi / g_lo: the G planes left by kge_softmax_*_planes, row stride ldgp bf16 elements (for
+ * that layout g_lo = g_hi + lds and ldgp = 2 lds); q_hi / q_lo: the query planes the forward
+ * contraction used (kge_prep_query_split), row stride ldqp, with rows [n, n_pad) zero.
+ * gscale: NULL or a DEVICE pointer to one float (the upstream gradient of the loss).  The dQ
+ * GEMM splits its long reduction into kge_score_dot_bwd_q_planes_ws_size(n, m, d) floats of
+ * caller workspace, summed in a fixed order.  All operands staged by LDS-DMA: no split, no
+ * masks.  Requires d % 4 == 0 and 16-B aligned rows everywhere (else KGE_ERR_ALIGN). */
+int64_t kge_score_dot_bwd_q_planes_ws_size(int64_t n, int64_t m, int d);
+int kge_score_dot_bwd_q_planes(const void* g_hi, const void* g_lo, int64_t ldgp, const float* t,
+                               int64_t ldt, int64_t n, int64_t m, int d, float* dq, int64_t lddq,
+                               int accumulate, const float* gscale, float* ws, int64_t ws_elems,
+                               void* stream);
+int kge_score_dot_bwd_t_planes(const void* g_hi, const void* g_lo, int64_t ldgp, const void* q_hi,
+                               const void* q_lo, int64_t ldqp, int64_t n_pad, int64_t m, int d, float* dt,
+                               int64_t lddt, int accumulate, const float* gscale, void* stream);
+
 /* dT[row(j), k] += sum_i G[i, j] * Q[i, k]   (always accumulates; rows scattered
  * atomically when tidx != NULL) */
 int kge_score_dot_bwd_t(const float* g, int64_t ldg, const float* q, int64_t ldq,
@@ -217,6 +237,19 @@ int kge_softmax_xent(const float* s, int64_t lds, int64_t n, int64_t m, const in
 int kge_softmax_kl(const float* s, int64_t lds, int64_t n, int64_t m, const int64_t* l_ptr,
                    const int64_t* l_col, float smoothing, float scale, float* loss, float* g,
                    int64_t ldg, void* stream);
+
+/* The two losses above with the gradient left as bf16 hi / lo PLANES in place of the score
+ * rows, for kge_score_dot_bwd_q_planes / _t_planes: on return row i of the buffer (lds floats)
+ * holds the hi plane of G[i, 0 .. lds) in its first lds bf16 and the lo plane in its second lds
+ * bf16 (G = hi + lo to 2^-16 relative; columns [m, lds) zero), and rows [n, n_pad) are zero in
+ * both planes (K padding of the dT GEMM).  Requires lds % 32 == 0, a 16-B aligned buffer of
+ * n_pad rows and m <= kge_softmax_planes_max_columns() (the row is held in registers); the
+ * scores are consumed.  Same objectives and reference lines as kge_softmax_xent / _kl. */
+int64_t kge_softmax_planes_max_columns(void);
+int kge_softmax_xent_planes(float* s, int64_t lds, int64_t n, int64_t n_pad, int64_t m,
+                            const int64_t* labels, float scale, float* loss, void* stream);
+int kge_softmax_kl_planes(float* s, int64_t lds, int64_t n, int64_t n_pad, int64_t m, const int64_t* l_ptr,
+                          const int64_t* l_col, float smoothing, float scale, float* loss, void* stream);
 
 /* Vocab-parallel 1vsAll (entity table row-sharded): S holds columns
  * [c0, c0 + m) of the full score rows, labels are global column ids.

@@ -9,11 +9,11 @@
 // shape, MI355X_MICROARCH 'DVFS give-back' item 7).  Row-vector epilogue through LDS.
 // Tile order is XCD-grouped: the workgroups that share an XCD take consecutive tiles, i.e.
 // the query tiles of one entity panel, so each panel is read from HBM once per XCD.
-#include "common.h"
+#include "mfma16.h"
 
 namespace {
 
-constexpr int BK = 32;
+constexpr int BK = KGE_BK;
 
 template <int BM, int BN, int WM, int WN>
 struct PCfg {
@@ -25,42 +25,11 @@ struct PCfg {
   static_assert(BM % (16 * WM) == 0 && BN % (16 * WN) == 0, "tile");
 };
 
-typedef float f32x4u __attribute__((ext_vector_type(4), aligned(4)));  // 4-B-aligned float4
-
 // ---------------------------------------------------------------------------------------
 // v_mfma_f32_16x16x32_bf16: one MFMA covers the whole BK = 32 stage, per wave
-// (BM/WM/16) x (BN/WN/16) tiles of 16 x 16 (f32x4 accumulators).  The 16x16x32 fragment reads
-// (row = lane & 15, slot = lane >> 4) need another LDS swizzle: slot ^ g((row >> 2) & 3),
-// g = {0, 2, 3, 1}, which puts every ds_read_b128 lane group on 16 distinct 4-bank groups.
-// Epilogue: the four 16 x 16 tiles of a 16-row band go through a padded LDS scratch and
-// leave as 256-B row segments of float4 stores.
-__device__ __forceinline__ int sw16_off(int row, int slot) {
-  return row * 64 + ((slot ^ ((0x78 >> (2 * ((row >> 2) & 3))) & 3)) << 4);
-}
-
-// VMEM issued from inline asm: hipcc neither counts nor waits for these, the kernel does
-// (mixing LDS-DMA with compiler-visible register loads makes hipcc drain vmcnt to 0 at
-// every use of a loaded register, cdna_hip_programming.md 'Projection GEMM' item 4(b)).
-// An asm register load's destination counts as written at the end of the statement, so
-// every path from a load to the next use of its registers must pass a wait statement that
-// names them ("+v") and retires the load: hipcc is otherwise free to reuse the registers
-// (e.g. for an address) while the data is still in flight (cdna_hip_programming.md §5.7).
-typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
-__device__ __forceinline__ void glds16_asm(const void* gsrc, unsigned lds_dst) {
-  unsigned keep;
-  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
-               : "=&s"(keep)
-               : "v"(gsrc), "s"(lds_dst)
-               : "memory");
-}
-__device__ __forceinline__ u32x4 gload16_asm(const void* gsrc) {
-  u32x4 r;
-  asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(r) : "v"(gsrc) : "memory");
-  return r;
-}
-__device__ __forceinline__ unsigned lds_addr(const void* p) {
-  return (unsigned)(uintptr_t)(const __attribute__((address_space(3))) void*)p;
-}
+// (BM/WM/16) x (BN/WN/16) tiles of 16 x 16 (f32x4 accumulators); LDS image, inline-asm VMEM
+// helpers: mfma16.h.  Epilogue: the four 16 x 16 tiles of a 16-row band go through a padded
+// LDS scratch and leave as 256-B row segments of float4 stores.
 
 // ABL: dev-only ablation / probe switches (kge_dev_score_dot_persist): 1 = no score stores,
 // 2 = no staging after the prologue, 4 = per-workgroup clock probe written to row n of s.

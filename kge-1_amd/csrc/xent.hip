@@ -144,18 +144,18 @@ struct RowRegs {
   float4 v[NI][U];
 };
 
-template <int NI>
+template <int NI, int NTH = NT>
 __device__ __forceinline__ void row_load_regs(const float* sr, int m, RowRegs<NI>& r) {
   const int tid = threadIdx.x, m4 = m & ~3;
 #pragma unroll
   for (int i = 0; i < NI; ++i)
 #pragma unroll
     for (int u = 0; u < U; ++u)
-      r.v[i][u] = *reinterpret_cast<const float4*>(sr + min(i * NT * 4 * U + (u * NT + tid) * 4, m4 - 4));
+      r.v[i][u] = *reinterpret_cast<const float4*>(sr + min(i * NTH * 4 * U + (u * NTH + tid) * 4, m4 - 4));
 }
 
-template <int NI>
-__device__ __forceinline__ void row_stats_regs(const float* sr, int m, const RowRegs<NI>& r, float (&red)[3][NT / 64],
+template <int NI, int NTH = NT>
+__device__ __forceinline__ void row_stats_regs(const float* sr, int m, const RowRegs<NI>& r, float (&red)[3][NTH / 64],
                                                float& mx, float& sm, float& rs) {
   const int tid = threadIdx.x, m4 = m & ~3;
   mx = -INFINITY;
@@ -166,7 +166,7 @@ __device__ __forceinline__ void row_stats_regs(const float* sr, int m, const Row
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const float4 v = r.v[i][u];
-      if (i * NT * 4 * U + (u * NT + tid) * 4 >= m4) continue;
+      if (i * NTH * 4 * U + (u * NTH + tid) * 4 >= m4) continue;
       rs += (v.x + v.y) + (v.z + v.w);
       const float vm = fmaxf(fmaxf(v.x, v.y), fmaxf(v.z, v.w));
       const float nm = fmaxf(mx, vm);
@@ -177,7 +177,7 @@ __device__ __forceinline__ void row_stats_regs(const float* sr, int m, const Row
         sm = NAN;
       }
     }
-  for (int j = m4 + tid; j < m; j += NT) {
+  for (int j = m4 + tid; j < m; j += NTH) {
     const float v = sr[j];
     rs += v;
     if (v > mx) {
@@ -203,14 +203,14 @@ __device__ __forceinline__ void row_stats_regs(const float* sr, int m, const Row
   sm = red[1][0];
   rs = red[2][0];
 #pragma unroll
-  for (int w = 1; w < NT / 64; ++w) {
+  for (int w = 1; w < NTH / 64; ++w) {
     lse_merge(mx, sm, red[0][w], red[1][w]);
     rs += red[2][w];
   }
   __syncthreads();
 }
 
-template <int NI>
+template <int NI, int NTH = NT>
 __device__ __forceinline__ void row_grad_regs(const float* sr, float* gr, int m, const RowRegs<NI>& r, float lse,
                                               float a, float b) {
   const int tid = threadIdx.x, m4 = m & ~3;
@@ -218,17 +218,16 @@ __device__ __forceinline__ void row_grad_regs(const float* sr, float* gr, int m,
   for (int i = 0; i < NI; ++i)
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const int j = i * NT * 4 * U + (u * NT + tid) * 4;
+      const int j = i * NTH * 4 * U + (u * NTH + tid) * 4;
       const float4 v = r.v[i][u];
       if (j < m4)
         *reinterpret_cast<float4*>(gr + j) = make_float4(a * __expf(v.x - lse) - b, a * __expf(v.y - lse) - b,
                                                          a * __expf(v.z - lse) - b, a * __expf(v.w - lse) - b);
     }
-  for (int j = m4 + tid; j < m; j += NT) gr[j] = a * __expf(sr[j] - lse) - b;
+  for (int j = m4 + tid; j < m; j += NTH) gr[j] = a * __expf(sr[j] - lse) - b;
 }
 
-__device__ __forceinline__ float block_sum(float v, float* red);
-
+template <int NTH = NT>
 __device__ __forceinline__ float block_sum(float v, float* red) {
   const int tid = threadIdx.x;
 #pragma unroll
@@ -237,7 +236,7 @@ __device__ __forceinline__ float block_sum(float v, float* red) {
   __syncthreads();
   float t = red[0];
 #pragma unroll
-  for (int w = 1; w < NT / 64; ++w) t += red[w];
+  for (int w = 1; w < NTH / 64; ++w) t += red[w];
   __syncthreads();
   return t;
 }
@@ -361,6 +360,144 @@ int launch(const float* s, int64_t lds, int64_t n, int64_t m, const int64_t* l_p
   return 0;
 }
 
+// ---------------------------------------------------------------------------------------
+// The same losses with G written as bf16 hi / lo planes IN PLACE of the score row, for the
+// plane-fed backward GEMMs (gemm_bwd3p.hip): row i of the buffer (lds floats = 4 lds bytes)
+// ends up holding the hi plane of G[i, :] in its first lds bf16 and the lo plane in its
+// second lds bf16 (G ~= hi + lo to 2^-16, the split the GEMMs would otherwise do per tile).
+// Columns [m, lds) of both planes and the rows [n, n_pad) are zeroed: the GEMMs read them as
+// K padding.  The row is held in registers (one read, one write per element); rows up to
+// NI * NTH * 4 * U floats.  Positives are fixed up from the planes themselves: hi + lo
+// reproduces the value to 2^-16 relative, far below the 2^-16 of the products it feeds.
+typedef __bf16 kge_bf16_t;
+
+template <int NI, int NTH>
+__global__ void __launch_bounds__(NTH) softmax_planes_kernel(float* s, int64_t lds, int n, int m,
+                                                             const int64_t* __restrict__ l_ptr,
+                                                             const int64_t* __restrict__ l_col, float eps, float scale,
+                                                             float* __restrict__ loss) {
+  __shared__ float red[3][NTH / 64];
+  const int64_t row = blockIdx.x;
+  float* sr = s + row * lds;
+  const int tid = threadIdx.x;
+  if (row >= n) {  // K-padding rows of both planes
+    for (int64_t j = (int64_t)tid * 4; j < lds; j += (int64_t)NTH * 4)
+      *reinterpret_cast<float4*>(sr + j) = make_float4(0.f, 0.f, 0.f, 0.f);
+    return;
+  }
+  const int m4 = m & ~3;
+  const int64_t p0 = l_ptr ? l_ptr[row] : row, p1 = l_ptr ? l_ptr[row + 1] : row + 1;
+  // every read of the score row happens before the barriers inside row_stats_regs, i.e.
+  // before any thread overwrites the row with the planes
+  float ps = 0.f;
+  for (int64_t k = p0 + tid; k < p1; k += NTH) {
+    const int64_t c = l_col[k];
+    ps += (c >= 0 && c < m) ? sr[c] : NAN;
+  }
+  const float tail = (m4 + tid < m) ? sr[m4 + tid] : 0.f;  // m - m4 <= 3 elements past the float4 part
+  float mx, sm, rs;
+  RowRegs<NI> regs;
+  row_load_regs<NI, NTH>(sr, m, regs);
+  row_stats_regs<NI, NTH>(sr, m, regs, red, mx, sm, rs);
+  ps = block_sum<NTH>(ps, red[0]);
+
+  const float lse = mx + __logf(sm);
+  const int64_t np = p1 - p0;
+  const float u = eps > 0.f ? 1.f / (float)m : 0.f;
+  const float z = (1.f - eps) * (float)np + (eps > 0.f ? 1.f : 0.f);
+  const float zi = z > 1e-12f ? 1.f / z : 0.f;
+  const float t0 = u * zi, t1 = ((1.f - eps) + u) * zi;
+  const float T = z > 0.f ? 1.f : 0.f;
+  if (tid == 0) {
+    if (!l_ptr) {
+      loss[row] = lse - ps;
+    } else {
+      const float H = (float)(m - np) * xlogx(t0) + (float)np * xlogx(t1);
+      loss[row] = H - t0 * rs - (t1 - t0) * ps + (T > 0.f ? lse : 0.f);
+    }
+  }
+  kge_bf16_t* hi = reinterpret_cast<kge_bf16_t*>(sr);
+  kge_bf16_t* lo = hi + lds;
+  const float a = scale * T, b = scale * t0;
+#pragma unroll
+  for (int i = 0; i < NI; ++i)
+#pragma unroll
+    for (int q = 0; q < U; ++q) {
+      const int j = i * NTH * 4 * U + (q * NTH + tid) * 4;
+      if (j >= m4) continue;
+      const float4 v = regs.v[i][q];
+      const float4 gv = make_float4(a * __expf(v.x - lse) - b, a * __expf(v.y - lse) - b, a * __expf(v.z - lse) - b,
+                                    a * __expf(v.w - lse) - b);
+      bf16x4 h, l;
+      split_bf16x4_pk(gv, h, l);
+      *reinterpret_cast<bf16x4*>(hi + j) = h;
+      *reinterpret_cast<bf16x4*>(lo + j) = l;
+    }
+  if (m4 + tid < m) {
+    kge_bf16_t h, l;
+    split_bf16(a * __expf(tail - lse) - b, h, l);
+    hi[m4 + tid] = h;
+    lo[m4 + tid] = l;
+  }
+  for (int64_t j = m + tid; j < lds; j += NTH) {  // K padding columns
+    hi[j] = (kge_bf16_t)0.f;
+    lo[j] = (kge_bf16_t)0.f;
+  }
+  __syncthreads();  // the row's planes are complete before the positives' fix-up
+  const float d = scale * (t1 - t0);
+  for (int64_t k = p0 + tid; k < p1; k += NTH) {
+    const int64_t c = l_col[k];
+    if (c >= 0 && c < m) {
+      kge_bf16_t h, l;
+      split_bf16(((float)hi[c] + (float)lo[c]) - d, h, l);
+      hi[c] = h;
+      lo[c] = l;
+    }
+  }
+}
+
+int launch_planes(float* s, int64_t lds, int64_t n, int64_t n_pad, int64_t m, const int64_t* l_ptr,
+                  const int64_t* l_col, float eps, float scale, float* loss, hipStream_t st) {
+  const int64_t m4 = m & ~3LL;
+  const dim3 grid((unsigned)n_pad);
+  if (m4 <= 256 * 4 * U)
+    softmax_planes_kernel<1, 256><<<grid, dim3(256), 0, st>>>(s, lds, (int)n, (int)m, l_ptr, l_col, eps, scale, loss);
+  else if (m4 <= 2 * 256 * 4 * U)
+    softmax_planes_kernel<2, 256><<<grid, dim3(256), 0, st>>>(s, lds, (int)n, (int)m, l_ptr, l_col, eps, scale, loss);
+  else if (m4 <= 1024 * 4 * U)
+    softmax_planes_kernel<1, 1024><<<grid, dim3(1024), 0, st>>>(s, lds, (int)n, (int)m, l_ptr, l_col, eps, scale, loss);
+  else if (m4 <= 2 * 1024 * 4 * U)
+    softmax_planes_kernel<2, 1024><<<grid, dim3(1024), 0, st>>>(s, lds, (int)n, (int)m, l_ptr, l_col, eps, scale, loss);
+  else
+    return KGE_ERR_ARG;
+  KGE_CHECK_LAUNCH();
+  return 0;
+}
+
+}  // namespace
+
+extern "C" int64_t kge_softmax_planes_max_columns(void) { return 2LL * 1024 * 4 * U; }
+
+extern "C" int kge_softmax_xent_planes(float* s, int64_t lds, int64_t n, int64_t n_pad, int64_t m,
+                                       const int64_t* labels, float scale, float* loss, void* stream) {
+  KGE_REQUIRE(n >= 0 && n_pad >= n && m >= 4 && m <= kge_softmax_planes_max_columns() && n_pad < (1LL << 31));
+  KGE_REQUIRE(s && labels && loss && lds >= m);
+  if (lds % 32 != 0 || !aligned16(s)) return KGE_ERR_ALIGN;
+  if (n_pad == 0) return 0;
+  return launch_planes(s, lds, n, n_pad, m, nullptr, labels, 0.f, scale, loss, as_stream(stream));
+}
+
+extern "C" int kge_softmax_kl_planes(float* s, int64_t lds, int64_t n, int64_t n_pad, int64_t m, const int64_t* l_ptr,
+                                     const int64_t* l_col, float smoothing, float scale, float* loss, void* stream) {
+  KGE_REQUIRE(n >= 0 && n_pad >= n && m >= 4 && m <= kge_softmax_planes_max_columns() && n_pad < (1LL << 31));
+  KGE_REQUIRE(s && l_ptr && l_col && loss && lds >= m);
+  KGE_REQUIRE(smoothing >= 0.f && smoothing < 1.f);
+  if (lds % 32 != 0 || !aligned16(s)) return KGE_ERR_ALIGN;
+  if (n_pad == 0) return 0;
+  return launch_planes(s, lds, n, n_pad, m, l_ptr, l_col, smoothing, scale, loss, as_stream(stream));
+}
+
+namespace {
 }  // namespace
 
 extern "C" int kge_softmax_xent(const float* s, int64_t lds, int64_t n, int64_t m, const int64_t* labels,

@@ -70,6 +70,12 @@ SIGNATURES = {
     "kge_bucket_scatter": ([_P, _I64, _P, _P, _P], _I),
     "kge_stage_i64": ([_P, _P, _I64, _P], _I),
     "kge_rank_hist_multi": ([_P, _P, _I64, _I64, _I, _P, _P, _I64, _P], _I),
+    "kge_softmax_planes_max_columns": ([], _I64),
+    "kge_softmax_xent_planes": ([_P, _I64, _I64, _I64, _I64, _P, _F, _P, _P], _I),
+    "kge_softmax_kl_planes": ([_P, _I64, _I64, _I64, _I64, _P, _P, _F, _F, _P, _P], _I),
+    "kge_score_dot_bwd_q_planes_ws_size": ([_I64, _I64, _I], _I64),
+    "kge_score_dot_bwd_q_planes": ([_P, _P, _I64, _P, _I64, _I64, _I64, _I, _P, _I64, _I, _P, _P, _I64, _P], _I),
+    "kge_score_dot_bwd_t_planes": ([_P, _P, _I64, _P, _P, _I64, _I64, _I64, _I, _P, _I64, _I, _P, _P], _I),
     "kge_softmax_row_stats": ([_P, _I64, _I64, _I64, _I64, _P, _P, _P, _P, _P], _I),
     "kge_softmax_grad": ([_P, _I64, _I64, _I64, _I64, _P, _P, _F, _P, _I64, _P], _I),
 }
@@ -464,6 +470,78 @@ def softmax_kl(s, l_ptr, l_col, smoothing, scale, g=None, loss=None):
     _check(lib().kge_softmax_kl(ptr(s), rows(s), n, m, ptr(l_ptr), ptr(l_col), float(smoothing), float(scale),
                                 ptr(loss), ptr(g), rows(g) if g is not None else 0, stream()), "kge_softmax_kl")
     return loss
+
+
+# ---- the fused loss with its gradient as bf16 planes, and the GEMMs that read them
+
+
+class GradPlanes:
+    """dL/dS of a fused loss as bf16 hi / lo planes living in the score buffer itself
+    (kge_softmax_*_planes): buf is the fp32 [n_pad, ld] buffer the scores were written to."""
+
+    def __init__(self, buf: torch.Tensor, n: int, m: int):
+        self.buf, self.n, self.m = buf, n, m
+        self.n_pad, self.ld = buf.shape
+        flat = buf.view(torch.bfloat16)  # [n_pad, 2 ld]: hi plane | lo plane per row
+        self.hi, self.lo = flat[:, :self.ld], flat[:, self.ld:]
+        self.ldgp = 2 * self.ld
+
+
+def planes_layout(n: int, m: int):
+    """(rows, leading dimension) of the score buffer when its gradient is to be left as
+    planes: rows padded to the GEMMs' K stage (32), columns to 32."""
+    return (n + 31) // 32 * 32, (m + 31) // 32 * 32
+
+
+def planes_ok(m: int) -> bool:
+    return 4 <= m <= lib().kge_softmax_planes_max_columns()
+
+
+def softmax_planes(buf, n, m, labels, l_ptr, smoothing, scale) -> tuple:
+    """Per-row losses [n] of the scores in buf[:n, :m]; the buffer is left holding the
+    gradient planes (GradPlanes).  l_ptr None: index labels (cross entropy), else CSR positives."""
+    require_device(buf)
+    labels, l_ptr = idx64(labels), idx64(l_ptr)
+    n_pad, ld = buf.shape
+    if l_ptr is None:
+        check_index(labels, m, "label")
+    else:
+        if l_ptr.numel() != n + 1:
+            raise ValueError(f"l_ptr has {l_ptr.numel()} entries, expected {n + 1}")
+        check_index(labels, m, "label column")
+    loss = torch.empty(n, device=buf.device, dtype=torch.float32)
+    if l_ptr is None:
+        _check(lib().kge_softmax_xent_planes(ptr(buf), ld, n, n_pad, m, ptr(labels), float(scale), ptr(loss),
+                                             stream()), "kge_softmax_xent_planes")
+    else:
+        _check(lib().kge_softmax_kl_planes(ptr(buf), ld, n, n_pad, m, ptr(l_ptr), ptr(labels), float(smoothing),
+                                           float(scale), ptr(loss), stream()), "kge_softmax_kl_planes")
+    return loss, GradPlanes(buf, n, m)
+
+
+def score_dot_bwd_q_planes(gp: GradPlanes, t, gscale=None, dq=None, accumulate=False):
+    """dq (+)= gscale * G . t from gradient planes (kge_score_dot_bwd_q_planes)."""
+    n, m, d = gp.n, gp.m, t.shape[1]
+    if dq is None:
+        dq = torch.empty(n, d, device=t.device, dtype=torch.float32)
+        accumulate = False
+    ws_n = lib().kge_score_dot_bwd_q_planes_ws_size(n, m, d)
+    ws = torch.empty(ws_n, device=t.device, dtype=torch.float32)
+    _check(lib().kge_score_dot_bwd_q_planes(ptr(gp.hi), ptr(gp.lo), gp.ldgp, ptr(t), rows(t), n, m, d, ptr(dq),
+                                            rows(dq), int(accumulate), ptr(gscale), ptr(ws), ws_n, stream()),
+           "kge_score_dot_bwd_q_planes")
+    return dq
+
+
+def score_dot_bwd_t_planes(gp: GradPlanes, q_hi, q_lo, dt, gscale=None, accumulate=False):
+    """dt (+)= gscale * G^T . Q from gradient planes and query planes whose rows
+    [n, n_pad) are zero (kge_score_dot_bwd_t_planes)."""
+    if q_hi.shape[0] < gp.n_pad or q_lo.shape[0] < gp.n_pad or q_hi.stride(0) != q_lo.stride(0):
+        raise ValueError("query planes must hold n_pad rows (zero past n) with equal row strides")
+    _check(lib().kge_score_dot_bwd_t_planes(ptr(gp.hi), ptr(gp.lo), gp.ldgp, ptr(q_hi), ptr(q_lo), q_hi.stride(0),
+                                            gp.n_pad, gp.m, dt.shape[1], ptr(dt), rows(dt), int(accumulate),
+                                            ptr(gscale), stream()), "kge_score_dot_bwd_t_planes")
+    return dt
 
 
 def stage_i64(src_pinned, dst):

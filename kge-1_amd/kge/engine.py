@@ -163,6 +163,80 @@ class _ScoreXent(torch.autograd.Function):
         return None, None, None, None, d_ent, None, d_rel, None, d_tab, None, None, None, None, None
 
 
+class _ScoreXentPlanes(torch.autograd.Function):
+    """The fused loss of one or two query batches against every row of the entity table with
+    its gradient kept as bf16 hi / lo PLANES (bf16x3 precision): the queries of all parts are
+    prepared straight into one block of hi / lo planes, one contraction writes the scores, the
+    loss kernel turns them in place into the planes of G = scale * dloss/dS, and the backward
+    GEMMs read G and Q from those planes by LDS-DMA (kge_score_dot_bwd_q_planes /
+    _t_planes): no fp32 copy of Q, no split per tile, dT written (not accumulated).
+    Returns (total, parts): total = scale * sum of all rows' losses carries the gradient;
+    parts[k] = scale * sum of part k's rows is a detached view for reporting."""
+
+    @staticmethod
+    def forward(ctx, kind, ent, rel, parts, labels, l_ptr, smoothing, scale):
+        ent, rel = _rows(ent), _rows(rel)
+        sizes = [p[1].numel() for p in parts]
+        n, m = sum(sizes), ent.shape[0]
+        d_e, d_r = ent.shape[1], rel.shape[1]
+        qw, tab_w = L.query_width(kind, d_e), window(kind, parts[0][0], ent)
+        n_pad, ld = L.planes_layout(n, m)
+        buf = torch.empty(n_pad, ld, device=ent.device, dtype=torch.float32)
+        ldp = (qw + 31) // 32 * 32
+        hi = torch.empty(n_pad, ldp, device=ent.device, dtype=torch.bfloat16)
+        lo = torch.empty_like(hi)
+        if n_pad > n:  # K padding of the dT GEMM
+            hi[n:].zero_()
+            lo[n:].zero_()
+        r0 = 0
+        for (dr, ei, ri), k in zip(parts, sizes):
+            L.prep_query_split(kind, dr, ent, ei, rel, ri, k, d_e, d_r, out=(None, hi[r0:r0 + k], lo[r0:r0 + k]))
+            r0 += k
+        _timed(L.score_dot_split, hi[:n], lo[:n], tab_w, None, qw, out=buf[:n, :m])
+        loss_rows, _ = L.softmax_planes(buf, n, m, labels, l_ptr, smoothing, scale)
+        ctx.meta = (kind, n, m, d_e, d_r, [(p[0], k) for p, k in zip(parts, sizes)])
+        ctx.save_for_backward(ent, rel, hi, lo, buf, *[t for p in parts for t in p[1:]])
+        if len(parts) == 2 and sizes[0] == sizes[1]:
+            per_part = loss_rows.view(2, sizes[0]).sum(1) * scale
+        else:
+            per_part = torch.stack([c.sum() for c in loss_rows.split(sizes)]) * scale
+        total = per_part.sum()
+        ctx.mark_non_differentiable(per_part)
+        return total, per_part
+
+    @staticmethod
+    def backward(ctx, g_total, _g_parts):
+        kind, n, m, d_e, d_r, parts = ctx.meta
+        ent, rel, hi, lo, buf, *idx = ctx.saved_tensors
+        gl = g_total.reshape(1).float().contiguous()  # read by the kernels from device memory
+        gp = L.GradPlanes(buf, n, m)
+        tab_w = window(kind, parts[0][0], ent)
+        dq = L.score_dot_bwd_q_planes(gp, tab_w, gscale=gl)
+        if tab_w.shape[1] == d_e:  # the GEMM covers every column: write, do not accumulate
+            d_ent = torch.empty_like(ent)
+            L.score_dot_bwd_t_planes(gp, hi, lo, d_ent, gscale=gl, accumulate=False)
+        else:  # CP: the contraction sees one half of the entity rows
+            d_ent = torch.zeros_like(ent)
+            L.score_dot_bwd_t_planes(gp, hi, lo, window(kind, parts[0][0], d_ent), gscale=gl, accumulate=False)
+        d_rel = torch.zeros_like(rel)
+        r0 = 0
+        for i, (dr, k) in enumerate(parts):
+            L.prep_query_bwd(kind, dr, ent, idx[2 * i], rel, idx[2 * i + 1], k, d_e, d_r, dq[r0:r0 + k], d_ent, d_rel)
+            r0 += k
+        return (None, d_ent if ctx.needs_input_grad[1] else None, d_rel if ctx.needs_input_grad[2] else None,
+                None, None, None, None, None)
+
+
+def _planes_applicable(kind, precision, ent, direction) -> bool:
+    """Whether the plane-fed fused loss serves this scorer: bf16x3, a bilinear model, layouts
+    the split contraction and the DMA-staged GEMMs take, rows the loss kernel holds in registers."""
+    if kind not in BILINEAR or precision != L.PREC_BF16X3 or ent.dim() != 2 or ent.stride(1) != 1:
+        return False
+    qw, tab_w = L.query_width(kind, ent.shape[1]), window(kind, direction, ent)
+    return (L.split_ok(qw, tab_w, precision) and L.planes_ok(ent.shape[0]) and ent.shape[1] % 4 == 0
+            and qw % 8 == 0 and ent.data_ptr() % 16 == 0)
+
+
 def score_all_xent(kind: int, direction: int, precision: int, l_norm: float, ent: torch.Tensor,
                    eidx: Optional[torch.Tensor], rel: torch.Tensor, ridx: Optional[torch.Tensor],
                    tab: torch.Tensor, tidx: Optional[torch.Tensor], labels: torch.Tensor,
@@ -175,6 +249,10 @@ def score_all_xent(kind: int, direction: int, precision: int, l_norm: float, ent
                   the smoothed, L1-normalised label row -- the KvsAll objective
                   (kge/util/loss.py:209-213; kge/job/train.py:715-721, 744-751)."""
     L.require_device(ent, rel, tab)
+    if tab is ent and tidx is None and eidx is not None and _planes_applicable(kind, precision, ent, direction):
+        total, _ = _ScoreXentPlanes.apply(kind, ent, rel, [(direction, L.idx64(eidx), L.idx64(ridx))], L.idx64(labels),
+                                          L.idx64(l_ptr), float(smoothing), float(scale))
+        return total
     return _ScoreXent.apply(kind, direction, precision, float(l_norm), ent, L.idx64(eidx), rel, L.idx64(ridx),
                             tab, L.idx64(tidx), L.idx64(labels), L.idx64(l_ptr), float(smoothing), float(scale))
 
@@ -222,24 +300,22 @@ class _ScoreXent2(torch.autograd.Function):
         ctx.meta = (kind, precision, n_a, n, d_e, d_r, dir_a, dir_b)
         ctx.save_for_backward(ent, rel, eidx_a, ridx_a, eidx_b, ridx_b, q if q is not None else s.new_empty(0), s)
         if 2 * n_a == n:  # equal parts (1vsAll): one reduction for both sums
-            return loss_rows.view(2, n_a).sum(1) * scale
-        return torch.stack((loss_rows[:n_a].sum(), loss_rows[n_a:].sum())) * scale
+            per_part = loss_rows.view(2, n_a).sum(1) * scale
+        else:
+            per_part = torch.stack((loss_rows[:n_a].sum(), loss_rows[n_a:].sum())) * scale
+        total = per_part.sum()
+        ctx.mark_non_differentiable(per_part)
+        return total, per_part
 
     @staticmethod
-    def backward(ctx, gl):
+    def backward(ctx, gl, _g_parts):
         kind, precision, n_a, n, d_e, d_r, dir_a, dir_b = ctx.meta
         ent, rel, eidx_a, ridx_a, eidx_b, ridx_b, q, g = ctx.saved_tensors
         tab_w = window(kind, dir_a, ent)
-        # dL/dS = gl[part] * G on each part's rows: folded into the [n, d] operands
+        # dL/dS = gl * G: the scalar is folded into the [n, d] operands
         dq = L.score_dot_bwd_q(g, tab_w, None, precision)
-        if 2 * n_a == n:  # equal parts: broadcast the two factors (no row-scale vector)
-            gl3 = gl.view(2, 1, 1)
-            dq.view(2, n_a, -1).mul_(gl3)
-            q_s = (q.view(2, n_a, -1) * gl3).view(n, -1)
-        else:
-            row_scale = torch.cat((gl[0].expand(n_a), gl[1].expand(n - n_a)))[:, None]
-            dq.mul_(row_scale)
-            q_s = q * row_scale
+        dq.mul_(gl)
+        q_s = q * gl
         if tab_w.shape[1] == d_e:  # the GEMM covers every column: write, do not accumulate
             d_ent = torch.empty_like(ent)
             L.score_dot_bwd_t(g, q_s, None, d_ent, precision, accumulate=False)
@@ -254,17 +330,29 @@ class _ScoreXent2(torch.autograd.Function):
 
 
 def score_all_xent2(kind: int, precision: int, ent: torch.Tensor, rel: torch.Tensor, part_a, part_b, scale: float,
-                    smoothing: float = 0.0) -> Optional[torch.Tensor]:
-    """[scale * sum of part a's per-row losses, the same for part b]: two query batches scored
-    against every row of ent in one engine pass (see _ScoreXent2).  part = (direction, eidx, ridx, labels, l_ptr) with the
-    label conventions of score_all_xent (both parts index labels, or both CSR).  None when
-    the batches cannot share one contraction (distance models; CP queries of different
-    directions contract different halves of the rows) -- the caller runs them separately."""
+                    smoothing: float = 0.0):
+    """Two query batches scored against every row of ent in ONE engine pass (the sp_ and _po
+    halves of a 1vsAll / KvsAll step).  Returns (total, parts): total = scale * sum of both
+    parts' per-row losses, a 0-dim tensor that backpropagates into ent / rel; parts = the two
+    parts' shares of it, detached (for reporting).  part = (direction, eidx, ridx, labels,
+    l_ptr) with the label conventions of score_all_xent (both parts index labels, or both
+    CSR).  None when the batches cannot share one contraction (distance models; CP queries
+    of different directions contract different halves of the rows) -- the caller runs them
+    separately."""
     dir_a, eidx_a, ridx_a, lab_a, lptr_a = part_a
     dir_b, eidx_b, ridx_b, lab_b, lptr_b = part_b
     if kind not in BILINEAR or (kind == L.CP and dir_a != dir_b) or (lptr_a is None) != (lptr_b is None):
         return None
     L.require_device(ent, rel)
+    if _planes_applicable(kind, precision, ent, dir_a):
+        lab = torch.cat((L.idx64(lab_a), L.idx64(lab_b)))
+        l_ptr = None
+        if lptr_a is not None:
+            lptr_a, lptr_b = L.idx64(lptr_a), L.idx64(lptr_b)
+            l_ptr = torch.cat((lptr_a[:-1], lptr_b + lptr_a[-1]))
+        return _ScoreXentPlanes.apply(kind, ent, rel, [(dir_a, L.idx64(eidx_a), L.idx64(ridx_a)),
+                                                       (dir_b, L.idx64(eidx_b), L.idx64(ridx_b))],
+                                      lab, l_ptr, float(smoothing), float(scale))
     return _ScoreXent2.apply(kind, precision, ent, rel, dir_a, L.idx64(eidx_a), L.idx64(ridx_a), L.idx64(lab_a),
                              L.idx64(lptr_a), dir_b, L.idx64(eidx_b), L.idx64(ridx_b), L.idx64(lab_b),
                              L.idx64(lptr_b), float(smoothing), float(scale))

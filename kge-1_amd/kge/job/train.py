@@ -387,9 +387,9 @@ class TrainingJob1vsAll(TrainingJob):
         fwd = -time.time()
         both = self.model.score_sp_po_xent(cols[S], cols[P], cols[O], 1.0 / bs) if fused else None
         if both is not None:  # sp_ and _po in one engine pass; one backward (same gradient sum)
+            total, _ = both
             fwd += time.time()
             bwd = -time.time()
-            total = both.sum()
             total.backward()
             bwd += time.time()
             return TrainingJob._ProcessBatchResult(total.detach(), bs, t, fwd, bwd)
@@ -610,7 +610,8 @@ class TrainingJobKvsAll(TrainingJob):
         fwd += time.time()
         if losses is None:
             return None
+        total, per_type = losses
         bwd = -time.time()
-        losses.sum().backward()
+        total.backward()
         bwd += time.time()
-        return TrainingJob._ProcessBatchResult(losses[1].detach(), bs, t, fwd, bwd)
+        return TrainingJob._ProcessBatchResult(per_type[1], bs, t, fwd, bwd)

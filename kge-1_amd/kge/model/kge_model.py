@@ -160,8 +160,9 @@ class RelationalScorer(KgeBase):
     def score_lookup_xent2(self, ent: Tensor, rel: Tensor, part_a, part_b, scale: float,
                            smoothing: float = 0.0) -> Optional[Tensor]:
         """Both halves of a training step in one engine pass: part = (direction "sp_" / "_po",
-        e_idx, p_idx, labels, l_ptr).  Returns [loss_a, loss_b] (see engine.score_all_xent2),
-        or None when this scorer cannot share one contraction between the parts."""
+        e_idx, p_idx, labels, l_ptr).  Returns (total, [loss_a, loss_b] detached) (see
+        engine.score_all_xent2), or None when this scorer cannot share one contraction between
+        the parts."""
         from .. import engine, _lib
 
         if self.engine_kind is None:
@@ -398,16 +399,18 @@ class KgeModel(KgeBase):
         return ("_po", o, p, labels, l_ptr)
 
     def score_xent_parts(self, part_a, part_b, scale: float, smoothing: float = 0.0) -> Optional[Tensor]:
-        """[loss_a, loss_b] of two query batches (xent_part_sp / xent_part_po) in one engine
-        pass; None when not fusable (the caller then runs score_*_xent / score_*_kl)."""
+        """(total, [loss_a, loss_b]) of two query batches (xent_part_sp / xent_part_po) in one
+        engine pass: total = loss_a + loss_b carries the gradient, the pair is detached (for
+        reporting); None when not fusable (the caller then runs score_*_xent / score_*_kl)."""
         tabs = self._lookup_tables()
         if tabs is None:
             return None
         return self._scorer.score_lookup_xent2(tabs[0], tabs[1], part_a, part_b, scale, smoothing)
 
     def score_sp_po_xent(self, s: Tensor, p: Tensor, o: Tensor, scale: float) -> Optional[Tensor]:
-        """[score_sp_xent(s, p, o, scale), score_po_xent(p, o, s, scale)] in one engine pass
-        (the two losses of a 1vsAll step, train.py:1041-1057), or None."""
+        """score_sp_xent(s, p, o, scale) + score_po_xent(p, o, s, scale) in one engine pass (the two
+        losses of a 1vsAll step, train.py:1041-1057) as (total, [sp part, po part] detached), or
+        None."""
         return self.score_xent_parts(self.xent_part_sp(s, p, o), self.xent_part_po(p, o, s), scale)
 
     def score_sp_cand(self, s: Tensor, p: Tensor, cand: Tensor) -> Optional[Tensor]:

@@ -1,0 +1,48 @@
+"""Dev timing: plane-fed backward GEMMs and loss kernel vs the fp32-G kernels at the stacked
+C2 training shape (2,048 queries x 14,541 entities x 512); interleaved rounds in one process."""
+import sys
+import os as _os; _R = _os.path.dirname(_os.path.dirname(_os.path.dirname(_os.path.abspath(__file__)))); sys.path.insert(0, _R); sys.path.insert(0, _os.path.join(_R, 'kge-1_amd'))
+import numpy as np, torch
+from kge import _lib as L
+n, m, d = (int(x) for x in (sys.argv[1:4] if len(sys.argv) > 3 else (2048, 14541, 512)))
+torch.manual_seed(0)
+ent = (torch.randn(m, d) * 0.1).cuda()
+q = (torch.randn(n, d) * 0.1).cuda()
+labels = torch.randint(0, m, (n,)).cuda()
+n_pad, ld = L.planes_layout(n, m)
+S = torch.randn(n_pad, ld, device="cuda")
+bufp = S.clone()
+_, gp = L.softmax_planes(bufp, n, m, labels, None, 0.0, 1.0 / n)
+buf4 = torch.empty(n, (m + 3) // 4 * 4, device="cuda"); s4 = buf4[:, :m]; s4.copy_(S[:n, :m])
+L.softmax_xent(s4, labels, 1.0 / n, g=s4)
+ldp = (d + 31) // 32 * 32
+qh = torch.zeros(n_pad, ldp, device="cuda", dtype=torch.bfloat16); ql = torch.zeros_like(qh)
+h, l = L.split_rows(q); qh[:n], ql[:n] = h, l
+dq = torch.empty(n, d, device="cuda"); de = torch.empty(m, d, device="cuda")
+src_p = S.clone(); src_4 = buf4.clone()
+def t_loss_planes():
+    bufp.copy_(src_p); 
+def run(name, fn, reps=20):
+    for _ in range(3): fn()
+    a = torch.cuda.Event(enable_timing=True); b = torch.cuda.Event(enable_timing=True)
+    a.record()
+    for _ in range(reps): fn()
+    b.record(); torch.cuda.synchronize()
+    return a.elapsed_time(b) / reps * 1e3
+variants = {
+    "dQ old (fp32 G, ws)": lambda: L.score_dot_bwd_q(s4, ent, None, L.PREC_BF16X3, dq=dq),
+    "dQ planes": lambda: L.score_dot_bwd_q_planes(gp, ent, dq=dq),
+    "dE old (fp32 G)": lambda: L.score_dot_bwd_t(s4, q, None, de, L.PREC_BF16X3, accumulate=False),
+    "dE planes": lambda: L.score_dot_bwd_t_planes(gp, qh, ql, de),
+    "loss old (in place fp32)": lambda: L.softmax_xent(s4, labels, 1.0 / n, g=s4),
+    "loss planes": lambda: L.softmax_planes(bufp, n, m, labels, None, 0.0, 1.0 / n),
+}
+res = {k: [] for k in variants}
+for r in range(5):
+    for k, fn in variants.items():
+        res[k].append(run(k, fn))
+for k, v in res.items():
+    print(f"{k:28s} {np.median(v):8.1f} us  (min {min(v):.1f})")
+flops = 2.0 * n * m * d
+for k in ("dQ planes", "dE planes", "dQ old (fp32 G, ws)", "dE old (fp32 G)"):
+    print(f"{k:28s} {flops / np.median(res[k]) / 1e6:6.1f} TF/s = {flops / np.median(res[k]) / 1e6 / 833.3:.3f} of the bf16x3 peak")

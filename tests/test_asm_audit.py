@@ -21,7 +21,8 @@ FLAGS = ["-O3", "-std=c++17", "--offload-arch=gfx950", "-munsafe-fp-atomics", "-
 
 
 @pytest.mark.parametrize("src,kernel,dev", [("score_dot3.hip", "score_dot_persist16_kernel", False),
-                                            ("score_dot3.hip", "score_dot_persist16_kernel", True)])
+                                            ("score_dot3.hip", "score_dot_persist16_kernel", True),
+                                            ("gemm_bwd3p.hip", "bwd3p_q_kernel", False)])
 def test_inline_asm_loads_are_retired_before_use(tmp_path, src, kernel, dev):
     if not os.path.exists(HIPCC):
         pytest.skip("no hipcc")

@@ -290,17 +290,18 @@ def test_fused_xent2_matches_separate(fn, prec):
             if both is None:
                 assert meta["model"] in K.DISTANCE or meta["model"] == "cp"
                 pytest.skip("not fusable across directions")
-            l_sp, l_po = both[0], both[1]
-            (both * torch.tensor([0.75, 1.25], device="cuda")).sum().backward()  # unequal upstream grads
+            total, (l_sp, l_po) = both
+            assert not l_sp.requires_grad and abs(total.item() - (l_sp + l_po).item()) <= 1e-6 * abs(total.item())
+            (0.75 * total).backward()  # an upstream gradient other than 1
         else:
             l_sp, l_po = m.score_sp_xent(s, p, o, 1.0 / B), m.score_po_xent(p, o, s, 1.0 / B)
-            (0.75 * l_sp + 1.25 * l_po).backward()
+            (0.75 * (l_sp + l_po)).backward()
         res.append((l_sp.item(), l_po.item(), m._entity_embedder._embeddings.weight.grad.cpu().numpy(),
                     m._relation_embedder._embeddings.weight.grad.cpu().numpy()))
     (a1, b1, ge1, gr1), (a0, b0, ge0, gr0) = res
     assert abs(a1 - a0) <= 1e-5 * abs(a0) and abs(b1 - b0) <= 1e-5 * abs(b0)
-    assert np.abs(ge1 - ge0).max() <= 1e-5 * np.abs(ge0).max()
-    assert np.abs(gr1 - gr0).max() <= 1e-5 * np.abs(gr0).max()
+    assert np.abs(ge1 - ge0).max() <= 2e-5 * np.abs(ge0).max()
+    assert np.abs(gr1 - gr0).max() <= 2e-5 * np.abs(gr0).max()
 
 
 def test_reciprocal_fused_xent():
@@ -324,7 +325,8 @@ def test_reciprocal_fused_xent():
     fused = m.score_po_xent(p, o, s, 0.5)
     ref = torch.nn.CrossEntropyLoss(reduction="sum")(m.score_po(p, o), s) * 0.5
     assert abs(fused.item() - ref.item()) <= 1e-5 * abs(ref.item())
-    both = m.score_sp_po_xent(s, p, o, 0.5)  # both halves as "sp_" queries in one pass
+    total, both = m.score_sp_po_xent(s, p, o, 0.5)  # both halves as "sp_" queries in one pass
     ref_sp = torch.nn.CrossEntropyLoss(reduction="sum")(m.score_sp(s, p), o) * 0.5
     assert abs(both[0].item() - ref_sp.item()) <= 1e-5 * abs(ref_sp.item())
     assert abs(both[1].item() - ref.item()) <= 1e-5 * abs(ref.item())
+    assert abs(total.item() - (ref_sp + ref).item()) <= 1e-5 * abs(total.item())
