@@ -251,6 +251,12 @@ int kge_softmax_xent_planes(float* s, int64_t lds, int64_t n, int64_t n_pad, int
 int kge_softmax_kl_planes(float* s, int64_t lds, int64_t n, int64_t n_pad, int64_t m, const int64_t* l_ptr,
                           const int64_t* l_col, float smoothing, float scale, float* loss, void* stream);
 
+/* The per-row losses of a fused two-part step reduced in one launch, in a fixed order:
+ * parts[0] = scale * sum loss[0 .. n_first), parts[1] = scale * sum loss[n_first .. n),
+ * total[0] = parts[0] + parts[1]  (the sp_ and _po losses of train.py:1042-1053 and their sum). */
+int kge_loss_sums(const float* loss, int64_t n, int64_t n_first, float scale, float* parts, float* total,
+                  void* stream);
+
 /* Vocab-parallel 1vsAll (entity table row-sharded): S holds columns
  * [c0, c0 + m) of the full score rows, labels are global column ids.
  * row_stats: row_max[i], row_sumexp[i] = sum_j exp(S[i, j] - row_max[i]) over the slice, and

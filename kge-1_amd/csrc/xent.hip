@@ -474,7 +474,38 @@ int launch_planes(float* s, int64_t lds, int64_t n, int64_t n_pad, int64_t m, co
   return 0;
 }
 
+// parts[0] = scale * sum of loss[0 .. n_first), parts[1] = scale * sum of loss[n_first .. n),
+// total[0] = parts[0] + parts[1]: one workgroup, fixed summation order (deterministic).
+__global__ void __launch_bounds__(256) loss_sums_kernel(const float* __restrict__ loss, int64_t n, int64_t n_first,
+                                                        float scale, float* __restrict__ parts,
+                                                        float* __restrict__ total) {
+  __shared__ float red[256 / 64];
+  float a = 0.f, b = 0.f;
+  for (int64_t i = threadIdx.x; i < n; i += 256) {
+    const float v = loss[i];
+    if (i < n_first)
+      a += v;
+    else
+      b += v;
+  }
+  a = block_sum<256>(a, red) * scale;
+  b = block_sum<256>(b, red) * scale;
+  if (threadIdx.x == 0) {
+    parts[0] = a;
+    parts[1] = b;
+    total[0] = a + b;
+  }
+}
+
 }  // namespace
+
+extern "C" int kge_loss_sums(const float* loss, int64_t n, int64_t n_first, float scale, float* parts, float* total,
+                             void* stream) {
+  KGE_REQUIRE(n >= 0 && n_first >= 0 && n_first <= n && (loss || n == 0) && parts && total);
+  loss_sums_kernel<<<dim3(1), dim3(256), 0, as_stream(stream)>>>(loss, n, n_first, scale, parts, total);
+  KGE_CHECK_LAUNCH();
+  return 0;
+}
 
 extern "C" int64_t kge_softmax_planes_max_columns(void) { return 2LL * 1024 * 4 * U; }
 
@@ -496,9 +527,6 @@ extern "C" int kge_softmax_kl_planes(float* s, int64_t lds, int64_t n, int64_t n
   if (n_pad == 0) return 0;
   return launch_planes(s, lds, n, n_pad, m, l_ptr, l_col, smoothing, scale, loss, as_stream(stream));
 }
-
-namespace {
-}  // namespace
 
 extern "C" int kge_softmax_xent(const float* s, int64_t lds, int64_t n, int64_t m, const int64_t* labels,
                                 float scale, float* loss, float* g, int64_t ldg, void* stream) {

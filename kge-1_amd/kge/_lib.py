@@ -76,6 +76,7 @@ SIGNATURES = {
     "kge_score_dot_bwd_q_planes_ws_size": ([_I64, _I64, _I], _I64),
     "kge_score_dot_bwd_q_planes": ([_P, _P, _I64, _P, _I64, _I64, _I64, _I, _P, _I64, _I, _P, _P, _I64, _P], _I),
     "kge_score_dot_bwd_t_planes": ([_P, _P, _I64, _P, _P, _I64, _I64, _I64, _I, _P, _I64, _I, _P, _P], _I),
+    "kge_loss_sums": ([_P, _I64, _I64, _F, _P, _P, _P], _I),
     "kge_softmax_row_stats": ([_P, _I64, _I64, _I64, _I64, _P, _P, _P, _P, _P], _I),
     "kge_softmax_grad": ([_P, _I64, _I64, _I64, _I64, _P, _P, _F, _P, _I64, _P], _I),
 }
@@ -517,6 +518,25 @@ def softmax_planes(buf, n, m, labels, l_ptr, smoothing, scale) -> tuple:
         _check(lib().kge_softmax_kl_planes(ptr(buf), ld, n, n_pad, m, ptr(l_ptr), ptr(labels), float(smoothing),
                                            float(scale), ptr(loss), stream()), "kge_softmax_kl_planes")
     return loss, GradPlanes(buf, n, m)
+
+
+def loss_sums(loss_rows, n_first, scale):
+    """(total [0-dim], parts [2]) = scale * sums of the per-row losses, split at row n_first."""
+    parts = torch.empty(2, device=loss_rows.device, dtype=torch.float32)
+    total = torch.empty((), device=loss_rows.device, dtype=torch.float32)
+    _check(lib().kge_loss_sums(ptr(loss_rows), loss_rows.numel(), int(n_first), float(scale), ptr(parts), ptr(total),
+                               stream()), "kge_loss_sums")
+    return total, parts
+
+
+def adjacent_or_cat(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
+    """cat((a, b)) of two 1-D tensors -- without a copy when b already follows a in memory
+    (rows of one index block)."""
+    if (a.dtype == b.dtype and a.is_contiguous() and b.is_contiguous()
+            and a.untyped_storage().data_ptr() == b.untyped_storage().data_ptr()
+            and b.storage_offset() == a.storage_offset() + a.numel()):
+        return a.as_strided((a.numel() + b.numel(),), (1,))
+    return torch.cat((a, b))
 
 
 def score_dot_bwd_q_planes(gp: GradPlanes, t, gscale=None, dq=None, accumulate=False):

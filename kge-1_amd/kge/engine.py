@@ -196,16 +196,17 @@ class _ScoreXentPlanes(torch.autograd.Function):
         loss_rows, _ = L.softmax_planes(buf, n, m, labels, l_ptr, smoothing, scale)
         ctx.meta = (kind, n, m, d_e, d_r, [(p[0], k) for p, k in zip(parts, sizes)])
         ctx.save_for_backward(ent, rel, hi, lo, buf, *[t for p in parts for t in p[1:]])
-        if len(parts) == 2 and sizes[0] == sizes[1]:
-            per_part = loss_rows.view(2, sizes[0]).sum(1) * scale
-        else:
-            per_part = torch.stack([c.sum() for c in loss_rows.split(sizes)]) * scale
-        total = per_part.sum()
+        total, per_part = L.loss_sums(loss_rows, sizes[0], scale)  # one launch, fixed order
+        if len(parts) == 1:
+            per_part = per_part[:1]
         ctx.mark_non_differentiable(per_part)
+        ctx.set_materialize_grads(False)  # no zero tensor for the detached parts' gradient
         return total, per_part
 
     @staticmethod
     def backward(ctx, g_total, _g_parts):
+        if g_total is None:
+            return (None,) * 8
         kind, n, m, d_e, d_r, parts = ctx.meta
         ent, rel, hi, lo, buf, *idx = ctx.saved_tensors
         gl = g_total.reshape(1).float().contiguous()  # read by the kernels from device memory
@@ -345,7 +346,7 @@ def score_all_xent2(kind: int, precision: int, ent: torch.Tensor, rel: torch.Ten
         return None
     L.require_device(ent, rel)
     if _planes_applicable(kind, precision, ent, dir_a):
-        lab = torch.cat((L.idx64(lab_a), L.idx64(lab_b)))
+        lab = L.adjacent_or_cat(L.idx64(lab_a), L.idx64(lab_b))
         l_ptr = None
         if lptr_a is not None:
             lptr_a, lptr_b = L.idx64(lptr_a), L.idx64(lptr_b)

@@ -261,7 +261,7 @@ class _GraphStep:
     def __init__(self, job: "TrainingJob"):
         self.job = job
         self.graph = None
-        self.static = None  # recorded [B, 3] int64 device index buffer
+        self.static = None  # recorded [4, B] int64 device index block (s, p, o, s)
         self.pinned = []  # two pinned host staging buffers (+ their copy events) for the batch
         self.turn = 0
         self.loss = None  # recorded 0-dim loss
@@ -298,7 +298,7 @@ class _GraphStep:
             self.turn ^= 1
             if slot[1] is not None:
                 slot[1].synchronize()
-            slot[0].copy_(triples)
+            self._fill(slot[0], triples)
             _lib.stage_i64(slot[0], self.static)  # a kernel, not a DMA copy, on this stream
             slot[1] = torch.cuda.Event()
             slot[1].record()
@@ -307,16 +307,24 @@ class _GraphStep:
         t += time.time()
         return TrainingJob._ProcessBatchResult(self.loss, triples.shape[0], 0.0, t, 0.0)
 
+    @staticmethod
+    def _fill(block, triples):
+        """[B, 3] host triples -> the [4, B] index block s, p, o, s."""
+        block[:3].copy_(triples.t())
+        block[3].copy_(triples[:, 0])
+
     def _record(self, batch_index, triples) -> bool:
         job = self.job
         opt = job.optimizer
         steps = {p: st["step"].clone() for p, st in opt.state.items() if "step" in st}
-        self.static = triples.to(job.device).long()
+        host = torch.empty(4, triples.shape[0], dtype=torch.int64)
+        self._fill(host, triples.long())
+        self.static = host.to(job.device)
         opt.zero_grad(set_to_none=True)
         g = torch.cuda.CUDAGraph()
         try:
             with torch.cuda.graph(g):
-                res = job.process_batch(batch_index, {"triples": self.static})
+                res = job.process_batch(batch_index, {"cols": self.static})
                 opt.step()
         except Exception as e:  # not recordable: this and every later batch run eagerly
             for p, s in steps.items():
@@ -346,6 +354,7 @@ class TrainingJob1vsAll(TrainingJob):
         self.type_str = "1vsAll"
         self._graph_step = None
         self._sharded = None
+        self._one = None
         #: compute ops of the row-sharded path; None: the engine (kge.sharded.EngineOps).
         #: Tests inject CPU ops here to run the exchange logic over gloo.
         self.sharded_ops = None
@@ -379,18 +388,28 @@ class TrainingJob1vsAll(TrainingJob):
         if self._sharded is not None:
             return self._sharded.process_batch(batch)
         t = -time.time()
-        triples = batch["triples"].to(self.device, non_blocking=True)
-        bs = len(triples)
-        cols = triples.t().contiguous()  # s, p, o as contiguous index vectors (one copy)
+        if "cols" in batch:  # [4, B] device index block s, p, o, s (the replayed step stages it this way)
+            cols = batch["cols"]
+        else:
+            triples = batch["triples"].to(self.device, non_blocking=True)
+            # s, p, o as contiguous index vectors plus a second copy of s right behind o: the
+            # labels of the two fused parts (o for sp_, s for _po) are then one contiguous vector
+            cols = triples.t()[[S, P, O, S]].contiguous()
+        bs = cols.shape[1]
         t += time.time()
         fused = self.config.get("engine.fused_loss") and isinstance(self.loss, KLDivWithSoftmaxKgeLoss)
         fwd = -time.time()
-        both = self.model.score_sp_po_xent(cols[S], cols[P], cols[O], 1.0 / bs) if fused else None
+        both = None
+        if fused:
+            both = self.model.score_xent_parts(self.model.xent_part_sp(cols[S], cols[P], cols[O]),
+                                               self.model.xent_part_po(cols[P], cols[O], cols[3]), 1.0 / bs)
         if both is not None:  # sp_ and _po in one engine pass; one backward (same gradient sum)
             total, _ = both
             fwd += time.time()
             bwd = -time.time()
-            total.backward()
+            if self._one is None:
+                self._one = torch.ones((), device=total.device, dtype=total.dtype)
+            total.backward(self._one)  # a persistent seed gradient: no fill kernel per step
             bwd += time.time()
             return TrainingJob._ProcessBatchResult(total.detach(), bs, t, fwd, bwd)
         loss_sp = self.model.score_sp_xent(cols[S], cols[P], cols[O], 1.0 / bs) if fused else None
