@@ -362,6 +362,36 @@ int kge_rank_hist_multi(const int64_t* greater, const int64_t* ties, int64_t n,
                         int64_t rows_per_hist, int tie_handling, int64_t* ranks,
                         float* hist, int64_t hist_len, void* stream);
 
+/* One launch for a whole evaluation batch: the score block S[n_a + n_b, m] stacks the
+ * (s, p, ?) queries (rows [0, n_a), true column o, entity_ranking.py:153-168 "sp" half) on
+ * the (?, p, o) queries (rows [n_a, n_a + n_b), true column s, the "po" half); each batch
+ * brings its own true_idx / true_score / CSR pointers, the CSR columns (f_col, t_col) are
+ * shared.  Counting follows kge_rank_counts; greater / ties are [1 + #filters][n_a + n_b]
+ * (ranking-major), added to when accumulate != 0 and overwritten otherwise.
+ * tie_handling >= 0 (needs accumulate == 0: one chunk covers every entity) also finishes
+ * the batch: ranks[r, i] by the tie rule and hist[(r * n + i) / rows_per_hist][rank] += 1
+ * (entity_ranking.py:531-551, eval.py:148-171).
+ * q != NULL refines scores produced by a reduced-precision contraction: with
+ *   band_i = band_rel * |q_i|_2 * t_norm_max[0]      (t_norm_max: kge_row_norm_max)
+ * an entry with |S[i, j] - true_score_i| <= band_i is replaced, before it is compared, by
+ * the correctly rounded fp32 value of the exact dot product q_i . t_j (fp64 accumulation,
+ * fixed order; q: fp32 query rows [n, d], t: the chunk's fp32 candidate rows [m, d]).
+ * When the contraction's error stays below the band, the counts equal those of exactly
+ * computed scores.  The reference ranks fp32 scores (entity_ranking.py:469-529). */
+int kge_rank_rows(const float* s, int64_t lds, int64_t n_a, int64_t n_b, int64_t m, int64_t c0,
+                  const int64_t* true_idx_a, const float* true_score_a, const int64_t* f_ptr_a,
+                  const int64_t* t_ptr_a, const int64_t* true_idx_b, const float* true_score_b,
+                  const int64_t* f_ptr_b, const int64_t* t_ptr_b, const int64_t* f_col,
+                  const int64_t* t_col, int64_t* greater, int64_t* ties, int accumulate,
+                  int tie_handling, int64_t* ranks, float* hist, int64_t hist_len,
+                  int64_t rows_per_hist, const float* q, int64_t ldq, const float* t, int64_t ldt,
+                  int d, float band_rel, const float* t_norm_max, void* stream);
+
+/* out[0] = max_j |t_j|_2 over the m rows of t (device scalar; the refinement band of
+ * kge_rank_rows).  No counterpart in the reference, which ranks exact fp32 scores
+ * (entity_ranking.py:469-529). */
+int kge_row_norm_max(const float* t, int64_t ldt, int64_t m, int d, float* out, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

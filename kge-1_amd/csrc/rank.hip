@@ -97,6 +97,183 @@ __global__ void __launch_bounds__(NT) rank_counts_kernel(const float* __restrict
   }
 }
 
+// ---------------------------------------------------------------------------------------
+// Stacked ranking pass: rows [0, n_a) belong to query batch A (e.g. the (s, p, ?) queries of
+// an evaluation batch), rows [n_a, n) to batch B (the (?, p, o) queries); each batch brings
+// its own true column / true score / filter-list pointers, the list columns are shared.
+// Optionally finishes the job in the same launch (rank per tie policy + histogram), and
+// optionally REFINES scores that came from a reduced-precision contraction: an entry whose
+// score lies within  band_i = band_rel * |q_i| * max_j |t_j|  of the true score is rescored
+// as the correctly rounded fp32 value of the exact dot product of the fp32 query row and
+// the fp32 candidate row (fp64 accumulation, fixed order) before it is compared.  Entries
+// outside the band are on the same side of the true score as their exact value whenever the
+// contraction's error is below the band, so the counts equal those of exact scoring.
+struct RankPart {
+  const int64_t* true_idx;
+  const float* true_score;
+  const int64_t* f_ptr;
+  const int64_t* t_ptr;
+};
+
+struct RankRowsArgs {
+  const float* s;
+  int64_t lds, n_a, n, m, c0;
+  RankPart part[2];
+  const int64_t* f_col;
+  const int64_t* t_col;
+  int64_t* greater;
+  int64_t* ties;
+  int accumulate;
+  int tie;  // < 0: counts only
+  int64_t* ranks;
+  float* hist;
+  int64_t hist_len, rows_per_hist;
+  const float* q;  // null: no refinement
+  int64_t ldq;
+  const float* t;  // row j of the chunk = t + j * ldt
+  int64_t ldt;
+  int d;
+  float band_rel;
+  const float* t_norm_max;
+};
+
+__device__ __forceinline__ float exact_dot(const float* __restrict__ a, const float* __restrict__ b, int d) {
+  double acc0 = 0.0, acc1 = 0.0, acc2 = 0.0, acc3 = 0.0;
+  for (int k = 0; k < d; k += 4) {
+    const float4 x = *reinterpret_cast<const float4*>(a + k);
+    const float4 y = *reinterpret_cast<const float4*>(b + k);
+    acc0 = fma((double)x.x, (double)y.x, acc0);
+    acc1 = fma((double)x.y, (double)y.y, acc1);
+    acc2 = fma((double)x.z, (double)y.z, acc2);
+    acc3 = fma((double)x.w, (double)y.w, acc3);
+  }
+  return (float)((acc0 + acc1) + (acc2 + acc3));
+}
+
+template <bool VEC>
+__global__ void __launch_bounds__(NT) rank_rows_kernel(const RankRowsArgs a) {
+  __shared__ int64_t sm[16];
+  __shared__ float fsm[NT / 64];
+  const int64_t i = blockIdx.x;
+  const int side = i >= a.n_a;
+  const int64_t li = side ? i - a.n_a : i;
+  const RankPart& P = a.part[side];
+  const float t = clean(P.true_score[li]);
+  const int64_t tj = P.true_idx[li] - a.c0;
+  const float* row = a.s + i * a.lds;
+  const int64_t m = a.m;
+
+  float band = -1.f;  // no score satisfies |v - t| <= band
+  const float* qrow = nullptr;
+  if (a.q) {
+    qrow = a.q + i * a.ldq;
+    float ss = 0.f;
+    for (int k = threadIdx.x; k < a.d; k += NT) ss += qrow[k] * qrow[k];
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) ss += __shfl_xor(ss, off, 64);
+    if ((threadIdx.x & 63) == 0) fsm[threadIdx.x >> 6] = ss;
+    __syncthreads();
+    ss = 0.f;
+    for (int w = 0; w < NT / 64; ++w) ss += fsm[w];
+    band = a.band_rel * sqrtf(ss) * a.t_norm_max[0];
+  }
+  auto value = [&](int64_t j, float v) -> float {
+    if (j == tj) return t;
+    if (fabsf(v - t) <= band) v = exact_dot(qrow, a.t + j * a.ldt, a.d);
+    return clean(v);
+  };
+
+  int64_t gt = 0, eq = 0;
+  if (VEC) {
+    const int64_t m4 = m & ~(int64_t)3;
+    for (int64_t j = 4 * (int64_t)threadIdx.x; j < m4; j += 4 * NT) {
+      const float4 v4 = *reinterpret_cast<const float4*>(row + j);
+      const float v[4] = {v4.x, v4.y, v4.z, v4.w};
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const float v_ = value(j + c, v[c]);
+        gt += v_ > t;
+        eq += v_ == t;
+      }
+    }
+    for (int64_t j = m4 + threadIdx.x; j < m; j += NT) {
+      const float v_ = value(j, row[j]);
+      gt += v_ > t;
+      eq += v_ == t;
+    }
+  } else {
+    for (int64_t j = threadIdx.x; j < m; j += NT) {
+      const float v_ = value(j, row[j]);
+      gt += v_ > t;
+      eq += v_ == t;
+    }
+  }
+  block_sum2(gt, eq, sm);
+  auto emit = [&](int r, int64_t g, int64_t e) {  // thread 0 only
+    const int64_t x = (int64_t)r * a.n + i;
+    if (a.accumulate) {
+      a.greater[x] += g;
+      a.ties[x] += e;
+    } else {
+      a.greater[x] = g;
+      a.ties[x] = e;
+    }
+    if (a.tie >= 0) {
+      const int64_t rank = a.tie == KGE_TIE_ROUNDED_MEAN ? g + e / 2 : (a.tie == KGE_TIE_BEST ? g : g + e - 1);
+      if (a.ranks) a.ranks[x] = rank;
+      if (a.hist && rank >= 0 && rank < a.hist_len)
+        atomicAdd(a.hist + (x / a.rows_per_hist) * a.hist_len + rank, 1.0f);
+    }
+  };
+  if (threadIdx.x == 0) emit(0, gt, eq);
+  __syncthreads();
+
+  const int nfilt = P.t_ptr ? 2 : (P.f_ptr ? 1 : 0);
+  int64_t dgt_f = 0, deq_f = 0;
+  for (int r = 0; r < nfilt; ++r) {
+    const int64_t* ptr = r == 0 ? P.f_ptr : P.t_ptr;
+    const int64_t* col = r == 0 ? a.f_col : a.t_col;
+    int64_t dgt = 0, deq = 0;
+    if (ptr) {
+      const int64_t b = ptr[li], e = ptr[li + 1];
+      for (int64_t x = b + threadIdx.x; x < e; x += NT) {
+        const int64_t j = col[x] - a.c0;
+        if (j < 0 || j >= m || j == tj) continue;
+        const float v = value(j, row[j]);
+        dgt -= v > t;
+        deq -= v == t;
+        deq += (t == -INFINITY);  // the filtered entry is now -inf
+      }
+    }
+    block_sum2(dgt, deq, sm);
+    if (threadIdx.x == 0) {
+      dgt_f += dgt;
+      deq_f += deq;
+      emit(1 + r, gt + dgt_f, eq + deq_f);
+    }
+    __syncthreads();
+  }
+}
+
+// out[0] = max over rows of the Euclidean row norm (out[0] must hold 0 on entry)
+__global__ void __launch_bounds__(256) row_norm_max_kernel(const float* __restrict__ t, int64_t ldt, int64_t m, int d,
+                                                           float* out) {
+  const int lane = threadIdx.x & 63;
+  const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  float ss = 0.f;
+  if (r < m)
+    for (int k = lane; k < d; k += 64) {
+      const float v = t[r * ldt + k];
+      ss += v * v;
+    }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) ss += __shfl_xor(ss, off, 64);
+  // non-negative floats order like their bit patterns; NaN rows poison the maximum upwards
+  if (lane == 0 && r < m) atomicMax(reinterpret_cast<unsigned*>(out), __float_as_uint(sqrtf(ss) * 1.000001f));
+}
+
+__global__ void zero1_kernel(float* out) { out[0] = 0.f; }
+
 // row i counts into histogram i / rows_per_hist (hists of hist_len floats, back to back)
 __global__ void rank_hist_kernel(const int64_t* __restrict__ greater, const int64_t* __restrict__ ties, int64_t n,
                                  int64_t rows_per_hist, int tie, int64_t* ranks, float* hist, int64_t hist_len) {
@@ -136,6 +313,55 @@ extern "C" int kge_rank_hist_multi(const int64_t* greater, const int64_t* ties, 
   if (n == 0) return 0;
   rank_hist_kernel<<<dim3((unsigned)((n + 255) / 256)), dim3(256), 0, as_stream(stream)>>>(
       greater, ties, n, rows_per_hist, tie_handling, ranks, hist, hist_len);
+  KGE_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int kge_row_norm_max(const float* t, int64_t ldt, int64_t m, int d, float* out, void* stream) {
+  KGE_REQUIRE(m >= 0 && d > 0 && (t || m == 0) && out && ldt >= d);
+  hipStream_t st = as_stream(stream);
+  zero1_kernel<<<dim3(1), dim3(1), 0, st>>>(out);
+  if (m > 0) row_norm_max_kernel<<<dim3((unsigned)((m + 3) / 4)), dim3(256), 0, st>>>(t, ldt, m, d, out);
+  KGE_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int kge_rank_rows(const float* s, int64_t lds, int64_t n_a, int64_t n_b, int64_t m, int64_t c0,
+                             const int64_t* true_idx_a, const float* true_score_a, const int64_t* f_ptr_a,
+                             const int64_t* t_ptr_a, const int64_t* true_idx_b, const float* true_score_b,
+                             const int64_t* f_ptr_b, const int64_t* t_ptr_b, const int64_t* f_col,
+                             const int64_t* t_col, int64_t* greater, int64_t* ties, int accumulate, int tie_handling,
+                             int64_t* ranks, float* hist, int64_t hist_len, int64_t rows_per_hist, const float* q,
+                             int64_t ldq, const float* t, int64_t ldt, int d, float band_rel, const float* t_norm_max,
+                             void* stream) {
+  const int64_t n = n_a + n_b;
+  KGE_REQUIRE(n_a >= 0 && n_b >= 0 && m >= 0 && (m == 0 || s) && greater && ties && lds >= m && n < (1LL << 31));
+  KGE_REQUIRE(n_a == 0 || (true_idx_a && true_score_a));
+  KGE_REQUIRE(n_b == 0 || (true_idx_b && true_score_b));
+  KGE_REQUIRE((!f_ptr_a && !f_ptr_b) || f_col);
+  KGE_REQUIRE((!t_ptr_a && !t_ptr_b) || t_col);
+  // the rankings of both batches share one counts layout: filter lists come for both or neither
+  KGE_REQUIRE(n_a == 0 || n_b == 0 || ((!f_ptr_a == !f_ptr_b) && (!t_ptr_a == !t_ptr_b)));
+  KGE_REQUIRE(!(t_ptr_a && !f_ptr_a) && !(t_ptr_b && !f_ptr_b));
+  KGE_REQUIRE(tie_handling <= 2 && (tie_handling < 0 || !hist || (hist_len > 0 && rows_per_hist > 0)));
+  KGE_REQUIRE(tie_handling < 0 || !accumulate);  // ranks need the counts of every chunk
+  if (q) {
+    KGE_REQUIRE(t && t_norm_max && d > 0 && ldq >= d && ldt >= d && band_rel >= 0.f);
+    if (d % 4 != 0 || ldq % 4 != 0 || ldt % 4 != 0 || !aligned16(q) || !aligned16(t)) return KGE_ERR_ALIGN;
+  }
+  if (n == 0) return 0;
+  RankRowsArgs a;
+  a.s = s; a.lds = lds; a.n_a = n_a; a.n = n; a.m = m; a.c0 = c0;
+  a.part[0] = RankPart{true_idx_a, true_score_a, f_ptr_a, t_ptr_a};
+  a.part[1] = RankPart{true_idx_b, true_score_b, f_ptr_b, t_ptr_b};
+  a.f_col = f_col; a.t_col = t_col; a.greater = greater; a.ties = ties; a.accumulate = accumulate;
+  a.tie = tie_handling; a.ranks = ranks; a.hist = hist; a.hist_len = hist_len; a.rows_per_hist = rows_per_hist;
+  a.q = q; a.ldq = ldq; a.t = t; a.ldt = ldt; a.d = d; a.band_rel = band_rel; a.t_norm_max = t_norm_max;
+  hipStream_t st = as_stream(stream);
+  if (lds % 4 == 0 && aligned16(s))
+    rank_rows_kernel<true><<<dim3((unsigned)n), dim3(NT), 0, st>>>(a);
+  else
+    rank_rows_kernel<false><<<dim3((unsigned)n), dim3(NT), 0, st>>>(a);
   KGE_CHECK_LAUNCH();
   return 0;
 }

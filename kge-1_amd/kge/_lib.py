@@ -70,6 +70,9 @@ SIGNATURES = {
     "kge_bucket_scatter": ([_P, _I64, _P, _P, _P], _I),
     "kge_stage_i64": ([_P, _P, _I64, _P], _I),
     "kge_rank_hist_multi": ([_P, _P, _I64, _I64, _I, _P, _P, _I64, _P], _I),
+    "kge_rank_rows": ([_P, _I64, _I64, _I64, _I64, _I64, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _P, _P,
+                       _I64, _I64, _P, _I64, _P, _I64, _I, _F, _P, _P], _I),
+    "kge_row_norm_max": ([_P, _I64, _I64, _I, _P, _P], _I),
     "kge_softmax_planes_max_columns": ([], _I64),
     "kge_softmax_xent_planes": ([_P, _I64, _I64, _I64, _I64, _P, _F, _P, _P], _I),
     "kge_softmax_kl_planes": ([_P, _I64, _I64, _I64, _I64, _P, _P, _F, _F, _P, _P], _I),
@@ -358,6 +361,67 @@ def rank_hist_multi(greater, ties, rows_per_hist, tie_handling, ranks, hists):
         raise ValueError("rank_hist_multi: hists must be a contiguous [k, hist_len] tensor covering every row")
     _check(lib().kge_rank_hist_multi(ptr(greater), ptr(ties), n, rows_per_hist, TIE[tie_handling], ptr(ranks),
                                      ptr(hists), hists.shape[1], stream()), "kge_rank_hist_multi")
+
+
+def _i64c(t, what):
+    if t is not None and (t.dtype != torch.int64 or not t.is_contiguous()):
+        raise ValueError(f"rank_rows: {what} must be a contiguous int64 tensor")
+    return t
+
+
+def rank_rows(s, n_a, c0, part_a, part_b, f_col, t_col, greater, ties, accumulate, tie_handling=None, ranks=None,
+              hists=None, rows_per_hist=0, refine=None):
+    """kge_rank_rows: one ranking launch for the stacked score block s [n_a + n_b, m].
+    part = (true_idx, true_score, f_ptr, t_ptr) of each batch (part_b None: one batch);
+    tie_handling (a name) also writes ranks / hists [k, hist_len]; refine = (q, t_rows,
+    band_rel, t_norm_max) rescoring near-ties exactly.  Nothing is copied: every tensor
+    must already have the kernel's layout."""
+    n, m = s.shape
+    n_b = n - n_a
+    if part_b is None:
+        part_b = (None, None, None, None)
+        if n_b:
+            raise ValueError("rank_rows: rows beyond n_a need part_b")
+    args = []
+    for true_idx, true_score, f_ptr, t_ptr in (part_a, part_b):
+        if true_score is not None and (true_score.dtype != torch.float32 or not true_score.is_contiguous()):
+            raise ValueError("rank_rows: true scores must be contiguous float32")
+        args += [ptr(_i64c(true_idx, "true_idx")), ptr(true_score), ptr(_i64c(f_ptr, "f_ptr")),
+                 ptr(_i64c(t_ptr, "t_ptr"))]
+    if not (greater.is_contiguous() and ties.is_contiguous() and greater.dtype == torch.int64
+            and ties.dtype == torch.int64):
+        raise ValueError("rank_rows: greater / ties must be contiguous int64")
+    nrank = 1 + (part_a[2] is not None) + (part_a[3] is not None)
+    if greater.numel() < nrank * n or ties.numel() < nrank * n:
+        raise ValueError("rank_rows: greater / ties hold [rankings, rows] counts")
+    tie = -1 if tie_handling is None else TIE[tie_handling]
+    hist_len = 0
+    if hists is not None:
+        if hists.dim() != 2 or not hists.is_contiguous() or hists.dtype != torch.float32 \
+                or rows_per_hist <= 0 or nrank * n > hists.shape[0] * rows_per_hist:
+            raise ValueError("rank_rows: hists must be a contiguous float32 [k, hist_len] covering every row")
+        hist_len = hists.shape[1]
+    if ranks is not None and (_i64c(ranks, "ranks").numel() < nrank * n):
+        raise ValueError("rank_rows: ranks holds [rankings, rows]")
+    q = t_rows = tmax = None
+    band, d = 0.0, 0
+    if refine is not None:
+        q, t_rows, band, tmax = refine
+        d = q.shape[1]
+        if q.shape[0] != n or t_rows.shape[0] != m or t_rows.shape[1] != d:
+            raise ValueError("rank_rows: refinement operands do not match the score block")
+    _check(lib().kge_rank_rows(ptr(s), rows(s), n_a, n_b, m, c0, *args, ptr(_i64c(f_col, "f_col")),
+                               ptr(_i64c(t_col, "t_col")), ptr(greater), ptr(ties), int(accumulate), tie, ptr(ranks),
+                               ptr(hists), hist_len, rows_per_hist, ptr(q), rows(q) if q is not None else 0,
+                               ptr(t_rows), rows(t_rows) if t_rows is not None else 0, d, float(band), ptr(tmax),
+                               stream()), "kge_rank_rows")
+
+
+def row_norm_max(t):
+    """Device scalar max_j |t_j|_2 (kge_row_norm_max)."""
+    out = torch.empty(1, device=t.device, dtype=torch.float32)
+    _check(lib().kge_row_norm_max(ptr(t), rows(t), t.shape[0], t.shape[1], ptr(out), stream()), "kge_row_norm_max")
+    return out
 
 
 def rank_hist(greater, ties, tie_handling, ranks, hist):

@@ -369,6 +369,64 @@ def score_all(kind: int, direction: int, precision: int, l_norm: float, ent: tor
                            L.idx64(ridx), tab, L.idx64(tidx))
 
 
+class _NoGradCtx:
+    """Stands in for an autograd context where no gradient is taken."""
+    needs_input_grad = (False,) * 16
+    meta = None
+
+
+@torch.no_grad()
+def score_parts(kind: int, precision: int, l_norm: float, ent: torch.Tensor, rel: torch.Tensor, parts,
+                tidx: Optional[torch.Tensor] = None, want_q: bool = False, out: Optional[torch.Tensor] = None):
+    """Several query batches against the same candidates, stacked by rows, without gradient
+    (evaluation): parts = [(direction, eidx, ridx), ...]; returns (S, Q) with S [sum n_k, m]
+    a view of a buffer whose rows are padded to 16 B (or ``out``, e.g. column blocks of a
+    wider buffer) and Q the fp32 query rows [sum n_k, width] when want_q (None when the
+    parts' queries do not share one layout).  Bilinear models whose parts contract the same
+    columns run ONE query preparation block and ONE contraction; other models score the
+    parts into their row blocks one by one."""
+    L.require_device(ent, rel)
+    ent, rel = _rows(ent), _rows(rel)
+    tidx = L.idx64(tidx)
+    parts = [(d, L.idx64(e), L.idx64(r)) for d, e, r in parts]
+    sizes = [e.numel() for _, e, _ in parts]
+    n = sum(sizes)
+    m = tidx.numel() if tidx is not None else ent.shape[0]
+    d_e, d_r = ent.shape[1], rel.shape[1]
+    if out is None:
+        out = torch.empty(n, (m + 3) // 4 * 4, device=ent.device, dtype=torch.float32)[:, :m]
+    qw = L.query_width(kind, d_e)
+    same_window = kind != L.CP or len({d for d, _, _ in parts}) == 1
+    q = None
+    if kind in BILINEAR and same_window:
+        tab_w = window(kind, parts[0][0], ent)
+        split = L.split_ok(qw, tab_w, precision)
+        if want_q or not split:
+            q = torch.empty(n, qw, device=ent.device, dtype=torch.float32)
+        if split:
+            ldp = (qw + 31) // 32 * 32
+            hi = torch.empty(n, ldp, device=ent.device, dtype=torch.bfloat16)
+            lo = torch.empty_like(hi)
+            r0 = 0
+            for (dr, ei, ri), k in zip(parts, sizes):
+                L.prep_query_split(kind, dr, ent, ei, rel, ri, k, d_e, d_r,
+                                   out=(q[r0:r0 + k] if want_q else None, hi[r0:r0 + k], lo[r0:r0 + k]))
+                r0 += k
+            _timed(L.score_dot_split, hi, lo, tab_w, tidx, qw, out=out)
+        else:
+            r0 = 0
+            for (dr, ei, ri), k in zip(parts, sizes):
+                L.prep_query(kind, dr, ent, ei, rel, ri, k, d_e, d_r, out=q[r0:r0 + k])
+                r0 += k
+            _timed(L.contract, q, tab_w, tidx, precision, out=out)
+        return out, (q if want_q else None)
+    r0 = 0
+    for (dr, ei, ri), k in zip(parts, sizes):
+        _scores_forward(_NoGradCtx(), kind, dr, precision, l_norm, ent, ei, rel, ri, ent, tidx, out=out[r0:r0 + k])
+        r0 += k
+    return out, None
+
+
 class _ScoreSpo(torch.autograd.Function):
     @staticmethod
     def forward(ctx, kind, l_norm, ent, sidx, rel, pidx, oidx):

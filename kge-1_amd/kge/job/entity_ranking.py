@@ -3,11 +3,14 @@ entity_ranking.py:11-577) as an on-device pipeline.
 
 Per batch of evaluation triples:
   1. true scores via KgeModel.score_spo (entity_ranking.py:139-140);
-  2. per entity chunk, KgeModel.score_sp_po on the engine (entity_ranking.py:153-168);
-  3. kge_rank_counts: raw / filtered / filtered-with-test greater & tie counts straight
-     from the score chunk, the true entry replaced by the true score, filtering applied
-     from per-query CSR lists of known answers (entity_ranking.py:172-216, 469-529);
-  4. kge_rank_hist: tie handling + rank histogram (entity_ranking.py:531-551, eval.py:148-171).
+  2. per entity chunk, the scores of KgeModel.score_sp_po stacked by rows -- (s, p, ?)
+     queries on top of (?, p, o) queries, one engine pass (entity_ranking.py:153-168);
+  3. kge_rank_rows, one launch for both directions: raw / filtered / filtered-with-test
+     greater & tie counts straight from the score chunk, the true entry replaced by the true
+     score, filtering applied from per-query CSR lists of known answers
+     (entity_ranking.py:172-216, 469-529);
+  4. tie handling + rank histograms (entity_ranking.py:531-551, eval.py:148-171): in the same
+     launch when one chunk covers every entity, else kge_rank_hist_multi after the last chunk.
 The filter lists are built once per job from the dataset splits (vectorised numpy)
 instead of the reference's per-triple Python collate (job/util.py:5-38).  Counts are sums
 over chunks, which is exactly the reference's chunk_size decomposition and the
@@ -24,6 +27,13 @@ import torch
 from .. import _lib
 from ..dataset import KvsAllIndex
 from .job import Job
+
+#: engine.eval_precision value: bf16x3 contraction, near-ties of the true score rescored exactly
+REFINED = "bf16x3_refined"
+#: refinement band relative to |q_i| * max_j |t_j| (kge_rank_rows): the split contraction
+#: drops terms below 3 * 2^-18 of sum_k |q_k t_k| and adds the fp32 accumulation error of 3 d
+#: terms; 1e-4 covers the worst case up to d = 512 (measured errors stay below 1e-5)
+REFINE_BAND = 1e-4
 
 RANKING_SUFFIX = {"_raw": "", "_filt": "_filtered", "_filt_test": "_filtered_with_test"}
 
@@ -77,6 +87,7 @@ class EntityRankingJob(EvaluationJob):
         #: compute ops of the row-sharded path; None: the engine (kge.sharded.EngineOps)
         self.sharded_ops = None
         self.capture_ranks = False  # keep per-query ranks in self.ranks (tests / tracing)
+        self._refine = False  # set per run from engine.eval_precision
         self.ranks: Dict[str, np.ndarray] = {}
 
     # ---------------------------------------------------------------- preparation
@@ -104,6 +115,7 @@ class EntityRankingJob(EvaluationJob):
         self._f = {k: (torch.from_numpy(p).to(dev), torch.from_numpy(c if len(c) else np.zeros(1, np.int64)).to(dev))
                    for k, (p, c) in csr.items()}
         self._t = None
+        tcsr = None
         if self.use_test:
             t_sp, t_po = self._filter_index(["test"])
             tcsr = {"sp": _csr_minus(*t_sp.csr_for(tri[:, [0, 1]]), *csr["sp"], E),
@@ -111,15 +123,36 @@ class EntityRankingJob(EvaluationJob):
             self._t = {k: (torch.from_numpy(p).to(dev),
                            torch.from_numpy(c if len(c) else np.zeros(1, np.int64)).to(dev))
                        for k, (p, c) in tcsr.items()}
+        # the stacked ranking launch (kge_rank_rows) reads both directions' lists from ONE column
+        # array: the (?, p, o) pointers are shifted behind the (s, p, ?) columns
+        self._stacked = [self._stack_csr(csr, dev), self._stack_csr(tcsr, dev) if tcsr is not None else None]
+        self._cols = self.triples.t().contiguous().to(dev)  # [3, N]: s / p / o as contiguous vectors
+
+    @staticmethod
+    def _stack_csr(csr, dev):
+        (p_sp, c_sp), (p_po, c_po) = csr["sp"], csr["po"]
+        col = np.concatenate([c_sp, c_po, np.zeros(1, np.int64)]).astype(np.int64)
+        return (torch.from_numpy(p_sp.astype(np.int64)).to(dev),
+                torch.from_numpy((p_po + len(c_sp)).astype(np.int64)).to(dev), torch.from_numpy(col).to(dev))
 
     # ---------------------------------------------------------------- evaluation
     @torch.no_grad()
     def _run(self) -> dict:
-        """Scores with engine.eval_precision (default fp32: ranks compare near-ties, and
-        the reference ranks fp32 scores) for the whole run, whatever precision training uses."""
+        """Scores with engine.eval_precision for the whole run, whatever precision training
+        uses: ranks compare near-ties and the reference ranks fp32 scores, so evaluation either
+        contracts in fp32 or contracts in bf16x3 and rescores every near-tie of the true score
+        exactly (bf16x3_refined; kge_rank_rows)."""
         scorer = self.model.get_scorer()
         saved = scorer.precision_override
-        scorer.precision_override = self.config.check("engine.eval_precision", list(_lib.PRECISIONS))
+        name = self.config.check("engine.eval_precision", list(_lib.PRECISIONS) + [REFINED])
+        self._refine = name == REFINED
+        if self._refine:
+            from ..sharded import sharding_enabled
+
+            # the row-sharded path and models without a split contraction rank exact scores
+            name = "fp32" if sharding_enabled(self.config) else "bf16x3"
+            self._refine = name == "bf16x3"
+        scorer.precision_override = name
         try:
             return self._run_ranking()
         finally:
@@ -149,15 +182,29 @@ class EntityRankingJob(EvaluationJob):
         sharded = self._sharded_scorer()
         chunk = self.config.get("entity_ranking.chunk_size")
         chunk = E if chunk is None or chunk < 0 else chunk
-        hists_d = torch.zeros(2, nrank, E, device=dev)  # per direction: tail ("o"), head ("s")
+        #: [ranking, direction (tail "o", head "s"), rank] histograms
+        hists_d = torch.zeros(nrank, 2, E, device=dev)
+        hists_flat = hists_d.view(nrank * 2, E)
+        hists_sharded = torch.zeros(2, nrank, E, device=dev) if sharded is not None else None
+        tmax = None
+        ent_rows = None
+        if self._refine:
+            # refinement needs fp32 query rows that contract with whole entity rows: the bilinear
+            # lookup models except CP; every other model ranks fp32 scores
+            tabs = self.model._lookup_tables()
+            self._refine = tabs is not None and self.model.get_scorer().engine_kind in (
+                _lib.COMPLEX, _lib.DISTMULT, _lib.RESCAL, _lib.SIMPLE)
+            if self._refine:
+                ent_rows = tabs[0].detach()
+            else:
+                self.model.get_scorer().precision_override = "fp32"
         ranks_out = {f"{d}{r}": [] for d in "so" for r in self.rankings}
         epoch_time = -time.time()
-        triples = self.triples.to(dev)
-        N = len(triples)
+        N = len(self.triples)
         for b0 in range(0, N, self.batch_size):
             b1 = min(N, b0 + self.batch_size)
             B = b1 - b0
-            s, p, o = triples[b0:b1, 0], triples[b0:b1, 1], triples[b0:b1, 2]
+            s, p, o = self._cols[0, b0:b1], self._cols[1, b0:b1], self._cols[2, b0:b1]
             if sharded is not None:
                 # each rank counts over its own rows; one all_reduce of the int64 counts makes
                 # them global (the reference's chunk_size decomposition, entity_ranking.py:153-216)
@@ -170,7 +217,7 @@ class EntityRankingJob(EvaluationJob):
                 for di, d in enumerate("os"):
                     rk = torch.empty(nrank * B, dtype=torch.int64, device=dev)
                     sharded.ops.rank_hist_multi(counts[di, 0, :nrank * B], counts[di, 1, :nrank * B], B,
-                                                self.tie_handling, rk, hists_d[di])
+                                                self.tie_handling, rk, hists_sharded[di])
                     if self.capture_ranks:
                         for ri, r in enumerate(self.rankings):
                             ranks_out[f"{d}{r}"].append(rk[ri * B:(ri + 1) * B])
@@ -179,31 +226,49 @@ class EntityRankingJob(EvaluationJob):
             # score_spo(.., "s") is the same triple score unless the model scores the two
             # directions differently (reciprocal relations): skip the second launch then
             s_true = o_true if not self._two_sided else self.model.score_spo(s, p, o, "s").view(-1).float().contiguous()
-            counts = torch.zeros(4, 3 * B, dtype=torch.int64, device=dev)  # greater / ties per direction
-            g = {"o": counts[0], "s": counts[1]}
-            t = {"o": counts[2], "s": counts[3]}
+            (fp_sp, fp_po, f_col), tstack = self._stacked
+            tp_sp, tp_po, t_col = tstack if tstack is not None else (None, None, None)
+            part_a = (o, o_true, fp_sp[b0:], tp_sp[b0:] if tp_sp is not None else None)
+            part_b = (s, s_true, fp_po[b0:], tp_po[b0:] if tp_po is not None else None)
+            single = chunk >= E
+            counts = (torch.empty if single else torch.zeros)(2, nrank * 2 * B, dtype=torch.int64, device=dev)
+            rk = torch.empty(nrank * 2 * B, dtype=torch.int64, device=dev)
             for c0 in range(0, E, chunk):
                 c1 = min(E, c0 + chunk)
-                subset = None if (c0 == 0 and c1 == E) else torch.arange(c0, c1, device=dev)
-                scores = self.model.score_sp_po(s, p, o, subset)
-                C = c1 - c0
-                self._count(scores[:, :C], c0, o, o_true, "sp", b0, b1, g["o"], t["o"])
-                self._count(scores[:, C:], c0, s, s_true, "po", b0, b1, g["s"], t["s"])
+                subset = None if single else torch.arange(c0, c1, device=dev)
+                # [2B, C]: the (s, p, ?) rows on top of the (?, p, o) rows, one engine pass
+                scores, q = self.model.score_sp_po_rows(s, p, o, subset, want_q=self._refine)
+                refine = None
+                if q is not None:
+                    if tmax is None:
+                        tmax = _lib.row_norm_max(ent_rows)
+                    refine = (q, ent_rows[c0:c1], REFINE_BAND, tmax)
+                elif self._refine:
+                    raise RuntimeError("engine.eval_precision bf16x3_refined: the engine returned no fp32 query "
+                                       "rows to rescore near-ties with")
+                # a single chunk finishes the batch in the same launch: ranks + histograms
+                _lib.rank_rows(scores, B, c0, part_a, part_b, f_col, t_col, counts[0], counts[1],
+                               accumulate=not single, tie_handling=self.tie_handling if single else None,
+                               ranks=rk if single else None, hists=hists_flat if single else None,
+                               rows_per_hist=B, refine=refine)
                 del scores
-            for di, d in enumerate("os"):  # every ranking of one direction in one launch
-                rk = torch.empty(nrank * B, dtype=torch.int64, device=dev)
-                _lib.rank_hist_multi(g[d][:nrank * B], t[d][:nrank * B], B, self.tie_handling, rk, hists_d[di])
-                if self.capture_ranks:
+            if not single:
+                _lib.rank_hist_multi(counts[0], counts[1], B, self.tie_handling, rk, hists_flat)
+            if self.capture_ranks:
+                rk = rk.view(nrank, 2, B)
+                for di, d in enumerate("os"):
                     for ri, r in enumerate(self.rankings):
-                        ranks_out[f"{d}{r}"].append(rk[ri * B:(ri + 1) * B])
+                        ranks_out[f"{d}{r}"].append(rk[ri, di])
         epoch_time += time.time()
         metrics = {}
-        hists = hists_d.sum(0)  # counts are small integers: the fp32 sum is exact
+        if hists_sharded is not None:
+            hists_d += hists_sharded.permute(1, 0, 2)
+        hists = hists_d.sum(1)  # counts are small integers: the fp32 sum is exact
         for ri, r in enumerate(self.rankings):
             metrics.update(self._compute_metrics(hists[ri], RANKING_SUFFIX[r]))
             if self.head_and_tail:  # entity_ranking.py:376-387 (suffix order: ranking, then slot)
-                metrics.update(self._compute_metrics(hists_d[1, ri], RANKING_SUFFIX[r] + "_head"))
-                metrics.update(self._compute_metrics(hists_d[0, ri], RANKING_SUFFIX[r] + "_tail"))
+                metrics.update(self._compute_metrics(hists_d[ri, 1], RANKING_SUFFIX[r] + "_head"))
+                metrics.update(self._compute_metrics(hists_d[ri, 0], RANKING_SUFFIX[r] + "_tail"))
         if self.capture_ranks:
             self.ranks = {k: torch.cat(v).cpu().numpy() if v else np.zeros(0, np.int64)
                           for k, v in ranks_out.items()}
@@ -215,15 +280,6 @@ class EntityRankingJob(EvaluationJob):
         if was_training:
             self.model.train()
         return trace
-
-    def _count(self, scores, c0, true_idx, true_score, kind, b0, b1, greater, ties):
-        scores = scores.float()
-        if scores.stride(1) != 1:
-            scores = scores.contiguous()
-        fp, fc = self._f[kind]
-        tp, tc = self._t[kind] if self._t is not None else (None, None)
-        _lib.rank_counts(scores, c0, true_idx, true_score, fp[b0:], fc,
-                         tp[b0:] if tp is not None else None, tc, greater, ties)
 
     def _compute_metrics(self, rank_hist: torch.Tensor, suffix: str = "") -> Dict[str, float]:
         """entity_ranking.py:553-577 (fp32 histogram arithmetic like the reference)."""

@@ -146,6 +146,16 @@ class RelationalScorer(KgeBase):
         return engine.score_all(self.engine_kind, d, self.precision(), self.l_norm(), ent, e_idx, rel, p_idx,
                                 ent, cand_idx)
 
+    def score_lookup_parts(self, ent: Tensor, rel: Tensor, parts, cand_idx: Optional[Tensor] = None,
+                           want_q: bool = False, out: Optional[Tensor] = None):
+        """Several query batches (direction "sp_" / "_po", e_idx, p_idx) against the same
+        candidates, stacked by rows, without gradient (engine.score_parts): (S, Q)."""
+        from .. import engine, _lib
+
+        conv = [((_lib.DIR_SP if d == "sp_" else _lib.DIR_PO), e, p) for d, e, p in parts]
+        return engine.score_parts(self.engine_kind, self.precision(), self.l_norm(), ent, rel, conv, cand_idx,
+                                  want_q, out)
+
     def score_lookup_xent(self, ent: Tensor, rel: Tensor, e_idx: Tensor, p_idx: Tensor, direction: str,
                           labels: Tensor, scale: float, l_ptr: Optional[Tensor] = None,
                           smoothing: float = 0.0) -> Tensor:
@@ -453,13 +463,39 @@ class KgeModel(KgeBase):
         p = self.get_p_embedder().embed_all() if p is None else self.get_p_embedder().embed(p)
         return self._scorer.score_emb(s, p, o, combine="s_o")
 
+    def _sp_po_parts(self, s: Tensor, p: Tensor, o: Tensor):
+        """The two query batches of score_sp_po as (direction, e_idx, p_idx)."""
+        return [("sp_", s, p), ("_po", o, p)]
+
+    def score_sp_po_rows(self, s: Tensor, p: Tensor, o: Tensor, entity_subset: Tensor = None, want_q: bool = False):
+        """The scores of score_sp_po stacked by ROWS, without gradient: (S, Q) with S [2n, C],
+        rows [0, n) = score_sp(s, p, subset), rows [n, 2n) = score_po(p, o, subset); Q the fp32
+        query rows behind S (or None: not asked for / not available for this model).  One
+        engine pass where the model allows it; the evaluation job ranks from this block."""
+        tabs = self._lookup_tables()
+        if tabs is not None:
+            return self._scorer.score_lookup_parts(tabs[0], tabs[1], self._sp_po_parts(s, p, o), entity_subset,
+                                                   want_q)
+        with torch.no_grad():
+            both = self.score_sp_po(s, p, o, entity_subset)
+        C = both.shape[1] // 2
+        return torch.cat((both[:, :C], both[:, C:]), dim=0), None
+
     def score_sp_po(self, s: Tensor, p: Tensor, o: Tensor, entity_subset: Tensor = None) -> Tensor:
         """cat(score_sp(s,p,subset), score_po(p,o,subset)) -> [n, 2|subset|]
         (kge_model.py:706-746)."""
         tabs = self._lookup_tables()
         if tabs is not None:
-            sp = self._scorer.score_lookup(tabs[0], tabs[1], s, p, "sp_", entity_subset)
-            po = self._scorer.score_lookup(tabs[0], tabs[1], o, p, "_po", entity_subset)
+            parts = self._sp_po_parts(s, p, o)
+            if not (torch.is_grad_enabled() and (tabs[0].requires_grad or tabs[1].requires_grad)):
+                # both halves straight into their column blocks of one buffer
+                C = tabs[0].shape[0] if entity_subset is None else entity_subset.numel()
+                buf = torch.empty(s.numel(), 2 * C, device=tabs[0].device, dtype=torch.float32)
+                self._scorer.score_lookup_parts(tabs[0], tabs[1], parts[:1], entity_subset, out=buf[:, :C])
+                self._scorer.score_lookup_parts(tabs[0], tabs[1], parts[1:], entity_subset, out=buf[:, C:])
+                return buf
+            sp = self._scorer.score_lookup(tabs[0], tabs[1], parts[0][1], parts[0][2], parts[0][0], entity_subset)
+            po = self._scorer.score_lookup(tabs[0], tabs[1], parts[1][1], parts[1][2], parts[1][0], entity_subset)
             return torch.cat((sp, po), dim=1)
         s = self.get_s_embedder().embed(s)
         p = self.get_p_embedder().embed(p)

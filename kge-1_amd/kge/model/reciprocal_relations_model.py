@@ -75,13 +75,14 @@ class ReciprocalRelationsModel(KgeModel):
     def score_so(self, s, o, p=None):
         raise Exception("The reciprocal relations model cannot score relations.")
 
+    def _sp_po_parts(self, s: Tensor, p: Tensor, o: Tensor):
+        return [("sp_", s, p), ("sp_", o, p + self.dataset.num_relations())]
+
     def score_sp_po(self, s: Tensor, p: Tensor, o: Tensor, entity_subset: Tensor = None) -> Tensor:
         tabs = self._lookup_tables()
         p_inv = p + self.dataset.num_relations()
         if tabs is not None:
-            sp = self._scorer.score_lookup(tabs[0], tabs[1], s, p, "sp_", entity_subset)
-            po = self._scorer.score_lookup(tabs[0], tabs[1], o, p_inv, "sp_", entity_subset)
-            return torch.cat((sp, po), dim=1)
+            return super().score_sp_po(s, p, o, entity_subset)
         s = self.get_s_embedder().embed(s)
         pi = self.get_p_embedder().embed(p_inv)
         p = self.get_p_embedder().embed(p)

@@ -69,6 +69,9 @@ def tables(model):
 
 # ------------------------------------------------------------------------------ C2 eval
 
+#: engine.eval_precision of config-default.yaml
+DEFAULT_EVAL_PRECISION = "bf16x3_refined"
+
 
 def seeded_tables(seed, E, R, d_e, d_r, std=0.1):
     """The generator of tests/golden/make_golden.py (numpy PCG64 stream)."""
@@ -146,17 +149,20 @@ def assert_rank_moves_are_near_ties(got, ref, ent, rel, tri, splits, tol, what):
     return moved, worst
 
 
-@pytest.mark.parametrize("eval_precision", [None, "bf16x3"], ids=["default_fp32", "bf16x3"])
-def test_c2_entity_ranking_fullsize_real_valued_vs_reference(eval_precision):
+@pytest.mark.parametrize("chunk", [-1, 5000], ids=["one_chunk", "chunk5000"])
+@pytest.mark.parametrize("eval_precision", [None, "fp32", "bf16x3", "bf16x3_refined"])
+def test_c2_entity_ranking_fullsize_real_valued_vs_reference(eval_precision, chunk):
     """The reference's EntityRankingJob at E = 14,541 (ComplEx-512, N(0, 0.1) tables, 512
     validation triples, filtered + filtered-with-test) against this build's job in its DEFAULT
-    configuration (engine.eval_precision fp32), and with bf16x3 scoring.
+    configuration and with every engine.eval_precision: fp32 contraction, plain bf16x3, and
+    bf16x3 with near-ties of the true score rescored exactly (bf16x3_refined).
 
     Two fp32 implementations of a K = 512 contraction differ by ~1e-6 of the row maximum
     (summation order), so on real-valued tables a competitor closer than that to the true
     score can legitimately change sides.  The bar: every rank equals the reference's, except
     where near-ties explain the move (contract tolerance 1e-4 of the row maximum; asserted
-    much tighter: 1e-5 for fp32, 3e-5 for bf16x3), and the metrics agree accordingly."""
+    much tighter: 1e-5 for fp32 and bf16x3_refined, 3e-5 for bf16x3), and the metrics agree
+    accordingly."""
     from kge.job import EntityRankingJob
     from kge import KgeModel
 
@@ -166,10 +172,14 @@ def test_c2_entity_ranking_fullsize_real_valued_vs_reference(eval_precision):
     ent, rel = seeded_tables(meta["table_seed"], E, R, dim, dim, meta["std"])
     assert table_checksum(ent) == meta["ent_checksum"] and table_checksum(rel) == meta["rel_checksum"], \
         "seeded tables differ from the ones the reference was run on (numpy stream changed?)"
-    c = base_config("complex", dim, E, R, {"eval.batch_size": meta["batch_size"], "eval.split": "valid"})
-    assert c.get("engine.eval_precision") == "fp32" and c.get("engine.precision") == "bf16x3"  # defaults
+    if chunk > 0 and eval_precision in (None, "bf16x3"):
+        pytest.skip("chunked scoring is covered with fp32 and bf16x3_refined")
+    c = base_config("complex", dim, E, R, {"eval.batch_size": meta["batch_size"], "eval.split": "valid",
+                                           "entity_ranking.chunk_size": chunk})
+    assert c.get("engine.eval_precision") == DEFAULT_EVAL_PRECISION and c.get("engine.precision") == "bf16x3"
     if eval_precision is not None:
         c.set("engine.eval_precision", eval_precision)
+    exactish = (eval_precision or DEFAULT_EVAL_PRECISION) != "bf16x3"
     ds = dataset_from(c, f)
     model = KgeModel.create(c, ds)
     set_tables(model, ent, rel)
@@ -179,13 +189,13 @@ def test_c2_entity_ranking_fullsize_real_valued_vs_reference(eval_precision):
     ref = {k[5:]: f[k] for k in f.files if k.startswith("full_")}
     assert set(job.ranks) == set(ref)
     splits = {k: ds.split(k).long().numpy() for k in ("train", "valid", "test")}
-    tol = 1e-5 if eval_precision is None else 3e-5
+    tol = 1e-5 if exactish else 3e-5
     moved, worst = assert_rank_moves_are_near_ties(job.ranks, ref, ent, rel, splits["valid"], splits, tol,
-                                                   f"eval_precision={eval_precision or 'fp32'}")
+                                                   f"eval_precision={eval_precision or 'default'}")
     total = sum(len(v) for v in ref.values())
-    print(f"\nC2 full-size eval ({eval_precision or 'fp32 default'}): {moved} of {total} ranks differ from the "
-          f"reference, all near-ties (largest gap {worst:.2e} of the row maximum)")
-    assert moved <= (0.005 if eval_precision is None else 0.02) * total
+    print(f"\nC2 full-size eval ({eval_precision or 'default ' + DEFAULT_EVAL_PRECISION}, chunk {chunk}): {moved} of "
+          f"{total} ranks differ from the reference, all near-ties (largest gap {worst:.2e} of the row maximum)")
+    assert moved <= (0.005 if exactish else 0.02) * total
     # metrics: the job's own numbers follow from its ranks by the reference's formulas
     # (entity_ranking.py:553-577), and differ from the reference's by no more than the moved
     # ranks account for
@@ -214,7 +224,7 @@ def test_eval_precision_is_applied_and_restored():
     f = np.load(os.path.join(GOLDEN, "eval_normal.npz"))
     meta = json.loads(str(f["meta"]))
     seen = []
-    for ep in ("fp32", "bf16x3"):
+    for ep in ("fp32", "bf16x3", "bf16x3_refined"):
         c = base_config("complex", meta["dim"], meta["E"], meta["R"], {"engine.eval_precision": ep})
         ds = dataset_from(c, f)
         model = KgeModel.create(c, ds)
@@ -227,7 +237,8 @@ def test_eval_precision_is_applied_and_restored():
 
         scorer.precision = spy
         EntityRankingJob(c, ds, model=model).run()
-        assert set(seen) == {_lib.PRECISIONS[ep]}, (ep, set(seen))
+        # the refined mode contracts in bf16x3 and rescores near-ties in the ranking launch
+        assert set(seen) == {_lib.PRECISIONS[ep.replace("_refined", "")]}, (ep, set(seen))
         seen.clear()
         scorer.precision = orig
         assert scorer.precision_override is None and scorer.precision() == _lib.PREC_BF16X3

@@ -1,0 +1,207 @@
+"""GPU parity of the stacked ranking launch (kge_rank_rows) through the C ABI:
+* its counts, ranks and histograms against the CPU oracle's rank_and_ties / get_ranks
+  (entity_ranking.py:469-551 restated) and against the per-direction kge_rank_counts +
+  kge_rank_hist_multi pair it replaces -- bit-exact (integer work);
+* its refinement of reduced-precision scores: counts must EQUAL those of exactly computed
+  scores (float64 dot products rounded to fp32) on inputs built to be full of near-ties that
+  the bf16x3 contraction mis-orders."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import kge_oracle as K
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def L():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from kge import _lib
+    _lib.lib()
+    return _lib
+
+
+def _csr(rng, n, m, max_len):
+    lens = rng.integers(0, max_len + 1, size=n)
+    lens[0] = 0
+    ptr = np.zeros(n + 1, np.int64)
+    np.cumsum(lens, out=ptr[1:])
+    col = np.concatenate([rng.choice(m, size=k, replace=False) for k in lens] + [np.zeros(0, np.int64)])
+    return ptr, col.astype(np.int64)
+
+
+def _minus(ptr_a, col_a, ptr_b, col_b):
+    """Per-row A \\ B."""
+    out_ptr, out = [0], []
+    for i in range(len(ptr_a) - 1):
+        b = set(col_b[ptr_b[i]:ptr_b[i + 1]].tolist())
+        keep = [c for c in col_a[ptr_a[i]:ptr_a[i + 1]].tolist() if c not in b]
+        out += keep
+        out_ptr.append(len(out))
+    return np.asarray(out_ptr, np.int64), np.asarray(out, np.int64)
+
+
+def _oracle_counts(scores, c0, true_idx, true_score, lists):
+    """[1 + len(lists)] x (greater, ties) of one batch: the true entry takes the true score,
+    list entries (global ids, cumulative over the lists) go to -inf."""
+    sc = scores.copy()
+    n, m = sc.shape
+    for i in range(n):
+        j = true_idx[i] - c0
+        if 0 <= j < m:
+            sc[i, j] = true_score[i]
+    out = [K.rank_and_ties(sc, true_score)]
+    for ptr, col in lists:
+        for i in range(n):
+            for j in col[ptr[i]:ptr[i + 1]]:
+                if c0 <= j < c0 + m and j != true_idx[i]:
+                    sc[i, j - c0] = -np.inf
+        out.append(K.rank_and_ties(sc, true_score))
+    return out
+
+
+def _dev(x):
+    return torch.from_numpy(np.ascontiguousarray(x)).cuda()
+
+
+@pytest.mark.parametrize("n_a,n_b,m,c0,ld,with_test", [
+    (37, 37, 1001, 0, 1004, True),      # padded rows: vector loads
+    (16, 9, 517, 100, 517, True),       # odd leading dimension: scalar loads; a chunk at c0 = 100
+    (5, 0, 64, 0, 64, False),           # one batch only, raw + filtered
+    (64, 64, 14541, 0, 14544, True),    # FB15K-237 width
+])
+def test_rank_rows_counts_ranks_hists_vs_oracle_and_rank_counts(L, n_a, n_b, m, c0, ld, with_test):
+    rng = np.random.default_rng(n_a * 7 + m)
+    n = n_a + n_b
+    E = c0 + m + 50  # entity ids beyond the chunk exist
+    # coarse scores: plenty of exact ties; NaN and infinities sprinkled in
+    sc = np.round(rng.standard_normal((n, m)).astype(np.float32) * 4) / 4
+    sc[rng.random((n, m)) < 0.002] = np.nan
+    sc[rng.random((n, m)) < 0.001] = np.inf
+    sc[rng.random((n, m)) < 0.001] = -np.inf
+    true_idx = rng.integers(0, E, size=n).astype(np.int64)
+    true_score = (np.round(rng.standard_normal(n).astype(np.float32) * 4) / 4).astype(np.float32)
+    true_score[0] = np.nan
+    if n > 3:
+        true_score[3] = -np.inf
+    f_ptr_a, f_col_a = _csr(rng, n_a, E, 40)
+    f_ptr_b, f_col_b = _csr(rng, n_b, E, 40) if n_b else (np.zeros(1, np.int64), np.zeros(0, np.int64))
+    t_a = _minus(*_csr(rng, n_a, E, 25), f_ptr_a, f_col_a)
+    t_b = _minus(*_csr(rng, n_b, E, 25), f_ptr_b, f_col_b) if n_b else (np.zeros(1, np.int64), np.zeros(0, np.int64))
+    nrank = 3 if with_test else 2
+
+    exp = []  # per batch: [(greater, ties)] * nrank
+    for r0, r1, (fp, fc), (tp, tc) in ((0, n_a, (f_ptr_a, f_col_a), t_a), (n_a, n, (f_ptr_b, f_col_b), t_b)):
+        lists = [(fp, fc)] + ([(tp, tc)] if with_test else [])
+        exp.append(_oracle_counts(sc[r0:r1], c0, true_idx[r0:r1], true_score[r0:r1], lists))
+    exp_g = np.stack([np.concatenate([exp[0][r][0], exp[1][r][0]]) for r in range(nrank)])
+    exp_t = np.stack([np.concatenate([exp[0][r][1], exp[1][r][1]]) for r in range(nrank)])
+
+    buf = torch.full((n, ld), 3.25, device="cuda")
+    buf[:, :m] = _dev(sc)
+    s = buf[:, :m]
+    ti, ts = _dev(true_idx), _dev(true_score)
+    f_col = _dev(np.concatenate([f_col_a, f_col_b, np.zeros(1, np.int64)]))
+    t_col = _dev(np.concatenate([t_a[1], t_b[1], np.zeros(1, np.int64)]))
+    fpa, fpb = _dev(f_ptr_a), _dev(f_ptr_b + len(f_col_a))
+    tpa, tpb = (_dev(t_a[0]), _dev(t_b[0] + len(t_a[1]))) if with_test else (None, None)
+    part_a = (ti[:n_a], ts[:n_a], fpa, tpa)
+    part_b = (ti[n_a:], ts[n_a:], fpb, tpb) if n_b else None
+
+    for tie in ("rounded_mean_rank", "best_rank", "worst_rank"):
+        g = torch.full((nrank * n,), -7, dtype=torch.int64, device="cuda")  # overwritten, not added to
+        t = torch.full((nrank * n,), -7, dtype=torch.int64, device="cuda")
+        rk = torch.empty(nrank * n, dtype=torch.int64, device="cuda")
+        rows_per_hist = n_a if n_b == n_a else n
+        hists = torch.zeros(nrank * n // rows_per_hist, E, device="cuda")
+        L.rank_rows(s, n_a, c0, part_a, part_b, f_col, t_col if with_test else None, g, t, accumulate=False,
+                    tie_handling=tie, ranks=rk, hists=hists, rows_per_hist=rows_per_hist)
+        torch.cuda.synchronize()
+        assert np.array_equal(g.view(nrank, n).cpu().numpy(), exp_g)
+        assert np.array_equal(t.view(nrank, n).cpu().numpy(), exp_t)
+        exp_rk = K.get_ranks(exp_g, exp_t, tie)
+        assert np.array_equal(rk.view(nrank, n).cpu().numpy(), exp_rk)
+        flat = exp_rk.reshape(-1)
+        exp_h = np.zeros((nrank * n // rows_per_hist, E), np.float32)
+        for x, r in enumerate(flat):
+            if 0 <= r < E:
+                exp_h[x // rows_per_hist, r] += 1
+        assert np.array_equal(hists.cpu().numpy(), exp_h)
+
+    # accumulate mode adds to what the buffers hold; the per-direction kernel it replaces agrees
+    g = torch.full((nrank * n,), 5, dtype=torch.int64, device="cuda")
+    t = torch.full((nrank * n,), 2, dtype=torch.int64, device="cuda")
+    L.rank_rows(s, n_a, c0, part_a, part_b, f_col, t_col if with_test else None, g, t, accumulate=True)
+    assert np.array_equal(g.view(nrank, n).cpu().numpy(), exp_g + 5)
+    assert np.array_equal(t.view(nrank, n).cpu().numpy(), exp_t + 2)
+    for r0, r1, fp, fc, tp, tc in ((0, n_a, f_ptr_a, f_col_a, *t_a), (n_a, n, f_ptr_b, f_col_b, *t_b)):
+        if r1 == r0:
+            continue
+        k = r1 - r0
+        g1 = torch.zeros(3 * k, dtype=torch.int64, device="cuda")
+        t1 = torch.zeros(3 * k, dtype=torch.int64, device="cuda")
+        L.rank_counts(s[r0:r1], c0, ti[r0:r1], ts[r0:r1], _dev(fp), _dev(np.concatenate([fc, [0]])),
+                      _dev(tp) if with_test else None, _dev(np.concatenate([tc, [0]])) if with_test else None, g1, t1)
+        assert np.array_equal(g1.view(3, k)[:nrank].cpu().numpy(), exp_g[:, r0:r1])
+        assert np.array_equal(t1.view(3, k)[:nrank].cpu().numpy(), exp_t[:, r0:r1])
+
+
+@pytest.mark.parametrize("d,m", [(512, 3000), (128, 1500)])
+def test_rank_rows_refinement_equals_exact_scoring(L, d, m):
+    """Candidate rows built as tiny perturbations of each query's true row give scores within
+    1e-7 .. 1e-5 of the true score: the bf16x3 contraction (error up to ~1e-5 of the row
+    maximum) puts many of them on the wrong side; the refined counts must equal the counts of
+    float64 dot products rounded to fp32 -- for the raw and the filtered ranking."""
+    rng = np.random.default_rng(d + m)
+    n = 48
+    q = (rng.standard_normal((n, d)) * 0.3).astype(np.float32)
+    t = (rng.standard_normal((m, d)) * 0.3).astype(np.float32)
+    true_idx = rng.choice(m, size=n, replace=False).astype(np.int64)
+    # 20 near-copies of every query's true row, at relative distances 1e-7 .. 1e-5
+    for i in range(n):
+        for c in range(20):
+            j = (true_idx[i] + 1 + c * 53 + i) % m
+            if j in true_idx:
+                continue
+            eps = 10.0 ** rng.uniform(-7, -5) * rng.choice([-1.0, 1.0])
+            t[j] = (t[true_idx[i]].astype(np.float64) * (1.0 + eps)
+                    + rng.standard_normal(d) * 1e-7).astype(np.float32)
+    exact = (q.astype(np.float64) @ t.astype(np.float64).T).astype(np.float32)
+    true_score = exact[np.arange(n), true_idx].copy()
+    f_ptr, f_col = _csr(rng, n, m, 30)
+    # filter lists that hit near-ties too: add each row's first near-copy
+    cols = [np.unique(np.append(f_col[f_ptr[i]:f_ptr[i + 1]], (true_idx[i] + 1 + i) % m)) for i in range(n)]
+    f_ptr = np.zeros(n + 1, np.int64)
+    np.cumsum([len(c) for c in cols], out=f_ptr[1:])
+    f_col = np.concatenate(cols).astype(np.int64)
+    exp = _oracle_counts(exact, 0, true_idx, true_score, [(f_ptr, f_col)])
+
+    qd, td = _dev(q), _dev(t)
+    hi, lo = L.split_rows(qd)
+    buf = torch.empty(n, (m + 3) // 4 * 4, device="cuda")
+    s = L.score_dot_split(hi, lo, td, None, d, out=buf[:, :m])
+    part = (_dev(true_idx), _dev(true_score), _dev(f_ptr), None)
+    f_col_d = _dev(np.concatenate([f_col, [0]]))
+
+    def counts(refine):
+        g = torch.empty(2 * n, dtype=torch.int64, device="cuda")
+        tt = torch.empty(2 * n, dtype=torch.int64, device="cuda")
+        L.rank_rows(s, n, 0, part, None, f_col_d, None, g, tt, accumulate=False, refine=refine)
+        return g.view(2, n).cpu().numpy(), tt.view(2, n).cpu().numpy()
+
+    tmax = L.row_norm_max(td)
+    assert float(tmax) == pytest.approx(np.linalg.norm(t.astype(np.float64), axis=1).max(), rel=1e-5)
+    g0, t0 = counts(None)
+    wrong = int((g0[0] != exp[0][0]).sum())
+    g1, t1 = counts((qd, td, 1e-4, tmax))
+    for r in range(2):
+        assert np.array_equal(g1[r], exp[r][0]), f"ranking {r}: refined 'greater' counts differ from exact scoring"
+        assert np.array_equal(t1[r], exp[r][1]), f"ranking {r}: refined tie counts differ from exact scoring"
+    # the inputs do exercise the refinement: plain bf16x3 scores mis-count some rows
+    assert wrong > 0, "test inputs too easy: bf16x3 ranked every near-tie correctly"
+    # the contraction's error is far inside the band the refinement assumes
+    err = np.abs(s.cpu().numpy().astype(np.float64) - q.astype(np.float64) @ t.astype(np.float64).T)
+    bound = np.linalg.norm(q.astype(np.float64), axis=1)[:, None] * float(tmax)
+    assert (err / bound).max() < 0.25e-4

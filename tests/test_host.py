@@ -70,7 +70,7 @@ def test_config_set_rejects_unknown_keys_and_wrong_types():
     c.set("train.optimizer_args.lr", 0.5)        # "+++" dictionaries take new keys
     c.set("brand_new.key", 3, create=True)
     assert c.get("train.optimizer_args.lr") == 0.5 and c.get("brand_new.key") == 3
-    assert c.get("engine.eval_precision") == "fp32"
+    assert c.get("engine.eval_precision") == "bf16x3_refined"
 
 
 def test_model_dims_match_reference_shapes():
