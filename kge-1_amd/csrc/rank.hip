@@ -137,23 +137,33 @@ struct RankRowsArgs {
   const float* t_norm_max;
 };
 
-__device__ __forceinline__ float exact_dot(const float* __restrict__ a, const float* __restrict__ b, int d) {
-  double acc0 = 0.0, acc1 = 0.0, acc2 = 0.0, acc3 = 0.0;
-  for (int k = 0; k < d; k += 4) {
+// Correctly rounded fp32 value of the exact dot product of two fp32 rows, computed by ONE
+// WAVE in a fixed order (lane l accumulates the float4 chunks l, l + 64, ... in fp64, then a
+// butterfly sum): every lane returns the same value, and the value depends on (a, b, d) only.
+__device__ __forceinline__ float exact_dot_wave(const float* __restrict__ a, const float* __restrict__ b, int d) {
+  const int lane = threadIdx.x & 63;
+  double acc = 0.0;
+  for (int k = 4 * lane; k < d; k += 256) {
     const float4 x = *reinterpret_cast<const float4*>(a + k);
     const float4 y = *reinterpret_cast<const float4*>(b + k);
-    acc0 = fma((double)x.x, (double)y.x, acc0);
-    acc1 = fma((double)x.y, (double)y.y, acc1);
-    acc2 = fma((double)x.z, (double)y.z, acc2);
-    acc3 = fma((double)x.w, (double)y.w, acc3);
+    acc = fma((double)x.x, (double)y.x, acc);
+    acc = fma((double)x.y, (double)y.y, acc);
+    acc = fma((double)x.z, (double)y.z, acc);
+    acc = fma((double)x.w, (double)y.w, acc);
   }
-  return (float)((acc0 + acc1) + (acc2 + acc3));
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) acc += __shfl_xor(acc, off, 64);
+  return (float)acc;
 }
 
-template <bool VEC>
+constexpr int EV_CAP = 8 * NT;  // near-tie ring: one scan step pushes at most 8 entries per thread
+
+template <bool VEC, bool REFINE>
 __global__ void __launch_bounds__(NT) rank_rows_kernel(const RankRowsArgs a) {
   __shared__ int64_t sm[16];
   __shared__ float fsm[NT / 64];
+  __shared__ int ev[REFINE ? EV_CAP : 1];
+  __shared__ unsigned ev_total;
   const int64_t i = blockIdx.x;
   const int side = i >= a.n_a;
   const int64_t li = side ? i - a.n_a : i;
@@ -162,50 +172,87 @@ __global__ void __launch_bounds__(NT) rank_rows_kernel(const RankRowsArgs a) {
   const int64_t tj = P.true_idx[li] - a.c0;
   const float* row = a.s + i * a.lds;
   const int64_t m = a.m;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
 
   float band = -1.f;  // no score satisfies |v - t| <= band
   const float* qrow = nullptr;
-  if (a.q) {
+  if (REFINE) {
     qrow = a.q + i * a.ldq;
     float ss = 0.f;
     for (int k = threadIdx.x; k < a.d; k += NT) ss += qrow[k] * qrow[k];
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) ss += __shfl_xor(ss, off, 64);
-    if ((threadIdx.x & 63) == 0) fsm[threadIdx.x >> 6] = ss;
+    if (lane == 0) fsm[wave] = ss;
+    if (threadIdx.x == 0) ev_total = 0;
     __syncthreads();
     ss = 0.f;
     for (int w = 0; w < NT / 64; ++w) ss += fsm[w];
     band = a.band_rel * sqrtf(ss) * a.t_norm_max[0];
   }
-  auto value = [&](int64_t j, float v) -> float {
-    if (j == tj) return t;
-    if (fabsf(v - t) <= band) v = exact_dot(qrow, a.t + j * a.ldt, a.d);
-    return clean(v);
-  };
 
+  // Counting one entry: the true column takes the true score; a score inside the band is
+  // deferred to the ring (REFINE) and counted after it has been rescored.
   int64_t gt = 0, eq = 0;
-  if (VEC) {
-    const int64_t m4 = m & ~(int64_t)3;
-    for (int64_t j = 4 * (int64_t)threadIdx.x; j < m4; j += 4 * NT) {
-      const float4 v4 = *reinterpret_cast<const float4*>(row + j);
-      const float v[4] = {v4.x, v4.y, v4.z, v4.w};
-#pragma unroll
-      for (int c = 0; c < 4; ++c) {
-        const float v_ = value(j + c, v[c]);
-        gt += v_ > t;
-        eq += v_ == t;
+  int pushed = 0;  // this thread deferred an entry since the last drain
+  auto count = [&](int64_t j, float v, int sign) {
+    if (j == tj) v = t;
+    else if (REFINE && fabsf(v - t) <= band) {
+      ev[atomicAdd(&ev_total, 1u) % EV_CAP] = (int)j;
+      pushed = 1;
+      return;
+    }
+    v = clean(v);
+    gt += sign * (v > t);
+    eq += sign * (v == t);
+  };
+  // Rescore and count the entries pushed since `done` (block-uniform control flow): wave w
+  // takes entries w, w + 4, ...; its lane 0 owns the counts.  Returns the new `done`.
+  auto drain = [&](unsigned done, int sign) -> unsigned {
+    // the barrier makes the pushes visible and tells every thread alike whether there are any
+    // (ev_total itself may already be moving again when a slower thread would read it)
+    const int any = __syncthreads_or(pushed);
+    pushed = 0;
+    if (!any) return done;
+    const unsigned total = ev_total;  // stable: nobody pushes before the barrier below
+    for (unsigned x = done + wave; x < total; x += NT / 64) {
+      const int64_t j = ev[x % EV_CAP];
+      const float v = clean(exact_dot_wave(qrow, a.t + j * a.ldt, a.d));
+      if (lane == 0) {
+        gt += sign * (v > t);
+        eq += sign * (v == t);
       }
     }
-    for (int64_t j = m4 + threadIdx.x; j < m; j += NT) {
-      const float v_ = value(j, row[j]);
-      gt += v_ > t;
-      eq += v_ == t;
+    __syncthreads();  // ring entries consumed before the next step overwrites them
+    return total;
+  };
+
+  unsigned done = 0;
+  if (VEC) {
+    const int64_t m4 = m & ~(int64_t)3;
+    for (int64_t base = 0; base < m4; base += 8 * NT) {  // uniform trip count
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int64_t j = base + 4 * (int64_t)(threadIdx.x + h * NT);
+        if (j < m4) {
+          const float4 v4 = *reinterpret_cast<const float4*>(row + j);
+          count(j, v4.x, 1);
+          count(j + 1, v4.y, 1);
+          count(j + 2, v4.z, 1);
+          count(j + 3, v4.w, 1);
+        }
+      }
+      if (REFINE) done = drain(done, 1);
     }
+    if (m4 + threadIdx.x < m) count(m4 + threadIdx.x, row[m4 + threadIdx.x], 1);
+    if (REFINE) done = drain(done, 1);
   } else {
-    for (int64_t j = threadIdx.x; j < m; j += NT) {
-      const float v_ = value(j, row[j]);
-      gt += v_ > t;
-      eq += v_ == t;
+    for (int64_t base = 0; base < m; base += 8 * NT) {
+#pragma unroll
+      for (int h = 0; h < 8; ++h) {
+        const int64_t j = base + threadIdx.x + h * NT;
+        if (j < m) count(j, row[j], 1);
+      }
+      if (REFINE) done = drain(done, 1);
     }
   }
   block_sum2(gt, eq, sm);
@@ -225,31 +272,37 @@ __global__ void __launch_bounds__(NT) rank_rows_kernel(const RankRowsArgs a) {
         atomicAdd(a.hist + (x / a.rows_per_hist) * a.hist_len + rank, 1.0f);
     }
   };
-  if (threadIdx.x == 0) emit(0, gt, eq);
+  int64_t g_run = 0, e_run = 0;  // thread 0: the running counts of the cumulative rankings
+  if (threadIdx.x == 0) {
+    g_run = gt;
+    e_run = eq;
+    emit(0, g_run, e_run);
+  }
   __syncthreads();
 
   const int nfilt = P.t_ptr ? 2 : (P.f_ptr ? 1 : 0);
-  int64_t dgt_f = 0, deq_f = 0;
   for (int r = 0; r < nfilt; ++r) {
     const int64_t* ptr = r == 0 ? P.f_ptr : P.t_ptr;
     const int64_t* col = r == 0 ? a.f_col : a.t_col;
-    int64_t dgt = 0, deq = 0;
-    if (ptr) {
-      const int64_t b = ptr[li], e = ptr[li + 1];
-      for (int64_t x = b + threadIdx.x; x < e; x += NT) {
+    gt = 0;
+    eq = 0;
+    const int64_t b = ptr[li], e = ptr[li + 1];
+    for (int64_t x0 = b; x0 < e; x0 += NT) {  // uniform trip count
+      const int64_t x = x0 + threadIdx.x;
+      if (x < e) {
         const int64_t j = col[x] - a.c0;
-        if (j < 0 || j >= m || j == tj) continue;
-        const float v = value(j, row[j]);
-        dgt -= v > t;
-        deq -= v == t;
-        deq += (t == -INFINITY);  // the filtered entry is now -inf
+        if (j >= 0 && j < m && j != tj) {
+          count(j, row[j], -1);
+          eq += (t == -INFINITY);  // the filtered entry is now -inf
+        }
       }
+      if (REFINE) done = drain(done, -1);
     }
-    block_sum2(dgt, deq, sm);
+    block_sum2(gt, eq, sm);
     if (threadIdx.x == 0) {
-      dgt_f += dgt;
-      deq_f += deq;
-      emit(1 + r, gt + dgt_f, eq + deq_f);
+      g_run += gt;
+      e_run += eq;
+      emit(1 + r, g_run, e_run);
     }
     __syncthreads();
   }
@@ -335,7 +388,8 @@ extern "C" int kge_rank_rows(const float* s, int64_t lds, int64_t n_a, int64_t n
                              int64_t ldq, const float* t, int64_t ldt, int d, float band_rel, const float* t_norm_max,
                              void* stream) {
   const int64_t n = n_a + n_b;
-  KGE_REQUIRE(n_a >= 0 && n_b >= 0 && m >= 0 && (m == 0 || s) && greater && ties && lds >= m && n < (1LL << 31));
+  KGE_REQUIRE(n_a >= 0 && n_b >= 0 && m >= 0 && m < (1LL << 31) && (m == 0 || s) && greater && ties && lds >= m &&
+              n < (1LL << 31));
   KGE_REQUIRE(n_a == 0 || (true_idx_a && true_score_a));
   KGE_REQUIRE(n_b == 0 || (true_idx_b && true_score_b));
   KGE_REQUIRE((!f_ptr_a && !f_ptr_b) || f_col);
@@ -358,10 +412,15 @@ extern "C" int kge_rank_rows(const float* s, int64_t lds, int64_t n_a, int64_t n
   a.tie = tie_handling; a.ranks = ranks; a.hist = hist; a.hist_len = hist_len; a.rows_per_hist = rows_per_hist;
   a.q = q; a.ldq = ldq; a.t = t; a.ldt = ldt; a.d = d; a.band_rel = band_rel; a.t_norm_max = t_norm_max;
   hipStream_t st = as_stream(stream);
-  if (lds % 4 == 0 && aligned16(s))
-    rank_rows_kernel<true><<<dim3((unsigned)n), dim3(NT), 0, st>>>(a);
+  const bool vec = lds % 4 == 0 && aligned16(s);
+  if (q && vec)
+    rank_rows_kernel<true, true><<<dim3((unsigned)n), dim3(NT), 0, st>>>(a);
+  else if (q)
+    rank_rows_kernel<false, true><<<dim3((unsigned)n), dim3(NT), 0, st>>>(a);
+  else if (vec)
+    rank_rows_kernel<true, false><<<dim3((unsigned)n), dim3(NT), 0, st>>>(a);
   else
-    rank_rows_kernel<false><<<dim3((unsigned)n), dim3(NT), 0, st>>>(a);
+    rank_rows_kernel<false, false><<<dim3((unsigned)n), dim3(NT), 0, st>>>(a);
   KGE_CHECK_LAUNCH();
   return 0;
 }
