@@ -137,23 +137,37 @@ struct RankRowsArgs {
   const float* t_norm_max;
 };
 
-// Correctly rounded fp32 value of the exact dot product of two fp32 rows, computed by ONE
-// WAVE in a fixed order (lane l accumulates the float4 chunks l, l + 64, ... in fp64, then a
-// butterfly sum): every lane returns the same value, and the value depends on (a, b, d) only.
-__device__ __forceinline__ float exact_dot_wave(const float* __restrict__ a, const float* __restrict__ b, int d) {
+// Correctly rounded fp32 values of the exact dot products of the fp32 row a with up to U fp32
+// rows b[u], computed by ONE WAVE in a fixed order per product (lane l accumulates the float4
+// chunks l, l + 64, ... in fp64, then a butterfly sum): every lane returns the same values,
+// and each value depends on (a, b[u], d) only -- not on U or on the other rows.  U products at
+// a time keep U row loads in flight.
+template <int U>
+__device__ __forceinline__ void exact_dots_wave(const float* __restrict__ a, const float* const (&b)[U], int d,
+                                                float (&out)[U]) {
   const int lane = threadIdx.x & 63;
-  double acc = 0.0;
+  double acc[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) acc[u] = 0.0;
   for (int k = 4 * lane; k < d; k += 256) {
     const float4 x = *reinterpret_cast<const float4*>(a + k);
-    const float4 y = *reinterpret_cast<const float4*>(b + k);
-    acc = fma((double)x.x, (double)y.x, acc);
-    acc = fma((double)x.y, (double)y.y, acc);
-    acc = fma((double)x.z, (double)y.z, acc);
-    acc = fma((double)x.w, (double)y.w, acc);
+    float4 y[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) y[u] = *reinterpret_cast<const float4*>(b[u] + k);
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      acc[u] = fma((double)x.x, (double)y[u].x, acc[u]);
+      acc[u] = fma((double)x.y, (double)y[u].y, acc[u]);
+      acc[u] = fma((double)x.z, (double)y[u].z, acc[u]);
+      acc[u] = fma((double)x.w, (double)y[u].w, acc[u]);
+    }
   }
 #pragma unroll
-  for (int off = 32; off > 0; off >>= 1) acc += __shfl_xor(acc, off, 64);
-  return (float)acc;
+  for (int off = 32; off > 0; off >>= 1)
+#pragma unroll
+    for (int u = 0; u < U; ++u) acc[u] += __shfl_xor(acc[u], off, 64);
+#pragma unroll
+  for (int u = 0; u < U; ++u) out[u] = (float)acc[u];
 }
 
 constexpr int EV_CAP = 8 * NT;  // near-tie ring: one scan step pushes at most 8 entries per thread
@@ -214,12 +228,24 @@ __global__ void __launch_bounds__(NT) rank_rows_kernel(const RankRowsArgs a) {
     pushed = 0;
     if (!any) return done;
     const unsigned total = ev_total;  // stable: nobody pushes before the barrier below
-    for (unsigned x = done + wave; x < total; x += NT / 64) {
-      const int64_t j = ev[x % EV_CAP];
-      const float v = clean(exact_dot_wave(qrow, a.t + j * a.ldt, a.d));
+    constexpr int U = 4;  // entries a wave rescores at a time: wave w takes w, w + 4, ...
+    for (unsigned x0 = done + wave; x0 < total; x0 += U * (NT / 64)) {
+      const float* rows_[U];
+      float v[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const unsigned x = x0 + u * (NT / 64);
+        rows_[u] = a.t + (int64_t)ev[(x < total ? x : x0) % EV_CAP] * a.ldt;  // idle slots redo the first
+      }
+      exact_dots_wave<U>(qrow, rows_, a.d, v);
       if (lane == 0) {
-        gt += sign * (v > t);
-        eq += sign * (v == t);
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          if (x0 + u * (NT / 64) >= total) continue;
+          const float v_ = clean(v[u]);
+          gt += sign * (v_ > t);
+          eq += sign * (v_ == t);
+        }
       }
     }
     __syncthreads();  // ring entries consumed before the next step overwrites them
@@ -308,21 +334,34 @@ __global__ void __launch_bounds__(NT) rank_rows_kernel(const RankRowsArgs a) {
   }
 }
 
-// out[0] = max over rows of the Euclidean row norm (out[0] must hold 0 on entry)
+// out[0] = max over rows of the Euclidean row norm (out[0] must hold 0 on entry): a wave per
+// row, 16 rows per wave, one atomic per workgroup
+constexpr int NORM_ROWS = 64;
 __global__ void __launch_bounds__(256) row_norm_max_kernel(const float* __restrict__ t, int64_t ldt, int64_t m, int d,
                                                            float* out) {
-  const int lane = threadIdx.x & 63;
-  const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-  float ss = 0.f;
-  if (r < m)
+  __shared__ float wmax[4];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  float best = 0.f;
+  for (int i = 0; i < NORM_ROWS / 4; ++i) {
+    const int64_t r = (int64_t)blockIdx.x * NORM_ROWS + wave * (NORM_ROWS / 4) + i;
+    if (r >= m) break;  // wave-uniform
+    float ss = 0.f;
     for (int k = lane; k < d; k += 64) {
       const float v = t[r * ldt + k];
       ss += v * v;
     }
 #pragma unroll
-  for (int off = 32; off > 0; off >>= 1) ss += __shfl_xor(ss, off, 64);
-  // non-negative floats order like their bit patterns; NaN rows poison the maximum upwards
-  if (lane == 0 && r < m) atomicMax(reinterpret_cast<unsigned*>(out), __float_as_uint(sqrtf(ss) * 1.000001f));
+    for (int off = 32; off > 0; off >>= 1) ss += __shfl_xor(ss, off, 64);
+    ss = sqrtf(ss) * 1.000001f;
+    best = (ss > best || ss != ss) ? ss : best;  // a NaN row poisons the maximum
+  }
+  if (lane == 0) wmax[wave] = best;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int w = 1; w < 4; ++w) best = (wmax[w] > best || wmax[w] != wmax[w]) ? wmax[w] : best;
+    // non-negative floats order like their bit patterns (NaN above every number)
+    atomicMax(reinterpret_cast<unsigned*>(out), __float_as_uint(best));
+  }
 }
 
 __global__ void zero1_kernel(float* out) { out[0] = 0.f; }
@@ -374,7 +413,8 @@ extern "C" int kge_row_norm_max(const float* t, int64_t ldt, int64_t m, int d, f
   KGE_REQUIRE(m >= 0 && d > 0 && (t || m == 0) && out && ldt >= d);
   hipStream_t st = as_stream(stream);
   zero1_kernel<<<dim3(1), dim3(1), 0, st>>>(out);
-  if (m > 0) row_norm_max_kernel<<<dim3((unsigned)((m + 3) / 4)), dim3(256), 0, st>>>(t, ldt, m, d, out);
+  if (m > 0)
+    row_norm_max_kernel<<<dim3((unsigned)((m + NORM_ROWS - 1) / NORM_ROWS)), dim3(256), 0, st>>>(t, ldt, m, d, out);
   KGE_CHECK_LAUNCH();
   return 0;
 }

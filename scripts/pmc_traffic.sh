@@ -2,8 +2,8 @@
 # HBM traffic of the headline contraction kernel per launch, as MI355X_MICROARCH.md §HBM
 # prescribes: separate --pmc passes for FETCH_SIZE and WRITE_SIZE (kernel-trace only, no
 # sys/runtime trace), FETCH_SIZE doubled for the 16-B-per-lane streaming reads on gfx950.
-# Writes gpurun_out/pmc_traffic/pmc_traffic.json (copy it to profiles/r01/, which bench.py
-# reports as roofline.traffic) and also refreshes profiles/r01/ in the box's copy of the repo.
+# Writes gpurun_out/pmc_traffic/pmc_traffic.json: copy it into this round's profiles/
+# directory, where bench.py reads roofline.traffic from.
 set -o pipefail
 export TMPDIR=/tmp
 OUT=$GRAFT_REPO_ROOT/gpurun_out/pmc_traffic
@@ -39,4 +39,3 @@ out = {"kernel": name, "dispatches": {k: len(v) for k, v in vals.items()},
 json.dump(out, open(dst, "w"), indent=1)
 print(json.dumps(out))
 EOF
-cp $OUT/pmc_traffic.json $GRAFT_REPO_ROOT/profiles/r02/pmc_traffic.json
