@@ -147,7 +147,7 @@ def eval_job(f, tag, precision):
     c._import("complex")
     c.set("job.device", "cuda")
     c.set("lookup_embedder.dim", meta["dim"])
-    c.set("engine.precision", precision)
+    c.set("engine.precision", precision.replace("_refined", ""))
     c.set("engine.eval_precision", precision)
     c.set("eval.batch_size", meta["batch_size"])
     c.set("eval.split", "valid")
@@ -156,7 +156,8 @@ def eval_job(f, tag, precision):
     c.set("dataset.num_relations", meta["R"])
     ds = Dataset(c, None)
     ds._triples = {k: torch.from_numpy(f["tri_" + k].astype(np.int32)) for k in ("train", "valid", "test")}
-    m = make_model("complex", meta["dim"], meta["E"], meta["R"], f["ent"], f["rel"], precision=precision)
+    m = make_model("complex", meta["dim"], meta["E"], meta["R"], f["ent"], f["rel"],
+                   precision=precision.replace("_refined", ""))
     m.config = c
     m.get_scorer().config = c
     job = EntityRankingJob(c, ds, model=m)
@@ -165,7 +166,8 @@ def eval_job(f, tag, precision):
     return job, trace
 
 
-@pytest.mark.parametrize("regime,precision", [("dyadic", "bf16x3"), ("dyadic", "fp32"), ("normal", "fp32")])
+@pytest.mark.parametrize("regime,precision", [("dyadic", "bf16x3"), ("dyadic", "fp32"), ("normal", "fp32"),
+                                              ("dyadic", "bf16x3_refined"), ("normal", "bf16x3_refined")])
 @pytest.mark.parametrize("tag", ["full", "chunk8"])
 def test_entity_ranking_vs_golden(regime, precision, tag):
     f = np.load(os.path.join(GOLDEN, f"eval_{regime}.npz"))

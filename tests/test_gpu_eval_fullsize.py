@@ -16,7 +16,7 @@ from oracle import kge_oracle as K
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("precision", ["bf16x3", "fp32"])
+@pytest.mark.parametrize("precision", ["bf16x3", "fp32", "bf16x3_refined"])
 def test_entity_ranking_fb15k237_size_dyadic(precision):
     from kge import Config, Dataset, KgeModel
     from kge.job import EntityRankingJob
@@ -26,8 +26,8 @@ def test_entity_ranking_fb15k237_size_dyadic(precision):
     c._import("complex")
     c.set("job.device", "cuda")
     c.set("lookup_embedder.dim", 512)
-    c.set("engine.precision", precision)
-    c.set("engine.eval_precision", precision)
+    c.set("engine.precision", precision.replace("_refined", ""))
+    c.set("engine.eval_precision", precision)  # refined: every exact tie of the true score is rescored
     c.set("eval.split", "test")
     c.set("eval.batch_size", 1024)
     c.set("verbose", False)

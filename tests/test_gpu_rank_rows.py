@@ -205,3 +205,62 @@ def test_rank_rows_refinement_equals_exact_scoring(L, d, m):
     err = np.abs(s.cpu().numpy().astype(np.float64) - q.astype(np.float64) @ t.astype(np.float64).T)
     bound = np.linalg.norm(q.astype(np.float64), axis=1)[:, None] * float(tmax)
     assert (err / bound).max() < 0.25e-4
+
+
+@pytest.mark.parametrize("model,dim", [("distmult", 64), ("rescal", 16), ("simple", 64), ("complex", 64), ("cp", 64),
+                                       ("transe", 64), ("rotate", 64)])
+@pytest.mark.parametrize("chunk", [-1, 700])
+def test_refined_eval_job_every_model_vs_exact_scoring(model, dim, chunk):
+    """EntityRankingJob with engine.eval_precision bf16x3_refined (the default) for every
+    scorer against the oracle's job on float64 scores rounded to fp32 (entity_ranking.py:79-577
+    restated): DistMult / RESCAL / SimplE / ComplEx take the refined bf16x3 path, CP and the
+    distance models fall back to fp32 scoring.  The engine prepares its query rows in fp32, so
+    a rank may differ from exact scoring only at a near-tie at the level of fp32 rounding:
+    every moved rank is checked against the float64 score row (1e-6 of the row maximum)."""
+    from test_gpu_configs import base_config, set_tables
+    from kge import Dataset, KgeModel
+    from kge.job import EntityRankingJob
+
+    E, R, n_eval = 2000, 11, 300
+    rng = np.random.default_rng(sum(map(ord, model)) + dim)
+    ent = (rng.standard_normal((E, dim)) * 0.3).astype(np.float32)
+
+    def triples(k):
+        return np.stack([rng.integers(0, E, k), rng.integers(0, R, k), rng.integers(0, E, k)], 1).astype(np.int64)
+
+    splits = {"train": triples(4000), "valid": triples(n_eval), "test": triples(500)}
+    # near-ties on purpose: entity rows that nearly repeat other rows
+    for j in range(0, 200, 2):
+        ent[1000 + j] = ent[j] * np.float32(1 + 3e-7 * (j % 5 - 2))
+    c = base_config(model, dim, E, R, {"eval.batch_size": 128, "eval.split": "valid",
+                                       "entity_ranking.chunk_size": chunk})
+    assert c.get("engine.eval_precision") == "bf16x3_refined"
+    ds = Dataset(c, None)
+    ds._triples = {k: torch.from_numpy(v.astype(np.int32)) for k, v in splits.items()}
+    m = KgeModel.create(c, ds)
+    d_r = m._relation_embedder._embeddings.weight.shape[1]  # config-derived (rotate d/2, rescal d^2, cp d/2)
+    rel = (rng.standard_normal((R, d_r)) * 0.3).astype(np.float32)
+    if model == "rotate":
+        rel = (rng.uniform(-np.pi, np.pi, (R, d_r))).astype(np.float32)
+    set_tables(m, ent, rel)
+    job = EntityRankingJob(c, ds, model=m)
+    job.capture_ranks = True
+    job.run()
+    l_norm = float(c.get(model + ".l_norm")) if model in K.DISTANCE else 1.0
+    ranks, _ = K.entity_ranking(model, ent, rel, splits, eval_split="valid", filter_splits=("train", "valid"),
+                                batch_size=128, l_norm=l_norm)
+    assert set(job.ranks) == set(ranks)
+    tri = splits["valid"]
+    moved = 0
+    for key, exp in ranks.items():
+        bad = np.flatnonzero(job.ranks[key] != exp)
+        moved += len(bad)
+        for i in bad:
+            s, p, o = tri[i:i + 1, 0], tri[i:i + 1, 1], tri[i:i + 1, 2]
+            sc = K.model_scores(model, ent, rel, s, p, o, np.arange(1), l_norm)
+            row = sc["sp_all"][0] if key[0] == "o" else sc["po_all"][0]
+            dist = np.abs(row - sc["spo"][0]) / np.abs(row).max()
+            dist[o[0] if key[0] == "o" else s[0]] = np.inf
+            delta = abs(int(job.ranks[key][i]) - int(exp[i]))
+            assert np.sort(dist)[delta - 1] <= 1e-6, (key, i, delta, np.sort(dist)[:delta])
+    assert moved <= 0.02 * sum(len(v) for v in ranks.values())
