@@ -472,6 +472,15 @@ def extras(args, model, c, E, R, device):
     with torch.no_grad():
         sec = timed_loop(lambda i: model.score_po(p[i], o[i]), 30, 10, 1)
     res["score_po_ms"] = round(sec * 1e3, 4)
+    # the same step with the query indexes handed over in (pageable) HOST memory: one H2D copy of
+    # 2 x 8 KB per step ahead of the kernels -- the PCIe-inclusive rate of the boundary (the
+    # scores stay on the device: their consumers are the loss / ranking kernels)
+    s_h = torch.randint(0, E, (40, B))
+    p_h = p.cpu()
+    with torch.no_grad():
+        sec = timed_loop(lambda i: model.score_sp(s_h[i].to(device), p_h[i].to(device)), 30, 10, 1)
+    res["score_sp_host_indexes_ms"] = round(sec * 1e3, 4)
+    res["score_sp_host_indexes_scored_triples_per_s"] = B * E / sec
     c2 = c.clone()
     ds = Dataset.synthetic(c2, args.dataset, seed=0)
     # filtered eval BEFORE any training step, on the N(0, 0.1) tables the CPU replica also gets:

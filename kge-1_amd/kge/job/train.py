@@ -123,7 +123,15 @@ class TrainingJob(Job):
                 self.kge_lr_scheduler.step(vtrace[metric_name])
             else:
                 self.kge_lr_scheduler.step()
+        self.sync_model()
         return traces
+
+    def sync_model(self):
+        """Make the model's tables complete on every rank: a row-sharded job all-gathers its
+        entity-row shards (a collective: every rank calls it); otherwise nothing to do."""
+        sharded = getattr(self, "_sharded", None)
+        if sharded is not None:
+            sharded.sync_model()
 
     def _validate(self) -> Dict[str, Any]:
         """Run the validation job (created on first use, train.py:77-84) on this model."""
