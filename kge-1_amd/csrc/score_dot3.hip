@@ -32,7 +32,8 @@ struct PCfg {
 // LDS scratch and leave as 256-B row segments of float4 stores.
 
 // ABL: dev-only ablation / probe switches (kge_dev_score_dot_persist): 1 = no score stores,
-// 2 = no staging after the prologue, 4 = per-workgroup clock probe written to row n of s.
+// 2 = no staging after the prologue, 4 = per-workgroup clock probe written to row n of s,
+// 8 = no barrier inside the K loop (timing only: the waves race on the LDS image).
 template <int BM, int BN, int WM, int WN, int ABL = 0>
 __global__ void __launch_bounds__(64 * WM * WN, 1)
     score_dot_persist16_kernel(const __bf16* __restrict__ qhi, const __bf16* __restrict__ qlo, int64_t ldq,
@@ -213,7 +214,7 @@ __global__ void __launch_bounds__(64 * WM * WN, 1)
       compute_x(cur, XS, TM);
       KGE_WAIT_VM(C::B_PER_T);  // A(st + 1) has landed
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();
+      if constexpr (!(ABL & 8)) __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");
     }
     KGE_WAIT_VM(0);
@@ -337,6 +338,8 @@ extern "C" int kge_dev_score_dot_persist(int variant, const void* qhi, const voi
     case 12: return launch_persist16<256, 256, 2, 4, 2>(h, l, ldq, t, ldt, tidx, n, m, d, s, lds, st);
     case 13: return launch_persist16<256, 256, 2, 4, 3>(h, l, ldq, t, ldt, tidx, n, m, d, s, lds, st);
     case 14: return launch_persist16<256, 256, 2, 4, 4>(h, l, ldq, t, ldt, tidx, n, m, d, s, lds, st);
+    case 18: return launch_persist16<256, 256, 2, 4, 8>(h, l, ldq, t, ldt, tidx, n, m, d, s, lds, st);
+    case 19: return launch_persist16<256, 256, 2, 4, 11>(h, l, ldq, t, ldt, tidx, n, m, d, s, lds, st);
     // one wave per SIMD, 128 x 128 wave tiles (accumulators in AGPRs)
     case 20: return launch_persist16<256, 256, 2, 2>(h, l, ldq, t, ldt, tidx, n, m, d, s, lds, st);
     case 24: return launch_persist16<256, 256, 2, 2, 4>(h, l, ldq, t, ldt, tidx, n, m, d, s, lds, st);
