@@ -260,10 +260,10 @@ __global__ void __launch_bounds__(NT) score_dist_bwd_kernel(float sign, const fl
 }  // namespace
 
 #ifdef KGE_DEV_BUILD  // libkgescore_dev.so only: A/B switch between the two kernels
-static int g_dist_impl = 2;  // 2: register-tiled kernel when applicable, 1: this file's kernel
+static int g_dist_impl = 2;  // 2: production choice, 1: always this file's kernel, 3: always the tiled kernel
 extern "C" int kge_dev_dist_impl(int impl) {
   const int old = g_dist_impl;
-  if (impl == 1 || impl == 2) g_dist_impl = impl;
+  if (impl >= 1 && impl <= 3) g_dist_impl = impl;
   return old;
 }
 #else
@@ -280,7 +280,10 @@ extern "C" int kge_score_dist(int kind, float sign, const float* q, int64_t ldq,
   if (n == 0 || m == 0) return 0;
   KGE_REQUIRE((n + TM - 1) / TM < 65536);
   hipStream_t st = as_stream(stream);
-  if (g_dist_impl == 2) {  // register-tiled kernel (score_dist2.hip) when the layout allows
+  // The register-tiled kernel (score_dist2.hip) when the layout allows -- except for RotatE-L1,
+  // whose per-pair v_sqrt and second accumulator plane run faster on this file's kernel
+  // (746 vs 843 us at B = 1024, E = 14,541, d = 512; the other kinds: 358-394 vs 433-498 us).
+  if (g_dist_impl == 3 || (g_dist_impl == 2 && kind != KGE_DIST_ROT_L1)) {
     const int r = kge_score_dist2(kind, sign, q, ldq, t, ldt, tidx, n, m, d, s, lds, st);
     if (r >= 0) return r;
   }

@@ -1,14 +1,16 @@
-// All-entities distance scoring for TransE / RotatE on packed-fp32 VALU (SURVEY.md §8a A9/A10;
-// no MFMA: the north star's "wavefront-reduced L1/L2 distance kernel").
+// All-entities distance scoring for TransE / RotatE on the VALU (no MFMA: a register-tiled,
+// wavefront-reduced L1 / L2 distance kernel).
 //
 // S[i, j] = sign * dist(Q[i], T[row(j)]), 128 x 128 output tile per 256-thread workgroup,
-// 8 x 8 outputs per thread held as 8 x 4 f32x2 pairs of adjacent columns, so the per-pair
-// arithmetic issues as v_pk_add_f32 / v_pk_mul_f32 / v_pk_fma_f32 (two lane-ops per
-// instruction; the scalar form was VALU-issue-bound at ~85 % of the non-packed rate):
-//   L1      : d = q - t (packed), acc += |d| (two v_add_f32 with |.| modifiers)  1.5 instr / pair
-//   L2      : d = q - t, acc = d * d + acc (packed)                              1   instr / pair
-//   ROT_L1  : dr, di packed, sq = dr dr + di di (packed), acc += sqrt(sq)        ~4.5 instr / pair
-//   ROT_L2  : dr, di packed, acc = dr dr + acc, acc = di di + acc (packed)       2   instr / pair
+// 8 x 8 outputs per thread held as 8 x 4 pairs of adjacent columns (plain scalar fp32 VALU:
+// the library is built with packed fp32 instructions switched off):
+//   L1      : d = q - t, acc += |d|                 (|.| as a source modifier)
+//   L2      : d = q - t, acc = d * d + acc
+//   ROT_L1  : dr, di, sq = dr dr + di di, acc += sqrt(sq)
+//   ROT_L2  : dr, di, acc = dr dr + acc, acc = di di + acc
+// Measured at B = 1024, E = 14,541, d = 512: L1 358 us, L2 360, RotatE-L2 394 (score_dist.hip's
+// kernel: 498 / 478 / 433); RotatE-L1 843 vs 746 us, so kge_score_dist keeps that kind on
+// score_dist.hip.
 // K is staged KC = 16 columns (complex components for RotatE) at a time, K-major in LDS,
 // double-buffered with the next chunk prefetched into registers (one barrier per chunk).
 // A thread owns rows {4 ty .. 4 ty + 3, 64 + 4 ty ..} and columns {4 tx .., 64 + 4 tx ..}:
