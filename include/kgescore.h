@@ -92,6 +92,24 @@ int kge_prep_query_split(int model, int dir, const float* ent, int64_t ld_ent,
                          const int64_t* ridx, int64_t n, int d_e, int d_r, float* q,
                          int64_t ldq, void* q_hi, void* q_lo, int64_t ldp, void* stream);
 
+/* kge_prep_query_split for TWO stacked query batches in one launch: rows [0, n_a) are prepared
+ * in direction dir_a, rows [n_a, n) in direction dir_b (eidx / ridx index all n rows) -- the
+ * (s, p, ?) and (?, p, o) halves of a 1vsAll / KvsAll step (train.py:1041-1057, 699-756) or of
+ * an evaluation batch (entity_ranking.py:153-168).  n_a_dev != NULL: the split point is read
+ * from device memory (a launch recorded in a HIP graph then serves batches whose split differs);
+ * n_a is ignored then. */
+int kge_prep_query_split2(int model, int dir_a, int dir_b, int64_t n_a, const int64_t* n_a_dev,
+                          const float* ent, int64_t ld_ent, const int64_t* eidx, const float* rel,
+                          int64_t ld_rel, const int64_t* ridx, int64_t n, int d_e, int d_r, float* q,
+                          int64_t ldq, void* q_hi, void* q_lo, int64_t ldp, void* stream);
+
+/* backward of kge_prep_query_split2 (see kge_prep_query_bwd) */
+int kge_prep_query_bwd2(int model, int dir_a, int dir_b, int64_t n_a, const int64_t* n_a_dev,
+                        const float* ent, int64_t ld_ent, const int64_t* eidx, const float* rel,
+                        int64_t ld_rel, const int64_t* ridx, int64_t n, int d_e, int d_r,
+                        const float* dq, int64_t lddq, float* d_ent, int64_t ld_dent, float* d_rel,
+                        int64_t ld_drel, void* stream);
+
 /* backward of kge_prep_query: scatter-adds dL/d(ent row) and dL/d(rel row) into
  * d_ent / d_rel (atomic fp32 adds; either may be NULL to skip). */
 int kge_prep_query_bwd(int model, int dir, const float* ent, int64_t ld_ent,
@@ -253,9 +271,11 @@ int kge_softmax_kl_planes(float* s, int64_t lds, int64_t n, int64_t n_pad, int64
 
 /* The per-row losses of a fused two-part step reduced in one launch, in a fixed order:
  * parts[0] = scale * sum loss[0 .. n_first), parts[1] = scale * sum loss[n_first .. n),
- * total[0] = parts[0] + parts[1]  (the sp_ and _po losses of train.py:1042-1053 and their sum). */
-int kge_loss_sums(const float* loss, int64_t n, int64_t n_first, float scale, float* parts, float* total,
-                  void* stream);
+ * total[0] = parts[0] + parts[1]  (the sp_ and _po losses of train.py:1042-1053 and their sum).
+ * n_first_dev != NULL: the split point is read from device memory instead (see
+ * kge_prep_query_split2). */
+int kge_loss_sums(const float* loss, int64_t n, int64_t n_first, const int64_t* n_first_dev, float scale,
+                  float* parts, float* total, void* stream);
 
 /* Vocab-parallel 1vsAll (entity table row-sharded): S holds columns
  * [c0, c0 + m) of the full score rows, labels are global column ids.

@@ -46,14 +46,20 @@ struct QOut {
   }
 };
 
+// Direction of query row i: rows [0, n_a) take direction a, the rest direction b (the stacked
+// sp_ / _po query batches of a training step or an evaluation batch in ONE launch).  n_a may
+// live in device memory (n_a_dev != null), so that a recorded launch serves batches whose
+// split differs.
+struct Dirs {
+  int a, b;
+  int64_t n_a;
+  const int64_t* n_a_dev;
+  __device__ __forceinline__ int of(int64_t i) const { return i < (n_a_dev ? *n_a_dev : n_a) ? a : b; }
+};
+
 // Elementwise models: complex / distmult / transe / rotate.  One block per query row.
 template <int MODEL, int DIR>
-__global__ void __launch_bounds__(256) prep_elementwise(const float* __restrict__ ent, int64_t ld_ent,
-                                                         const int64_t* __restrict__ eidx,
-                                                         const float* __restrict__ rel, int64_t ld_rel,
-                                                         const int64_t* __restrict__ ridx, int d_e, QOut out) {
-  const int64_t i = blockIdx.x;
-  Rows rw = fetch_rows(ent, ld_ent, eidx, rel, ld_rel, ridx, i);
+__device__ __forceinline__ void prep_row(const Rows rw, int64_t i, int d_e, const QOut& out) {
   out.pad(i, MODEL == KGE_CP ? d_e / 2 : d_e);
   if (MODEL == KGE_CP) {  // s_h * r (sp) / o_t * r (po), d_e / 2 columns
     const int h = d_e / 2;
@@ -95,19 +101,25 @@ __global__ void __launch_bounds__(256) prep_elementwise(const float* __restrict_
   }
 }
 
+template <int MODEL>
+__global__ void __launch_bounds__(256) prep_elementwise(const float* __restrict__ ent, int64_t ld_ent,
+                                                         const int64_t* __restrict__ eidx,
+                                                         const float* __restrict__ rel, int64_t ld_rel,
+                                                         const int64_t* __restrict__ ridx, int d_e, QOut out,
+                                                         Dirs dirs) {
+  const int64_t i = blockIdx.x;
+  const Rows rw = fetch_rows(ent, ld_ent, eidx, rel, ld_rel, ridx, i);
+  if (dirs.of(i) == KGE_DIR_SP)
+    prep_row<MODEL, KGE_DIR_SP>(rw, i, d_e, out);
+  else
+    prep_row<MODEL, KGE_DIR_PO>(rw, i, d_e, out);
+}
+
 // Vectorised elementwise prep: one wave per query row, 4 consecutive elements (complex
 // positions for ComplEx / RotatE) per lane per step, float4 loads, float4 / bf16x4 stores.
 // Needs d_e % 8 == 0 (complex halves % 4) and 16-B aligned rows (checked by the launcher).
 template <int MODEL, int DIR>
-__global__ void __launch_bounds__(256) prep_elementwise_vec(const float* __restrict__ ent, int64_t ld_ent,
-                                                             const int64_t* __restrict__ eidx,
-                                                             const float* __restrict__ rel, int64_t ld_rel,
-                                                             const int64_t* __restrict__ ridx, int64_t n, int d_e,
-                                                             QOut out) {
-  const int64_t i = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (i >= n) return;
-  const int lane = threadIdx.x & 63;
-  Rows rw = fetch_rows(ent, ld_ent, eidx, rel, ld_rel, ridx, i);
+__device__ __forceinline__ void prep_row_vec(const Rows rw, int64_t i, int lane, int d_e, const QOut& out) {
   auto put4 = [&](int k, float4 v) {
     if (out.q) *reinterpret_cast<float4*>(out.q + i * out.ldq + k) = v;
     if (out.hi) {
@@ -180,15 +192,25 @@ __global__ void __launch_bounds__(256) prep_elementwise_vec(const float* __restr
   }
 }
 
+template <int MODEL>
+__global__ void __launch_bounds__(256) prep_elementwise_vec(const float* __restrict__ ent, int64_t ld_ent,
+                                                             const int64_t* __restrict__ eidx,
+                                                             const float* __restrict__ rel, int64_t ld_rel,
+                                                             const int64_t* __restrict__ ridx, int64_t n, int d_e,
+                                                             QOut out, Dirs dirs) {
+  const int64_t i = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (i >= n) return;
+  const int lane = threadIdx.x & 63;
+  const Rows rw = fetch_rows(ent, ld_ent, eidx, rel, ld_rel, ridx, i);
+  if (dirs.of(i) == KGE_DIR_SP)  // wave-uniform
+    prep_row_vec<MODEL, KGE_DIR_SP>(rw, i, lane, d_e, out);
+  else
+    prep_row_vec<MODEL, KGE_DIR_PO>(rw, i, lane, d_e, out);
+}
+
 // RESCAL: Q = s^T M (sp) or M o (po), M = rel row viewed as [d, d] row-major.
 template <int DIR>
-__global__ void __launch_bounds__(256) prep_rescal(const float* __restrict__ ent, int64_t ld_ent,
-                                                    const int64_t* __restrict__ eidx,
-                                                    const float* __restrict__ rel, int64_t ld_rel,
-                                                    const int64_t* __restrict__ ridx, int d, QOut out) {
-  extern __shared__ float xs[];
-  const int64_t i = blockIdx.x;
-  Rows rw = fetch_rows(ent, ld_ent, eidx, rel, ld_rel, ridx, i);
+__device__ __forceinline__ void prep_rescal_row(const Rows rw, int64_t i, int d, const QOut& out, float* xs) {
   for (int k = threadIdx.x; k < d; k += blockDim.x) xs[k] = rw.e[k];
   out.pad(i, d);
   __syncthreads();
@@ -209,22 +231,27 @@ __global__ void __launch_bounds__(256) prep_rescal(const float* __restrict__ ent
   }
 }
 
+__global__ void __launch_bounds__(256) prep_rescal(const float* __restrict__ ent, int64_t ld_ent,
+                                                    const int64_t* __restrict__ eidx,
+                                                    const float* __restrict__ rel, int64_t ld_rel,
+                                                    const int64_t* __restrict__ ridx, int d, QOut out, Dirs dirs) {
+  extern __shared__ float xs[];
+  const int64_t i = blockIdx.x;
+  const Rows rw = fetch_rows(ent, ld_ent, eidx, rel, ld_rel, ridx, i);
+  if (dirs.of(i) == KGE_DIR_SP)  // block-uniform: the barrier inside is reached by every thread
+    prep_rescal_row<KGE_DIR_SP>(rw, i, d, out, xs);
+  else
+    prep_rescal_row<KGE_DIR_PO>(rw, i, d, out, xs);
+}
+
 // ---------------------------------------------------------------------- backward
 __device__ __forceinline__ void atomic_add_row(float* base, int k, float v) {
   if (base) atomicAdd(base + k, v);
 }
 
 template <int MODEL, int DIR>
-__global__ void __launch_bounds__(256) prep_elementwise_bwd(
-    const float* __restrict__ ent, int64_t ld_ent, const int64_t* __restrict__ eidx,
-    const float* __restrict__ rel, int64_t ld_rel, const int64_t* __restrict__ ridx, int d_e,
-    const float* __restrict__ dq, int64_t lddq, float* d_ent, int64_t ld_dent, float* d_rel,
-    int64_t ld_drel) {
-  const int64_t i = blockIdx.x;
-  Rows rw = fetch_rows(ent, ld_ent, eidx, rel, ld_rel, ridx, i);
-  const float* g = dq + i * lddq;
-  float* ge = d_ent ? d_ent + (eidx ? eidx[i] : i) * ld_dent : nullptr;
-  float* gr = d_rel ? d_rel + (ridx ? ridx[i] : i) * ld_drel : nullptr;
+__device__ __forceinline__ void prep_row_bwd(const Rows rw, int d_e, const float* __restrict__ g, float* ge,
+                                             float* gr) {
   if (MODEL == KGE_CP) {
     const int h = d_e / 2, off = DIR == KGE_DIR_SP ? 0 : h;
     for (int k = threadIdx.x; k < h; k += blockDim.x) {
@@ -288,24 +315,26 @@ __global__ void __launch_bounds__(256) prep_elementwise_bwd(
   }
 }
 
-template <int DIR>
-__global__ void __launch_bounds__(256) prep_rescal_bwd(
+template <int MODEL>
+__global__ void __launch_bounds__(256) prep_elementwise_bwd(
     const float* __restrict__ ent, int64_t ld_ent, const int64_t* __restrict__ eidx,
-    const float* __restrict__ rel, int64_t ld_rel, const int64_t* __restrict__ ridx, int d,
+    const float* __restrict__ rel, int64_t ld_rel, const int64_t* __restrict__ ridx, int d_e,
     const float* __restrict__ dq, int64_t lddq, float* d_ent, int64_t ld_dent, float* d_rel,
-    int64_t ld_drel) {
-  extern __shared__ float sm[];
-  float* xs = sm;      // entity row
-  float* gs = sm + d;  // dq row
+    int64_t ld_drel, Dirs dirs) {
   const int64_t i = blockIdx.x;
-  Rows rw = fetch_rows(ent, ld_ent, eidx, rel, ld_rel, ridx, i);
-  for (int k = threadIdx.x; k < d; k += blockDim.x) {
-    xs[k] = rw.e[k];
-    gs[k] = dq[i * lddq + k];
-  }
-  __syncthreads();
+  const Rows rw = fetch_rows(ent, ld_ent, eidx, rel, ld_rel, ridx, i);
+  const float* g = dq + i * lddq;
   float* ge = d_ent ? d_ent + (eidx ? eidx[i] : i) * ld_dent : nullptr;
   float* gr = d_rel ? d_rel + (ridx ? ridx[i] : i) * ld_drel : nullptr;
+  if (dirs.of(i) == KGE_DIR_SP)
+    prep_row_bwd<MODEL, KGE_DIR_SP>(rw, d_e, g, ge, gr);
+  else
+    prep_row_bwd<MODEL, KGE_DIR_PO>(rw, d_e, g, ge, gr);
+}
+
+template <int DIR>
+__device__ __forceinline__ void prep_rescal_row_bwd(const Rows rw, int d, const float* xs, const float* gs, float* ge,
+                                                    float* gr) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
   // dM[a][b] = x_a g_b (sp) or g_a x_b (po)
   if (gr) {
@@ -332,9 +361,31 @@ __global__ void __launch_bounds__(256) prep_rescal_bwd(
   }
 }
 
-template <int DIR>
+__global__ void __launch_bounds__(256) prep_rescal_bwd(
+    const float* __restrict__ ent, int64_t ld_ent, const int64_t* __restrict__ eidx,
+    const float* __restrict__ rel, int64_t ld_rel, const int64_t* __restrict__ ridx, int d,
+    const float* __restrict__ dq, int64_t lddq, float* d_ent, int64_t ld_dent, float* d_rel,
+    int64_t ld_drel, Dirs dirs) {
+  extern __shared__ float sm[];
+  float* xs = sm;      // entity row
+  float* gs = sm + d;  // dq row
+  const int64_t i = blockIdx.x;
+  const Rows rw = fetch_rows(ent, ld_ent, eidx, rel, ld_rel, ridx, i);
+  for (int k = threadIdx.x; k < d; k += blockDim.x) {
+    xs[k] = rw.e[k];
+    gs[k] = dq[i * lddq + k];
+  }
+  __syncthreads();
+  float* ge = d_ent ? d_ent + (eidx ? eidx[i] : i) * ld_dent : nullptr;
+  float* gr = d_rel ? d_rel + (ridx ? ridx[i] : i) * ld_drel : nullptr;
+  if (dirs.of(i) == KGE_DIR_SP)
+    prep_rescal_row_bwd<KGE_DIR_SP>(rw, d, xs, gs, ge, gr);
+  else
+    prep_rescal_row_bwd<KGE_DIR_PO>(rw, d, xs, gs, ge, gr);
+}
+
 int launch_prep(int model, const float* ent, int64_t ld_ent, const int64_t* eidx, const float* rel,
-                int64_t ld_rel, const int64_t* ridx, int64_t n, int d_e, QOut q, hipStream_t st) {
+                int64_t ld_rel, const int64_t* ridx, int64_t n, int d_e, QOut q, Dirs dirs, hipStream_t st) {
   dim3 grid((unsigned)n), block(256);
   const bool halves = model == KGE_COMPLEX || model == KGE_ROTATE || model == KGE_CP || model == KGE_SIMPLE;
   const int unit = halves ? d_e / 2 : d_e;
@@ -346,22 +397,22 @@ int launch_prep(int model, const float* ent, int64_t ld_ent, const int64_t* eidx
     const dim3 g4((unsigned)((n + 3) / 4));
     switch (model) {
       case KGE_COMPLEX:
-        prep_elementwise_vec<KGE_COMPLEX, DIR><<<g4, block, 0, st>>>(ent, ld_ent, eidx, rel, ld_rel, ridx, n, d_e, q);
+        prep_elementwise_vec<KGE_COMPLEX><<<g4, block, 0, st>>>(ent, ld_ent, eidx, rel, ld_rel, ridx, n, d_e, q, dirs);
         break;
       case KGE_DISTMULT:
-        prep_elementwise_vec<KGE_DISTMULT, DIR><<<g4, block, 0, st>>>(ent, ld_ent, eidx, rel, ld_rel, ridx, n, d_e, q);
+        prep_elementwise_vec<KGE_DISTMULT><<<g4, block, 0, st>>>(ent, ld_ent, eidx, rel, ld_rel, ridx, n, d_e, q, dirs);
         break;
       case KGE_TRANSE:
-        prep_elementwise_vec<KGE_TRANSE, DIR><<<g4, block, 0, st>>>(ent, ld_ent, eidx, rel, ld_rel, ridx, n, d_e, q);
+        prep_elementwise_vec<KGE_TRANSE><<<g4, block, 0, st>>>(ent, ld_ent, eidx, rel, ld_rel, ridx, n, d_e, q, dirs);
         break;
       case KGE_CP:
-        prep_elementwise_vec<KGE_CP, DIR><<<g4, block, 0, st>>>(ent, ld_ent, eidx, rel, ld_rel, ridx, n, d_e, q);
+        prep_elementwise_vec<KGE_CP><<<g4, block, 0, st>>>(ent, ld_ent, eidx, rel, ld_rel, ridx, n, d_e, q, dirs);
         break;
       case KGE_SIMPLE:
-        prep_elementwise_vec<KGE_SIMPLE, DIR><<<g4, block, 0, st>>>(ent, ld_ent, eidx, rel, ld_rel, ridx, n, d_e, q);
+        prep_elementwise_vec<KGE_SIMPLE><<<g4, block, 0, st>>>(ent, ld_ent, eidx, rel, ld_rel, ridx, n, d_e, q, dirs);
         break;
       default:
-        prep_elementwise_vec<KGE_ROTATE, DIR><<<g4, block, 0, st>>>(ent, ld_ent, eidx, rel, ld_rel, ridx, n, d_e, q);
+        prep_elementwise_vec<KGE_ROTATE><<<g4, block, 0, st>>>(ent, ld_ent, eidx, rel, ld_rel, ridx, n, d_e, q, dirs);
         break;
     }
     KGE_CHECK_LAUNCH();
@@ -369,25 +420,25 @@ int launch_prep(int model, const float* ent, int64_t ld_ent, const int64_t* eidx
   }
   switch (model) {
     case KGE_COMPLEX:
-      prep_elementwise<KGE_COMPLEX, DIR><<<grid, block, 0, st>>>(ent, ld_ent, eidx, rel, ld_rel, ridx, d_e, q);
+      prep_elementwise<KGE_COMPLEX><<<grid, block, 0, st>>>(ent, ld_ent, eidx, rel, ld_rel, ridx, d_e, q, dirs);
       break;
     case KGE_DISTMULT:
-      prep_elementwise<KGE_DISTMULT, DIR><<<grid, block, 0, st>>>(ent, ld_ent, eidx, rel, ld_rel, ridx, d_e, q);
+      prep_elementwise<KGE_DISTMULT><<<grid, block, 0, st>>>(ent, ld_ent, eidx, rel, ld_rel, ridx, d_e, q, dirs);
       break;
     case KGE_TRANSE:
-      prep_elementwise<KGE_TRANSE, DIR><<<grid, block, 0, st>>>(ent, ld_ent, eidx, rel, ld_rel, ridx, d_e, q);
+      prep_elementwise<KGE_TRANSE><<<grid, block, 0, st>>>(ent, ld_ent, eidx, rel, ld_rel, ridx, d_e, q, dirs);
       break;
     case KGE_ROTATE:
-      prep_elementwise<KGE_ROTATE, DIR><<<grid, block, 0, st>>>(ent, ld_ent, eidx, rel, ld_rel, ridx, d_e, q);
+      prep_elementwise<KGE_ROTATE><<<grid, block, 0, st>>>(ent, ld_ent, eidx, rel, ld_rel, ridx, d_e, q, dirs);
       break;
     case KGE_CP:
-      prep_elementwise<KGE_CP, DIR><<<grid, block, 0, st>>>(ent, ld_ent, eidx, rel, ld_rel, ridx, d_e, q);
+      prep_elementwise<KGE_CP><<<grid, block, 0, st>>>(ent, ld_ent, eidx, rel, ld_rel, ridx, d_e, q, dirs);
       break;
     case KGE_SIMPLE:
-      prep_elementwise<KGE_SIMPLE, DIR><<<grid, block, 0, st>>>(ent, ld_ent, eidx, rel, ld_rel, ridx, d_e, q);
+      prep_elementwise<KGE_SIMPLE><<<grid, block, 0, st>>>(ent, ld_ent, eidx, rel, ld_rel, ridx, d_e, q, dirs);
       break;
     case KGE_RESCAL:
-      prep_rescal<DIR><<<grid, block, d_e * sizeof(float), st>>>(ent, ld_ent, eidx, rel, ld_rel, ridx, d_e, q);
+      prep_rescal<<<grid, block, d_e * sizeof(float), st>>>(ent, ld_ent, eidx, rel, ld_rel, ridx, d_e, q, dirs);
       break;
     default:
       return KGE_ERR_ARG;
@@ -396,15 +447,14 @@ int launch_prep(int model, const float* ent, int64_t ld_ent, const int64_t* eidx
   return 0;
 }
 
-template <int DIR>
 int launch_prep_bwd(int model, const float* ent, int64_t ld_ent, const int64_t* eidx, const float* rel,
                     int64_t ld_rel, const int64_t* ridx, int64_t n, int d_e, const float* dq,
-                    int64_t lddq, float* d_ent, int64_t ld_dent, float* d_rel, int64_t ld_drel,
+                    int64_t lddq, float* d_ent, int64_t ld_dent, float* d_rel, int64_t ld_drel, Dirs dirs,
                     hipStream_t st) {
   dim3 grid((unsigned)n), block(256);
 #define KGE_PB(M)                                                                          \
-  prep_elementwise_bwd<M, DIR><<<grid, block, 0, st>>>(ent, ld_ent, eidx, rel, ld_rel, ridx, \
-                                                       d_e, dq, lddq, d_ent, ld_dent, d_rel, ld_drel)
+  prep_elementwise_bwd<M><<<grid, block, 0, st>>>(ent, ld_ent, eidx, rel, ld_rel, ridx, d_e, dq, lddq, d_ent, \
+                                                  ld_dent, d_rel, ld_drel, dirs)
   switch (model) {
     case KGE_COMPLEX: KGE_PB(KGE_COMPLEX); break;
     case KGE_DISTMULT: KGE_PB(KGE_DISTMULT); break;
@@ -413,8 +463,8 @@ int launch_prep_bwd(int model, const float* ent, int64_t ld_ent, const int64_t* 
     case KGE_CP: KGE_PB(KGE_CP); break;
     case KGE_SIMPLE: KGE_PB(KGE_SIMPLE); break;
     case KGE_RESCAL:
-      prep_rescal_bwd<DIR><<<grid, block, 2 * d_e * sizeof(float), st>>>(
-          ent, ld_ent, eidx, rel, ld_rel, ridx, d_e, dq, lddq, d_ent, ld_dent, d_rel, ld_drel);
+      prep_rescal_bwd<<<grid, block, 2 * d_e * sizeof(float), st>>>(
+          ent, ld_ent, eidx, rel, ld_rel, ridx, d_e, dq, lddq, d_ent, ld_dent, d_rel, ld_drel, dirs);
       break;
     default:
       return KGE_ERR_ARG;
@@ -453,31 +503,43 @@ extern "C" int kge_prep_query_split(int model, int dir, const float* ent, int64_
                                     const float* rel, int64_t ld_rel, const int64_t* ridx, int64_t n, int d_e,
                                     int d_r, float* q, int64_t ldq, void* q_hi, void* q_lo, int64_t ldp,
                                     void* stream) {
+  return kge_prep_query_split2(model, dir, dir, 0, nullptr, ent, ld_ent, eidx, rel, ld_rel, ridx, n, d_e, d_r, q, ldq,
+                               q_hi, q_lo, ldp, stream);
+}
+
+extern "C" int kge_prep_query_split2(int model, int dir_a, int dir_b, int64_t n_a, const int64_t* n_a_dev,
+                                     const float* ent, int64_t ld_ent, const int64_t* eidx, const float* rel,
+                                     int64_t ld_rel, const int64_t* ridx, int64_t n, int d_e, int d_r, float* q,
+                                     int64_t ldq, void* q_hi, void* q_lo, int64_t ldp, void* stream) {
   if (int e = check_dims(model, d_e, d_r)) return e;
   KGE_REQUIRE(n >= 0 && ent && rel && (q || q_hi));
   KGE_REQUIRE(!q || ldq >= query_width(model, d_e));
   KGE_REQUIRE(!q_hi || (q_lo && ldp >= query_width(model, d_e) && ldp % 8 == 0));
+  KGE_REQUIRE((dir_a == KGE_DIR_SP || dir_a == KGE_DIR_PO) && (dir_b == KGE_DIR_SP || dir_b == KGE_DIR_PO));
+  KGE_REQUIRE(n_a >= 0);
   if (n == 0) return 0;
   QOut out{q, ldq, (__bf16*)q_hi, (__bf16*)q_lo, ldp};
-  hipStream_t st = as_stream(stream);
-  if (dir == KGE_DIR_SP) return launch_prep<KGE_DIR_SP>(model, ent, ld_ent, eidx, rel, ld_rel, ridx, n, d_e, out, st);
-  if (dir == KGE_DIR_PO) return launch_prep<KGE_DIR_PO>(model, ent, ld_ent, eidx, rel, ld_rel, ridx, n, d_e, out, st);
-  return KGE_ERR_ARG;
+  return launch_prep(model, ent, ld_ent, eidx, rel, ld_rel, ridx, n, d_e, out, Dirs{dir_a, dir_b, n_a, n_a_dev},
+                     as_stream(stream));
 }
 
 extern "C" int kge_prep_query_bwd(int model, int dir, const float* ent, int64_t ld_ent, const int64_t* eidx,
                                   const float* rel, int64_t ld_rel, const int64_t* ridx, int64_t n, int d_e,
                                   int d_r, const float* dq, int64_t lddq, float* d_ent, int64_t ld_dent,
                                   float* d_rel, int64_t ld_drel, void* stream) {
+  return kge_prep_query_bwd2(model, dir, dir, 0, nullptr, ent, ld_ent, eidx, rel, ld_rel, ridx, n, d_e, d_r, dq, lddq,
+                             d_ent, ld_dent, d_rel, ld_drel, stream);
+}
+
+extern "C" int kge_prep_query_bwd2(int model, int dir_a, int dir_b, int64_t n_a, const int64_t* n_a_dev,
+                                   const float* ent, int64_t ld_ent, const int64_t* eidx, const float* rel,
+                                   int64_t ld_rel, const int64_t* ridx, int64_t n, int d_e, int d_r, const float* dq,
+                                   int64_t lddq, float* d_ent, int64_t ld_dent, float* d_rel, int64_t ld_drel,
+                                   void* stream) {
   if (int e = check_dims(model, d_e, d_r)) return e;
-  KGE_REQUIRE(n >= 0 && ent && rel && dq);
+  KGE_REQUIRE(n >= 0 && ent && rel && dq && n_a >= 0);
+  KGE_REQUIRE((dir_a == KGE_DIR_SP || dir_a == KGE_DIR_PO) && (dir_b == KGE_DIR_SP || dir_b == KGE_DIR_PO));
   if (n == 0 || (!d_ent && !d_rel)) return 0;
-  hipStream_t st = as_stream(stream);
-  if (dir == KGE_DIR_SP)
-    return launch_prep_bwd<KGE_DIR_SP>(model, ent, ld_ent, eidx, rel, ld_rel, ridx, n, d_e, dq, lddq, d_ent,
-                                       ld_dent, d_rel, ld_drel, st);
-  if (dir == KGE_DIR_PO)
-    return launch_prep_bwd<KGE_DIR_PO>(model, ent, ld_ent, eidx, rel, ld_rel, ridx, n, d_e, dq, lddq, d_ent,
-                                       ld_dent, d_rel, ld_drel, st);
-  return KGE_ERR_ARG;
+  return launch_prep_bwd(model, ent, ld_ent, eidx, rel, ld_rel, ridx, n, d_e, dq, lddq, d_ent, ld_dent, d_rel, ld_drel,
+                         Dirs{dir_a, dir_b, n_a, n_a_dev}, as_stream(stream));
 }

@@ -477,9 +477,10 @@ int launch_planes(float* s, int64_t lds, int64_t n, int64_t n_pad, int64_t m, co
 // parts[0] = scale * sum of loss[0 .. n_first), parts[1] = scale * sum of loss[n_first .. n),
 // total[0] = parts[0] + parts[1]: one workgroup, fixed summation order (deterministic).
 __global__ void __launch_bounds__(256) loss_sums_kernel(const float* __restrict__ loss, int64_t n, int64_t n_first,
-                                                        float scale, float* __restrict__ parts,
-                                                        float* __restrict__ total) {
+                                                        const int64_t* __restrict__ n_first_dev, float scale,
+                                                        float* __restrict__ parts, float* __restrict__ total) {
   __shared__ float red[256 / 64];
+  if (n_first_dev) n_first = *n_first_dev;
   float a = 0.f, b = 0.f;
   for (int64_t i = threadIdx.x; i < n; i += 256) {
     const float v = loss[i];
@@ -499,10 +500,10 @@ __global__ void __launch_bounds__(256) loss_sums_kernel(const float* __restrict_
 
 }  // namespace
 
-extern "C" int kge_loss_sums(const float* loss, int64_t n, int64_t n_first, float scale, float* parts, float* total,
-                             void* stream) {
+extern "C" int kge_loss_sums(const float* loss, int64_t n, int64_t n_first, const int64_t* n_first_dev, float scale,
+                             float* parts, float* total, void* stream) {
   KGE_REQUIRE(n >= 0 && n_first >= 0 && n_first <= n && (loss || n == 0) && parts && total);
-  loss_sums_kernel<<<dim3(1), dim3(256), 0, as_stream(stream)>>>(loss, n, n_first, scale, parts, total);
+  loss_sums_kernel<<<dim3(1), dim3(256), 0, as_stream(stream)>>>(loss, n, n_first, n_first_dev, scale, parts, total);
   KGE_CHECK_LAUNCH();
   return 0;
 }

@@ -163,23 +163,44 @@ class _ScoreXent(torch.autograd.Function):
         return None, None, None, None, d_ent, None, d_rel, None, d_tab, None, None, None, None, None
 
 
-class _ScoreXentPlanes(torch.autograd.Function):
-    """The fused loss of one or two query batches against every row of the entity table with
-    its gradient kept as bf16 hi / lo PLANES (bf16x3 precision): the queries of all parts are
-    prepared straight into one block of hi / lo planes, one contraction writes the scores, the
-    loss kernel turns them in place into the planes of G = scale * dloss/dS, and the backward
-    GEMMs read G and Q from those planes by LDS-DMA (kge_score_dot_bwd_q_planes /
-    _t_planes): no fp32 copy of Q, no split per tile, dT written (not accumulated).
-    Returns (total, parts): total = scale * sum of all rows' losses carries the gradient;
-    parts[k] = scale * sum of part k's rows is a detached view for reporting."""
+class StackedQueries:
+    """Two query batches stacked by rows: rows [0, n_a) are direction dir_a queries, rows
+    [n_a, n) direction dir_b queries; eidx / ridx index all n rows.  n_a_dev (an int64 device
+    scalar) overrides n_a on the device, so that a recorded step serves batches whose split
+    differs (the host then only knows n)."""
+
+    def __init__(self, dir_a, dir_b, eidx, ridx, n_a, n_a_dev=None):
+        self.dir_a, self.dir_b, self.eidx, self.ridx, self.n_a, self.n_a_dev = dir_a, dir_b, eidx, ridx, n_a, n_a_dev
 
     @staticmethod
-    def forward(ctx, kind, ent, rel, parts, labels, l_ptr, smoothing, scale):
+    def of(parts):
+        """From one or two (direction, eidx, ridx) batches (no copy when the index vectors of
+        the second already follow the first's in memory)."""
+        if len(parts) == 1:
+            d, e, r = parts[0]
+            return StackedQueries(d, d, L.idx64(e), L.idx64(r), e.numel())
+        (da, ea, ra), (db, eb, rb) = parts
+        ea, ra, eb, rb = L.idx64(ea), L.idx64(ra), L.idx64(eb), L.idx64(rb)
+        return StackedQueries(da, db, L.adjacent_or_cat(ea, eb), L.adjacent_or_cat(ra, rb), ea.numel())
+
+
+class _ScoreXentPlanes(torch.autograd.Function):
+    """The fused loss of one or two stacked query batches against every row of the entity table
+    with its gradient kept as bf16 hi / lo PLANES (bf16x3 precision): ONE preparation launch
+    writes the queries of both parts straight into one block of hi / lo planes, one
+    contraction writes the scores, the loss kernel turns them in place into the planes of
+    G = scale * dloss/dS, and the backward GEMMs read G and Q from those planes by LDS-DMA
+    (kge_score_dot_bwd_q_planes / _t_planes): no fp32 copy of Q, no split per tile, dT written
+    (not accumulated).  Returns (total, parts): total = scale * sum of all rows' losses carries
+    the gradient; parts = scale * (sum of the first batch's rows, sum of the second's) is
+    detached (for reporting)."""
+
+    @staticmethod
+    def forward(ctx, kind, ent, rel, sq, labels, l_ptr, smoothing, scale):
         ent, rel = _rows(ent), _rows(rel)
-        sizes = [p[1].numel() for p in parts]
-        n, m = sum(sizes), ent.shape[0]
+        n, m = sq.eidx.numel(), ent.shape[0]
         d_e, d_r = ent.shape[1], rel.shape[1]
-        qw, tab_w = L.query_width(kind, d_e), window(kind, parts[0][0], ent)
+        qw, tab_w = L.query_width(kind, d_e), window(kind, sq.dir_a, ent)
         n_pad, ld = L.planes_layout(n, m)
         buf = torch.empty(n_pad, ld, device=ent.device, dtype=torch.float32)
         ldp = (qw + 31) // 32 * 32
@@ -188,17 +209,14 @@ class _ScoreXentPlanes(torch.autograd.Function):
         if n_pad > n:  # K padding of the dT GEMM
             hi[n:].zero_()
             lo[n:].zero_()
-        r0 = 0
-        for (dr, ei, ri), k in zip(parts, sizes):
-            L.prep_query_split(kind, dr, ent, ei, rel, ri, k, d_e, d_r, out=(None, hi[r0:r0 + k], lo[r0:r0 + k]))
-            r0 += k
+        L.prep_query_split2(kind, sq.dir_a, sq.dir_b, sq.n_a, sq.n_a_dev, ent, sq.eidx, rel, sq.ridx, d_e, d_r,
+                            out=(None, hi[:n], lo[:n]))
         _timed(L.score_dot_split, hi[:n], lo[:n], tab_w, None, qw, out=buf[:n, :m])
         loss_rows, _ = L.softmax_planes(buf, n, m, labels, l_ptr, smoothing, scale)
-        ctx.meta = (kind, n, m, d_e, d_r, [(p[0], k) for p, k in zip(parts, sizes)])
-        ctx.save_for_backward(ent, rel, hi, lo, buf, *[t for p in parts for t in p[1:]])
-        total, per_part = L.loss_sums(loss_rows, sizes[0], scale)  # one launch, fixed order
-        if len(parts) == 1:
-            per_part = per_part[:1]
+        ctx.meta = (kind, n, m, d_e, d_r, sq.dir_a, sq.dir_b, sq.n_a, sq.n_a_dev is not None)
+        ctx.save_for_backward(ent, rel, hi, lo, buf, sq.eidx, sq.ridx,
+                              sq.n_a_dev if sq.n_a_dev is not None else sq.eidx.new_empty(0))
+        total, per_part = L.loss_sums(loss_rows, sq.n_a, scale, sq.n_a_dev)  # one launch, fixed order
         ctx.mark_non_differentiable(per_part)
         ctx.set_materialize_grads(False)  # no zero tensor for the detached parts' gradient
         return total, per_part
@@ -207,23 +225,21 @@ class _ScoreXentPlanes(torch.autograd.Function):
     def backward(ctx, g_total, _g_parts):
         if g_total is None:
             return (None,) * 8
-        kind, n, m, d_e, d_r, parts = ctx.meta
-        ent, rel, hi, lo, buf, *idx = ctx.saved_tensors
+        kind, n, m, d_e, d_r, dir_a, dir_b, n_a, has_dev = ctx.meta
+        ent, rel, hi, lo, buf, eidx, ridx, n_a_dev = ctx.saved_tensors
         gl = g_total.reshape(1).float().contiguous()  # read by the kernels from device memory
         gp = L.GradPlanes(buf, n, m)
-        tab_w = window(kind, parts[0][0], ent)
+        tab_w = window(kind, dir_a, ent)
         dq = L.score_dot_bwd_q_planes(gp, tab_w, gscale=gl)
         if tab_w.shape[1] == d_e:  # the GEMM covers every column: write, do not accumulate
             d_ent = torch.empty_like(ent)
             L.score_dot_bwd_t_planes(gp, hi, lo, d_ent, gscale=gl, accumulate=False)
         else:  # CP: the contraction sees one half of the entity rows
             d_ent = torch.zeros_like(ent)
-            L.score_dot_bwd_t_planes(gp, hi, lo, window(kind, parts[0][0], d_ent), gscale=gl, accumulate=False)
+            L.score_dot_bwd_t_planes(gp, hi, lo, window(kind, dir_a, d_ent), gscale=gl, accumulate=False)
         d_rel = torch.zeros_like(rel)
-        r0 = 0
-        for i, (dr, k) in enumerate(parts):
-            L.prep_query_bwd(kind, dr, ent, idx[2 * i], rel, idx[2 * i + 1], k, d_e, d_r, dq[r0:r0 + k], d_ent, d_rel)
-            r0 += k
+        L.prep_query_bwd2(kind, dir_a, dir_b, n_a, n_a_dev if has_dev else None, ent, eidx, rel, ridx, d_e, d_r, dq,
+                          d_ent, d_rel)
         return (None, d_ent if ctx.needs_input_grad[1] else None, d_rel if ctx.needs_input_grad[2] else None,
                 None, None, None, None, None)
 
@@ -251,8 +267,8 @@ def score_all_xent(kind: int, direction: int, precision: int, l_norm: float, ent
                   (kge/util/loss.py:209-213; kge/job/train.py:715-721, 744-751)."""
     L.require_device(ent, rel, tab)
     if tab is ent and tidx is None and eidx is not None and _planes_applicable(kind, precision, ent, direction):
-        total, _ = _ScoreXentPlanes.apply(kind, ent, rel, [(direction, L.idx64(eidx), L.idx64(ridx))], L.idx64(labels),
-                                          L.idx64(l_ptr), float(smoothing), float(scale))
+        total, _ = _ScoreXentPlanes.apply(kind, ent, rel, StackedQueries.of([(direction, eidx, ridx)]),
+                                          L.idx64(labels), L.idx64(l_ptr), float(smoothing), float(scale))
         return total
     return _ScoreXent.apply(kind, direction, precision, float(l_norm), ent, L.idx64(eidx), rel, L.idx64(ridx),
                             tab, L.idx64(tidx), L.idx64(labels), L.idx64(l_ptr), float(smoothing), float(scale))
@@ -351,8 +367,7 @@ def score_all_xent2(kind: int, precision: int, ent: torch.Tensor, rel: torch.Ten
         if lptr_a is not None:
             lptr_a, lptr_b = L.idx64(lptr_a), L.idx64(lptr_b)
             l_ptr = torch.cat((lptr_a[:-1], lptr_b + lptr_a[-1]))
-        return _ScoreXentPlanes.apply(kind, ent, rel, [(dir_a, L.idx64(eidx_a), L.idx64(ridx_a)),
-                                                       (dir_b, L.idx64(eidx_b), L.idx64(ridx_b))],
+        return _ScoreXentPlanes.apply(kind, ent, rel, StackedQueries.of([(dir_a, eidx_a, ridx_a), (dir_b, eidx_b, ridx_b)]),
                                       lab, l_ptr, float(smoothing), float(scale))
     return _ScoreXent2.apply(kind, precision, ent, rel, dir_a, L.idx64(eidx_a), L.idx64(ridx_a), L.idx64(lab_a),
                              L.idx64(lptr_a), dir_b, L.idx64(eidx_b), L.idx64(ridx_b), L.idx64(lab_b),
@@ -407,11 +422,16 @@ def score_parts(kind: int, precision: int, l_norm: float, ent: torch.Tensor, rel
             ldp = (qw + 31) // 32 * 32
             hi = torch.empty(n, ldp, device=ent.device, dtype=torch.bfloat16)
             lo = torch.empty_like(hi)
-            r0 = 0
-            for (dr, ei, ri), k in zip(parts, sizes):
-                L.prep_query_split(kind, dr, ent, ei, rel, ri, k, d_e, d_r,
-                                   out=(q[r0:r0 + k] if want_q else None, hi[r0:r0 + k], lo[r0:r0 + k]))
-                r0 += k
+            if len(parts) <= 2:  # one preparation launch for the stacked block
+                sq = StackedQueries.of(parts)
+                L.prep_query_split2(kind, sq.dir_a, sq.dir_b, sq.n_a, None, ent, sq.eidx, rel, sq.ridx, d_e, d_r,
+                                    out=(q if want_q else None, hi, lo))
+            else:
+                r0 = 0
+                for (dr, ei, ri), k in zip(parts, sizes):
+                    L.prep_query_split(kind, dr, ent, ei, rel, ri, k, d_e, d_r,
+                                       out=(q[r0:r0 + k] if want_q else None, hi[r0:r0 + k], lo[r0:r0 + k]))
+                    r0 += k
             _timed(L.score_dot_split, hi, lo, tab_w, tidx, qw, out=out)
         else:
             r0 = 0

@@ -134,7 +134,16 @@ class EntityRankingJob(EvaluationJob):
         # the stacked ranking launch (kge_rank_rows) reads both directions' lists from ONE column
         # array: the (?, p, o) pointers are shifted behind the (s, p, ?) columns
         self._stacked = [self._stack_csr(csr, dev), self._stack_csr(tcsr, dev) if tcsr is not None else None]
-        self._cols = self.triples.t().contiguous().to(dev)  # [3, N]: s / p / o as contiguous vectors
+        # per batch the index vectors [s_b | o_b] and [p_b | p_b], batch after batch: the stacked
+        # (s, p, ?) / (?, p, o) queries of a batch read ONE contiguous entity-index vector and one
+        # relation-index vector (no per-batch gather or concatenation)
+        se, sp = [], []
+        for b0 in range(0, len(self.triples), self.batch_size):
+            t = self.triples[b0:b0 + self.batch_size]
+            se += [t[:, 0], t[:, 2]]
+            sp += [t[:, 1], t[:, 1]]
+        self._stack_e = torch.cat(se).contiguous().to(dev) if se else torch.zeros(0, dtype=torch.int64, device=dev)
+        self._stack_p = torch.cat(sp).contiguous().to(dev) if sp else torch.zeros(0, dtype=torch.int64, device=dev)
 
     @staticmethod
     def _stack_csr(csr, dev):
@@ -212,7 +221,8 @@ class EntityRankingJob(EvaluationJob):
         for b0 in range(0, N, self.batch_size):
             b1 = min(N, b0 + self.batch_size)
             B = b1 - b0
-            s, p, o = self._cols[0, b0:b1], self._cols[1, b0:b1], self._cols[2, b0:b1]
+            s, o = self._stack_e[2 * b0:2 * b0 + B], self._stack_e[2 * b0 + B:2 * b0 + 2 * B]
+            p, p_po = self._stack_p[2 * b0:2 * b0 + B], self._stack_p[2 * b0 + B:2 * b0 + 2 * B]
             if sharded is not None:
                 # each rank counts over its own rows; one all_reduce of the int64 counts makes
                 # them global (the reference's chunk_size decomposition, entity_ranking.py:153-216)
@@ -245,7 +255,7 @@ class EntityRankingJob(EvaluationJob):
                 c1 = min(E, c0 + chunk)
                 subset = None if single else torch.arange(c0, c1, device=dev)
                 # [2B, C]: the (s, p, ?) rows on top of the (?, p, o) rows, one engine pass
-                scores, q = self.model.score_sp_po_rows(s, p, o, subset, want_q=self._refine)
+                scores, q = self.model.score_sp_po_rows(s, p, o, subset, want_q=self._refine, p_po=p_po)
                 refine = None
                 if q is not None:
                     if tmax is None:

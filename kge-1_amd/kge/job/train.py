@@ -269,7 +269,7 @@ class _GraphStep:
     def __init__(self, job: "TrainingJob"):
         self.job = job
         self.graph = None
-        self.static = None  # recorded [4, B] int64 device index block (s, p, o, s)
+        self.static = None  # recorded [5, B] int64 device index block (TrainingJob1vsAll.INDEX_BLOCK)
         self.pinned = []  # two pinned host staging buffers (+ their copy events) for the batch
         self.turn = 0
         self.loss = None  # recorded 0-dim loss
@@ -317,15 +317,15 @@ class _GraphStep:
 
     @staticmethod
     def _fill(block, triples):
-        """[B, 3] host triples -> the [4, B] index block s, p, o, s."""
-        block[:3].copy_(triples.t())
-        block[3].copy_(triples[:, 0])
+        """[B, 3] host triples -> the [5, B] index block (TrainingJob1vsAll.INDEX_BLOCK)."""
+        for r, c in enumerate(TrainingJob1vsAll.INDEX_BLOCK):
+            block[r].copy_(triples[:, c])
 
     def _record(self, batch_index, triples) -> bool:
         job = self.job
         opt = job.optimizer
         steps = {p: st["step"].clone() for p, st in opt.state.items() if "step" in st}
-        host = torch.empty(4, triples.shape[0], dtype=torch.int64)
+        host = torch.empty(len(TrainingJob1vsAll.INDEX_BLOCK), triples.shape[0], dtype=torch.int64)
         self._fill(host, triples.long())
         self.static = host.to(job.device)
         opt.zero_grad(set_to_none=True)
@@ -356,6 +356,9 @@ class _GraphStep:
 
 class TrainingJob1vsAll(TrainingJob):
     """Each (s, p, o) scores (s, p, ?) and (?, p, o) against all entities; CE loss."""
+
+    #: triple columns of the rows of a batch's device index block: s, o, s, p, p
+    INDEX_BLOCK = (S, O, S, P, P)
 
     def __init__(self, config, dataset, parent_job=None, model=None):
         super().__init__(config, dataset, parent_job, model=model)
@@ -396,21 +399,22 @@ class TrainingJob1vsAll(TrainingJob):
         if self._sharded is not None:
             return self._sharded.process_batch(batch)
         t = -time.time()
-        if "cols" in batch:  # [4, B] device index block s, p, o, s (the replayed step stages it this way)
+        if "cols" in batch:  # the [5, B] device index block (the replayed step stages it this way)
             cols = batch["cols"]
         else:
             triples = batch["triples"].to(self.device, non_blocking=True)
-            # s, p, o as contiguous index vectors plus a second copy of s right behind o: the
-            # labels of the two fused parts (o for sp_, s for _po) are then one contiguous vector
-            cols = triples.t()[[S, P, O, S]].contiguous()
+            cols = triples.t()[list(self.INDEX_BLOCK)].contiguous()
+        # Rows s, o, s, p, p: the stacked queries of the fused step read ONE contiguous vector each
+        # for their entity indexes (s | o), their labels (o | s) and their relation indexes (p | p)
+        s_, o_, s2_, p_, p2_ = cols[0], cols[1], cols[2], cols[3], cols[4]
         bs = cols.shape[1]
         t += time.time()
         fused = self.config.get("engine.fused_loss") and isinstance(self.loss, KLDivWithSoftmaxKgeLoss)
         fwd = -time.time()
         both = None
         if fused:
-            both = self.model.score_xent_parts(self.model.xent_part_sp(cols[S], cols[P], cols[O]),
-                                               self.model.xent_part_po(cols[P], cols[O], cols[3]), 1.0 / bs)
+            both = self.model.score_xent_parts(self.model.xent_part_sp(s_, p_, o_),
+                                               self.model.xent_part_po(p2_, o_, s2_), 1.0 / bs)
         if both is not None:  # sp_ and _po in one engine pass; one backward (same gradient sum)
             total, _ = both
             fwd += time.time()
@@ -420,20 +424,20 @@ class TrainingJob1vsAll(TrainingJob):
             total.backward(self._one)  # a persistent seed gradient: no fill kernel per step
             bwd += time.time()
             return TrainingJob._ProcessBatchResult(total.detach(), bs, t, fwd, bwd)
-        loss_sp = self.model.score_sp_xent(cols[S], cols[P], cols[O], 1.0 / bs) if fused else None
+        loss_sp = self.model.score_sp_xent(s_, p_, o_, 1.0 / bs) if fused else None
         if loss_sp is None:
-            scores_sp = self.model.score_sp(cols[S], cols[P])
-            loss_sp = self.loss(scores_sp, cols[O]) / bs
+            scores_sp = self.model.score_sp(s_, p_)
+            loss_sp = self.loss(scores_sp, o_) / bs
             del scores_sp
         fwd += time.time()
         bwd = -time.time()
         loss_sp.backward()
         bwd += time.time()
         fwd -= time.time()
-        loss_po = self.model.score_po_xent(cols[P], cols[O], cols[S], 1.0 / bs) if fused else None
+        loss_po = self.model.score_po_xent(p_, o_, s_, 1.0 / bs) if fused else None
         if loss_po is None:
-            scores_po = self.model.score_po(cols[P], cols[O])
-            loss_po = self.loss(scores_po, cols[S]) / bs
+            scores_po = self.model.score_po(p_, o_)
+            loss_po = self.loss(scores_po, s_) / bs
             del scores_po
         fwd += time.time()
         bwd -= time.time()

@@ -463,18 +463,22 @@ class KgeModel(KgeBase):
         p = self.get_p_embedder().embed_all() if p is None else self.get_p_embedder().embed(p)
         return self._scorer.score_emb(s, p, o, combine="s_o")
 
-    def _sp_po_parts(self, s: Tensor, p: Tensor, o: Tensor):
-        """The two query batches of score_sp_po as (direction, e_idx, p_idx)."""
-        return [("sp_", s, p), ("_po", o, p)]
+    def _sp_po_parts(self, s: Tensor, p: Tensor, o: Tensor, p_po: Tensor = None):
+        """The two query batches of score_sp_po as (direction, e_idx, p_idx); p_po: the relation
+        indexes of the (?, p, o) batch when the caller holds them as a vector of their own."""
+        return [("sp_", s, p), ("_po", o, p if p_po is None else p_po)]
 
-    def score_sp_po_rows(self, s: Tensor, p: Tensor, o: Tensor, entity_subset: Tensor = None, want_q: bool = False):
+    def score_sp_po_rows(self, s: Tensor, p: Tensor, o: Tensor, entity_subset: Tensor = None, want_q: bool = False,
+                         p_po: Tensor = None):
         """The scores of score_sp_po stacked by ROWS, without gradient: (S, Q) with S [2n, C],
         rows [0, n) = score_sp(s, p, subset), rows [n, 2n) = score_po(p, o, subset); Q the fp32
         query rows behind S (or None: not asked for / not available for this model).  One
-        engine pass where the model allows it; the evaluation job ranks from this block."""
+        engine pass where the model allows it; the evaluation job ranks from this block.  p_po
+        (equal to p) lets a caller whose index vectors (s | o) and (p | p_po) are contiguous in
+        memory avoid their concatenation."""
         tabs = self._lookup_tables()
         if tabs is not None:
-            return self._scorer.score_lookup_parts(tabs[0], tabs[1], self._sp_po_parts(s, p, o), entity_subset,
+            return self._scorer.score_lookup_parts(tabs[0], tabs[1], self._sp_po_parts(s, p, o, p_po), entity_subset,
                                                    want_q)
         with torch.no_grad():
             both = self.score_sp_po(s, p, o, entity_subset)

@@ -75,7 +75,7 @@ class ReciprocalRelationsModel(KgeModel):
     def score_so(self, s, o, p=None):
         raise Exception("The reciprocal relations model cannot score relations.")
 
-    def _sp_po_parts(self, s: Tensor, p: Tensor, o: Tensor):
+    def _sp_po_parts(self, s: Tensor, p: Tensor, o: Tensor, p_po: Tensor = None):
         return [("sp_", s, p), ("sp_", o, p + self.dataset.num_relations())]
 
     def score_sp_po(self, s: Tensor, p: Tensor, o: Tensor, entity_subset: Tensor = None) -> Tensor:

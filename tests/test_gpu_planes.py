@@ -130,3 +130,55 @@ def test_planes_entry_points_reject_bad_layouts(L):
     with pytest.raises(L.EngineError):
         L.softmax_planes(buf, 4, 90, torch.zeros(4, dtype=torch.int64, device="cuda"), None, 0.0, 1.0)
     assert not L.planes_ok(70000) and L.planes_ok(40943)
+
+
+@pytest.mark.parametrize("model", ["complex", "distmult", "rescal", "transe", "rotate", "cp", "simple"])
+@pytest.mark.parametrize("aligned", [True, False], ids=["vector", "scalar"])
+def test_two_part_prep_equals_the_per_direction_launches(L, model, aligned):
+    """kge_prep_query_split2 / kge_prep_query_bwd2 (rows [0, n_a) in one direction, the rest in
+    the other, split point on the host or in device memory) against the per-direction entry
+    points on the same rows: forward bit-identical (fp32 rows and both planes), backward equal up
+    to the order of the float atomics."""
+    kind = {"complex": L.COMPLEX, "distmult": L.DISTMULT, "rescal": L.RESCAL, "transe": L.TRANSE,
+            "rotate": L.ROTATE, "cp": L.CP, "simple": L.SIMPLE}[model]
+    d_e = (16 if model == "rescal" else 64) + (0 if aligned else 2)
+    d_r = K.relation_dim(model, d_e) if model != "cp" else d_e // 2
+    E, R, n, n_a = 50, 7, 37, 13
+    g = torch.Generator().manual_seed(d_e + kind)
+    ent = torch.randn(E, d_e, generator=g).cuda()
+    rel = torch.randn(R, d_r, generator=g).cuda()
+    eidx = torch.randint(0, E, (n,), generator=g).cuda()
+    ridx = torch.randint(0, R, (n,), generator=g).cuda()
+    qw = L.query_width(kind, d_e)
+    ldp = (qw + 31) // 32 * 32
+
+    def bufs():
+        return (torch.full((n, qw), 7.0, device="cuda"), torch.full((n, ldp), 3.0, device="cuda", dtype=torch.bfloat16),
+                torch.full((n, ldp), 3.0, device="cuda", dtype=torch.bfloat16))
+
+    q0, h0, l0 = bufs()
+    L.prep_query_split(kind, L.DIR_PO, ent, eidx[:n_a], rel, ridx[:n_a], n_a, d_e, d_r, out=(q0[:n_a], h0[:n_a], l0[:n_a]))
+    L.prep_query_split(kind, L.DIR_SP, ent, eidx[n_a:], rel, ridx[n_a:], n - n_a, d_e, d_r,
+                       out=(q0[n_a:], h0[n_a:], l0[n_a:]))
+    n_a_dev = torch.tensor([n_a], dtype=torch.int64, device="cuda")
+    for host_n_a, dev in ((n_a, None), (0, n_a_dev)):
+        q1, h1, l1 = bufs()
+        L.prep_query_split2(kind, L.DIR_PO, L.DIR_SP, host_n_a, dev, ent, eidx, rel, ridx, d_e, d_r, out=(q1, h1, l1))
+        torch.cuda.synchronize()
+        assert torch.equal(q0, q1) and torch.equal(h0, h1) and torch.equal(l0, l1)
+    dq = torch.randn(n, qw, generator=g).cuda()
+    de0, dr0 = torch.zeros_like(ent), torch.zeros_like(rel)
+    L.prep_query_bwd(kind, L.DIR_PO, ent, eidx[:n_a], rel, ridx[:n_a], n_a, d_e, d_r, dq[:n_a], de0, dr0)
+    L.prep_query_bwd(kind, L.DIR_SP, ent, eidx[n_a:], rel, ridx[n_a:], n - n_a, d_e, d_r, dq[n_a:], de0, dr0)
+    for host_n_a, dev in ((n_a, None), (0, n_a_dev)):
+        de1, dr1 = torch.zeros_like(ent), torch.zeros_like(rel)
+        L.prep_query_bwd2(kind, L.DIR_PO, L.DIR_SP, host_n_a, dev, ent, eidx, rel, ridx, d_e, d_r, dq, de1, dr1)
+        torch.cuda.synchronize()
+        assert float((de0 - de1).abs().max()) <= 1e-5 * float(de0.abs().max())
+        assert float((dr0 - dr1).abs().max()) <= 1e-5 * float(dr0.abs().max())
+    # the reductions of a two-part loss with the split point in device memory
+    loss = torch.randn(n, generator=g).cuda()
+    t0, p0 = L.loss_sums(loss, n_a, 0.5)
+    t1, p1 = L.loss_sums(loss, 0, 0.5, n_a_dev)
+    assert torch.equal(t0, t1) and torch.equal(p0, p1)
+    assert float(p0[0]) == pytest.approx(0.5 * float(loss[:n_a].double().sum()), rel=1e-5, abs=1e-6)
