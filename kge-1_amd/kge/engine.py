@@ -374,6 +374,22 @@ def score_all_xent2(kind: int, precision: int, ent: torch.Tensor, rel: torch.Ten
                              L.idx64(lptr_b), float(smoothing), float(scale))
 
 
+def score_all_xent_stacked(kind: int, precision: int, ent: torch.Tensor, rel: torch.Tensor, dir_a: int, dir_b: int,
+                           eidx: torch.Tensor, ridx: torch.Tensor, n_a_dev: torch.Tensor, labels: torch.Tensor,
+                           l_ptr: Optional[torch.Tensor], scale: float, smoothing: float = 0.0):
+    """score_all_xent2 for query rows that are already stacked (rows [0, n_a) direction dir_a, the
+    rest dir_b) with n_a an int64 device scalar -- nothing here depends on its value on the host,
+    so the launches can be recorded once and replayed for batches whose split differs.  Served by
+    the plane-fed path only: None when it does not apply to this scorer / precision / layout."""
+    if kind not in BILINEAR or (kind == L.CP and dir_a != dir_b):
+        return None
+    L.require_device(ent, rel, eidx, ridx, n_a_dev)
+    if not _planes_applicable(kind, precision, ent, dir_a):
+        return None
+    sq = StackedQueries(dir_a, dir_b, L.idx64(eidx), L.idx64(ridx), 0, L.idx64(n_a_dev))
+    return _ScoreXentPlanes.apply(kind, ent, rel, sq, L.idx64(labels), L.idx64(l_ptr), float(smoothing), float(scale))
+
+
 def score_all(kind: int, direction: int, precision: int, l_norm: float, ent: torch.Tensor,
               eidx: Optional[torch.Tensor], rel: torch.Tensor, ridx: Optional[torch.Tensor],
               tab: torch.Tensor, tidx: Optional[torch.Tensor] = None) -> torch.Tensor:

@@ -249,12 +249,11 @@ class TrainingJob(Job):
 
 
 class _GraphStep:
-    """A 1vsAll training step recorded once as a HIP graph and replayed per batch
-    (engine.graph_step).
+    """A training step recorded once as a HIP graph and replayed per batch (engine.graph_step).
 
-    The step's device work is fixed for a full batch: the index columns, one fused
-    sp+po scoring / softmax-CE pass, its backward GEMMs and prep backward, the fused
-    Adagrad kernels -- ~30 launches plus autograd bookkeeping on the host, which at C2 costs
+    The step's device work is fixed for a full batch: one fused scoring / softmax pass over
+    the stacked (s, p, ?) and (?, p, o) queries, its backward GEMMs and prep backward, the
+    fused Adagrad kernels -- a dozen launches plus autograd bookkeeping on the host, which costs
     as long as the device work itself.  Two full batches run eagerly first (kernel
     attributes, optimizer state, allocator warm-up); the third is recorded (recording runs
     nothing) and replayed, and every later full batch is copied into the recorded index
@@ -262,14 +261,19 @@ class _GraphStep:
     A partial last batch, or any step the recording cannot take, runs eagerly.  Like any
     recorded graph it assumes the parameters and optimizer state stay where they are
     (in-place updates such as load_state_dict are fine; re-creating the tensors is not:
-    call disable() or build a new job)."""
+    call disable() or build a new job).
+
+    Subclasses say what a batch's index block is: _block(batch) -> a flat int64 host tensor
+    (None: this batch runs eagerly) that is uploaded into the first len(block) elements of the
+    recorded device buffer of _capacity() elements, and _recorded_batch() -> the batch dict (views
+    of that buffer) the job's process_batch is recorded with."""
 
     WARMUP = 2
 
     def __init__(self, job: "TrainingJob"):
         self.job = job
         self.graph = None
-        self.static = None  # recorded [5, B] int64 device index block (TrainingJob1vsAll.INDEX_BLOCK)
+        self.static = None  # recorded flat int64 device index buffer
         self.pinned = []  # two pinned host staging buffers (+ their copy events) for the batch
         self.turn = 0
         self.loss = None  # recorded 0-dim loss
@@ -282,17 +286,34 @@ class _GraphStep:
         self.disabled = True
         self.graph = None
 
+    # ---- what a batch looks like (1vsAll: the [5, B] index block of TrainingJob1vsAll.INDEX_BLOCK)
+    def _capacity(self) -> int:
+        return len(TrainingJob1vsAll.INDEX_BLOCK) * self.job.batch_size
+
+    def _block(self, batch):
+        triples = batch["triples"]
+        if triples.dim() != 2 or triples.shape[0] != self.job.batch_size:
+            return None
+        return triples.long()[:, list(TrainingJob1vsAll.INDEX_BLOCK)].t().reshape(-1)
+
+    def _recorded_batch(self):
+        return {"cols": self.static.view(len(TrainingJob1vsAll.INDEX_BLOCK), self.job.batch_size)}
+
+    # ---- the step
     def run(self, batch_index, batch):
         job = self.job
-        triples = batch["triples"]
-        if self.disabled or triples.dim() != 2 or triples.shape[0] != job.batch_size:
+        if self.disabled:
             return None
+        if self.graph is None and self.warm < self.WARMUP:
+            self.warm += 1
+            return None  # the caller runs this batch eagerly
         t = -time.time()
+        block = self._block(batch)
+        if block is None or block.numel() > self._capacity():
+            return None
+        n = block.numel()
         if self.graph is None:
-            if self.warm < self.WARMUP:
-                self.warm += 1
-                return None  # the caller runs this batch eagerly
-            if not self._record(batch_index, triples):
+            if not self._record(batch_index, block):
                 return None
             # recording counted this step in the optimizer state already
         else:
@@ -300,39 +321,37 @@ class _GraphStep:
             # stage through pinned memory (two buffers: the read of batch b - 1 may still be
             # pending) and upload it with a kernel in stream order
             if not self.pinned:
-                self.pinned = [[torch.empty(self.static.shape, dtype=torch.int64, pin_memory=True), None]
+                self.pinned = [[torch.empty(self._capacity(), dtype=torch.int64, pin_memory=True), None]
                                for _ in range(2)]
             slot = self.pinned[self.turn]
             self.turn ^= 1
             if slot[1] is not None:
                 slot[1].synchronize()
-            self._fill(slot[0], triples)
-            _lib.stage_i64(slot[0], self.static)  # a kernel, not a DMA copy, on this stream
+            slot[0][:n].copy_(block)
+            _lib.stage_i64(slot[0][:n], self.static[:n])  # a kernel, not a DMA copy, on this stream
             slot[1] = torch.cuda.Event()
             slot[1].record()
             job.optimizer.advance_steps(self.stepped)
         self.graph.replay()
         t += time.time()
-        return TrainingJob._ProcessBatchResult(self.loss, triples.shape[0], 0.0, t, 0.0)
+        return TrainingJob._ProcessBatchResult(self._loss_of(block), job.batch_size, 0.0, t, 0.0)
 
-    @staticmethod
-    def _fill(block, triples):
-        """[B, 3] host triples -> the [5, B] index block (TrainingJob1vsAll.INDEX_BLOCK)."""
-        for r, c in enumerate(TrainingJob1vsAll.INDEX_BLOCK):
-            block[r].copy_(triples[:, c])
+    def _loss_of(self, block):
+        """The loss the step reports, from what the recording returned."""
+        return self.loss
 
-    def _record(self, batch_index, triples) -> bool:
+    def _record(self, batch_index, block) -> bool:
         job = self.job
         opt = job.optimizer
         steps = {p: st["step"].clone() for p, st in opt.state.items() if "step" in st}
-        host = torch.empty(len(TrainingJob1vsAll.INDEX_BLOCK), triples.shape[0], dtype=torch.int64)
-        self._fill(host, triples.long())
+        host = torch.zeros(self._capacity(), dtype=torch.int64)
+        host[:block.numel()] = block
         self.static = host.to(job.device)
         opt.zero_grad(set_to_none=True)
         g = torch.cuda.CUDAGraph()
         try:
             with torch.cuda.graph(g):
-                res = job.process_batch(batch_index, {"cols": self.static})
+                res = job.process_batch(batch_index, self._recorded_batch())
                 opt.step()
         except Exception as e:  # not recordable: this and every later batch run eagerly
             for p, s in steps.items():
@@ -352,6 +371,46 @@ class _GraphStep:
         self.loss = res.loss
         self.stepped = [p for grp in opt.param_groups for p in grp["params"] if p.grad is not None]
         return True
+
+
+class _KvsAllGraphStep(_GraphStep):
+    """The KvsAll step as a recorded graph.  A batch is B query rows -- the (s, p, ?) queries
+    stacked on the (?, p, o) queries, their split point differing from batch to batch -- with
+    their positives as a CSR of varying length, so the recorded buffer is
+        [entity index (B) | relation index (B) | label pointer (B + 1) | split point (1) | label columns (cap)]
+    and the recorded kernels read the split point from it (kge_prep_query_split2, kge_loss_sums).
+    A batch whose positives exceed the capacity (or a partial batch) runs eagerly."""
+
+    def __init__(self, job):
+        super().__init__(job)
+        B = job.batch_size
+        labels = sum(len(ix.values) for ix in job.query_indexes)
+        mean = labels / max(1, job.num_examples)
+        cap = 8192
+        while cap < 2 * mean * B:
+            cap *= 2
+        self.cap = cap
+
+    def _capacity(self) -> int:
+        return 3 * self.job.batch_size + 2 + self.cap
+
+    def _block(self, batch):
+        ex = batch["examples"]
+        if len(ex) != self.job.batch_size:
+            return None
+        return self.job._stacked_block(ex.numpy())
+
+    def _recorded_batch(self):
+        B = self.job.batch_size
+        st = self.static
+        return {"stacked": (st[:B], st[B:2 * B], st[2 * B:3 * B + 1], st[3 * B + 1:3 * B + 2], st[3 * B + 2:])}
+
+    def _loss_of(self, block):
+        # the recording returns both query types' losses; the reference reports the last query
+        # type that has examples in the batch (Q10), which the host knows from the split point
+        B = self.job.batch_size
+        two = len(self.job._part_spec) == 2 and int(block[3 * B + 1]) < B
+        return self.loss[1 if two else 0]
 
 
 class TrainingJob1vsAll(TrainingJob):
@@ -528,6 +587,7 @@ class TrainingJobKvsAll(TrainingJob):
         elif 0 < self.label_smoothing <= 1.0 / dataset.num_entities():
             self.label_smoothing = 1.0 / dataset.num_entities()
         self.type_str = "KvsAll"
+        self._graph_step = None
 
     def _prepare(self):
         super()._prepare()
@@ -542,6 +602,80 @@ class TrainingJobKvsAll(TrainingJob):
             self.query_indexes.append(idx)
             self.num_examples += len(idx)
             self.query_last_example.append(self.num_examples)
+        # How the model scores each query type, as (engine direction, key column of the entity
+        # index, key column of the relation index, offset added to the relation index): asked of
+        # the model itself (a reciprocal-relations model answers (?, p, o) as (o, p + R, ?)).
+        self._part_spec = []
+        for qt in self.query_types:
+            k0, k1 = torch.tensor([0]), torch.tensor([1])
+            if qt == "sp_":  # keys (s, p)
+                d, e, r, _, _ = self.model.xent_part_sp(k0, k1, None)
+            else:  # keys (p, o)
+                d, e, r, _, _ = self.model.xent_part_po(k0, k1, None)
+            e_col = 0 if int(e[0]) == 0 else 1
+            self._part_spec.append((d, e_col, 1 - e_col, int(r[0]) - (1 - e_col)))
+        from ..sharded import sharding_enabled
+
+        opt = self.optimizer
+        if (self.config.get("engine.graph_step") and self.config.get("engine.fused_loss")
+                and isinstance(self.loss, KLDivWithSoftmaxKgeLoss)
+                and 1 <= len(self.query_types) <= 2
+                and torch.device(self.device).type == "cuda"
+                and hasattr(opt, "graph_safe") and opt.graph_safe()
+                and self.kge_lr_scheduler._lr_scheduler is None
+                and not self.pre_batch_hooks
+                and not sharding_enabled(self.config)
+                and self.model._lookup_tables() is not None):
+            self._graph_step = _KvsAllGraphStep(self)
+
+    def _stacked_block(self, ex: np.ndarray):
+        """The batch as ONE flat int64 block for the recorded step (_KvsAllGraphStep): stacked
+        entity indexes [B], relation indexes [B], label pointer [B + 1], the number of rows of
+        the first query type [1], label columns [nnz] -- the first query type's rows first."""
+        e_parts, r_parts, len_parts, col_parts = [], [], [], []
+        start = 0
+        n_first = 0
+        for qi, (_, e_col, r_col, r_off) in enumerate(self._part_spec):
+            end = self.query_last_example[qi]
+            sel = ex[(ex >= start) & (ex < end)] - start
+            start = end
+            ix = self.query_indexes[qi]
+            keys = ix.keys[sel]
+            lo = ix.offsets[sel]
+            lens = ix.offsets[sel + 1] - lo
+            tot = int(lens.sum())
+            ends = np.cumsum(lens)
+            pos = np.arange(tot, dtype=np.int64) - np.repeat(ends - lens, lens) + np.repeat(lo, lens)
+            e_parts.append(keys[:, e_col])
+            r_parts.append(keys[:, r_col] + r_off)
+            len_parts.append(lens)
+            col_parts.append(ix.values[pos])
+            if qi == 0:
+                n_first = len(sel)
+        n = len(ex)
+        if len(self._part_spec) == 1:
+            n_first = n
+        l_ptr = np.zeros(n + 1, dtype=np.int64)
+        np.cumsum(np.concatenate(len_parts), out=l_ptr[1:])
+        block = np.concatenate(e_parts + r_parts + [l_ptr, np.asarray([n_first], dtype=np.int64)] + col_parts)
+        return torch.from_numpy(block.astype(np.int64, copy=False))
+
+    def _process_stacked(self, stacked, bs):
+        """The recorded step's body: both query types from the device block of _stacked_block."""
+        eidx, ridx, l_ptr, n_first, l_col = stacked
+        dirs = [spec[0] for spec in self._part_spec]
+        fwd = -time.time()
+        losses = self.model.score_xent_stacked(dirs[0], dirs[-1], eidx, ridx, n_first, l_col, l_ptr, 1.0 / bs,
+                                               self.label_smoothing)
+        fwd += time.time()
+        if losses is None:
+            raise RuntimeError("the scorer cannot run both query types in one engine pass")
+        total, per_type = losses
+        bwd = -time.time()
+        total.backward()
+        bwd += time.time()
+        # both query types' losses: the caller picks the one the reference would report (Q10)
+        return TrainingJob._ProcessBatchResult(per_type, bs, 0.0, fwd, bwd)
 
     def _collate(self, example_ids):
         return {"examples": example_ids}
@@ -567,6 +701,8 @@ class TrainingJobKvsAll(TrainingJob):
         return dev[:2 * n].view(n, 2), dev[2 * n:3 * n + 1], dev[3 * n + 1:]
 
     def _process_batch(self, batch_index, batch) -> TrainingJob._ProcessBatchResult:
+        if "stacked" in batch:
+            return self._process_stacked(batch["stacked"], self.batch_size)
         t = -time.time()
         ex = batch["examples"].numpy()
         bs = len(ex)

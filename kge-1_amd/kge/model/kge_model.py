@@ -185,6 +185,20 @@ class RelationalScorer(KgeBase):
         return engine.score_all_xent2(self.engine_kind, self.precision(), ent, rel, conv(part_a), conv(part_b),
                                       scale, smoothing)
 
+    def score_lookup_xent_stacked(self, ent: Tensor, rel: Tensor, dir_a: str, dir_b: str, e_idx: Tensor,
+                                  p_idx: Tensor, n_a_dev: Tensor, labels: Tensor, l_ptr: Optional[Tensor],
+                                  scale: float, smoothing: float = 0.0):
+        """score_lookup_xent2 on pre-stacked query rows with the split point in device memory
+        (engine.score_all_xent_stacked); None when this scorer cannot fuse them."""
+        from .. import engine, _lib
+
+        if self.engine_kind is None:
+            return None
+        da = _lib.DIR_SP if dir_a == "sp_" else _lib.DIR_PO
+        db = _lib.DIR_SP if dir_b == "sp_" else _lib.DIR_PO
+        return engine.score_all_xent_stacked(self.engine_kind, self.precision(), ent, rel, da, db, e_idx, p_idx,
+                                             n_a_dev, labels, l_ptr, scale, smoothing)
+
     def score_lookup_cand(self, ent: Tensor, rel: Tensor, e_idx: Tensor, p_idx: Tensor, direction: str,
                           cand: Tensor) -> Tensor:
         """[n, k]: query (ent[e_idx[i]], rel[p_idx[i]]) in direction "sp_" / "_po" against its
@@ -416,6 +430,19 @@ class KgeModel(KgeBase):
         if tabs is None:
             return None
         return self._scorer.score_lookup_xent2(tabs[0], tabs[1], part_a, part_b, scale, smoothing)
+
+    def score_xent_stacked(self, dir_a: str, dir_b: str, e_idx: Tensor, p_idx: Tensor, n_a_dev: Tensor, labels: Tensor,
+                           l_ptr: Optional[Tensor], scale: float, smoothing: float = 0.0):
+        """score_xent_parts for two query batches that are ALREADY stacked by rows (e_idx / p_idx
+        index every row; rows [0, n_a) are direction dir_a ("sp_" / "_po") queries, the rest dir_b
+        queries) with the split point n_a an int64 DEVICE scalar: a step recorded as a HIP graph
+        serves batches whose split differs.  Labels as in score_xent_parts, stacked likewise.
+        (total, [loss_a, loss_b] detached), or None when not fusable."""
+        tabs = self._lookup_tables()
+        if tabs is None:
+            return None
+        return self._scorer.score_lookup_xent_stacked(tabs[0], tabs[1], dir_a, dir_b, e_idx, p_idx, n_a_dev, labels,
+                                                      l_ptr, scale, smoothing)
 
     def score_sp_po_xent(self, s: Tensor, p: Tensor, o: Tensor, scale: float) -> Optional[Tensor]:
         """score_sp_xent(s, p, o, scale) + score_po_xent(p, o, s, scale) in one engine pass (the two

@@ -150,3 +150,88 @@ def test_graph_step_run_epoch_matches_eager():
             assert job._graph_step.graph is not None
     np.testing.assert_allclose(traces[True], traces[False], rtol=1e-5)
     assert traces[True][1] < traces[True][0]
+
+
+def _kvsall_job(graph, model, E=600, R=7, dim=64, seed=0, batch=64):
+    from kge import Config, Dataset
+    from kge.job import TrainingJob
+
+    c = Config()
+    c.set("model", model)
+    c._import(model)
+    if model == "reciprocal_relations_model":
+        c.set("reciprocal_relations_model.base_model.type", "distmult")
+        c._import("distmult")
+    c.set("job.device", "cuda")
+    c.set("lookup_embedder.dim", dim)
+    c.set("lookup_embedder.initialize_args", {"mean": 0.0, "std": 0.1})
+    c.set("train.type", "KvsAll")
+    c.set("KvsAll.label_smoothing", 0.1)
+    c.set("train.batch_size", batch)
+    c.set("engine.graph_step", graph)
+    c.set("train.optimizer", "Adagrad")
+    c.set("train.optimizer_args", {"lr": 0.2})
+    c.set("dataset.num_entities", E)
+    c.set("dataset.num_relations", R)
+    c.set("verbose", False)
+    ds = Dataset(c, None)
+    g = torch.Generator().manual_seed(seed)
+    # few distinct (s, p) / (p, o) keys: label lists of very different lengths
+    tr = torch.stack([torch.randint(0, 40, (900,), generator=g), torch.randint(0, R, (900,), generator=g),
+                      torch.randint(0, E, (900,), generator=g)], 1).int()
+    ds._triples = {"train": tr}
+    torch.manual_seed(seed)
+    job = TrainingJob.create(c, ds)
+    job._prepare()
+    return job
+
+
+@pytest.mark.parametrize("model", ["distmult", "complex", "reciprocal_relations_model"])
+def test_kvsall_graph_step_matches_eager(model):
+    """The KvsAll step recorded as a HIP graph -- stacked (s, p, ?) / (?, p, o) query rows whose
+    split point and label CSR differ from batch to batch and are read from the recorded device
+    block -- against the eager step on the same batches: losses per batch (the last query type's,
+    as the reference reports), tables and Adagrad state; batches with only one query type, a
+    partial batch and the batches after it included."""
+    runs = {}
+    for graph in (False, True):
+        job = _kvsall_job(graph, model)
+        n = job.num_examples
+        perm = torch.randperm(n, generator=torch.Generator().manual_seed(3))
+        n_first = job.query_last_example[0]
+        batches = [perm[b:b + 64] for b in range(0, 64 * 6, 64)]
+        batches.append(torch.arange(0, 64))                    # only the first query type
+        batches.append(torch.arange(n - 64, n))                # only the second
+        batches.append(perm[64 * 6:64 * 6 + 30])               # partial: eager
+        batches.append(perm[64 * 7:64 * 8])                    # replayed again afterwards
+        assert n_first > 64 and n - n_first > 64
+        losses = []
+        for b, ids in enumerate(batches):
+            res, _, _ = job.train_step(b, job._collate(ids))
+            losses.append(float(res.loss))
+        if graph:
+            assert job._graph_step is not None and job._graph_step.graph is not None, (
+                f"graph was not recorded: {job._graph_step.error}")
+        else:
+            assert job._graph_step is None
+        st = job.optimizer.state
+        ent = job.model.get_s_embedder()._embeddings.weight
+        rel = job.model.get_p_embedder()._embeddings.weight
+        runs[graph] = (np.array(losses), ent.detach().cpu().numpy(), rel.detach().cpu().numpy(),
+                       st[ent]["sum"].cpu().numpy(), int(st[ent]["step"]), int(st[rel]["step"]))
+    e, g = runs[False], runs[True]
+    np.testing.assert_allclose(g[0], e[0], rtol=2e-5, atol=1e-7)
+    for a, b in ((g[1], e[1]), (g[2], e[2])):
+        off = np.abs(a - b) > 1e-5
+        assert off.mean() < 0.05 and np.abs(a - b).max() < 2e-2, (off.mean(), np.abs(a - b).max())
+    np.testing.assert_allclose(g[3], e[3], rtol=1e-2, atol=1e-3 * np.abs(e[3]).max())
+    assert g[4] == e[4] == len(batches) and g[5] == e[5] == len(batches)
+
+
+def test_kvsall_graph_step_falls_back_when_labels_exceed_capacity():
+    """A batch whose positives do not fit the recorded label buffer runs eagerly (same result)."""
+    job = _kvsall_job(True, "distmult")
+    job._graph_step.cap = 16  # far below any batch's label count
+    for b in range(4):
+        job.train_step(b, job._collate(torch.arange(b * 64, b * 64 + 64)))
+    assert job._graph_step.graph is None and not job._graph_step.disabled
