@@ -24,6 +24,8 @@ c.set("train.optimizer", "Adagrad")
 c.set("train.optimizer_args", {"lr": 0.2})
 c.set("train.batch_size", 1024 if train_type == "1vsAll" else 512)
 c.set("verbose", False)
+if os.environ.get("KGE_NO_GRAPH") == "1":  # per-kernel times of the eager step, for comparison
+    c.set("engine.graph_step", False)
 ds = Dataset.synthetic(c, "fb15k-237" if train_type == "1vsAll" else "wn18rr", seed=0)
 job = TrainingJob.create(c, ds)
 job._prepare()
