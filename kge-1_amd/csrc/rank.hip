@@ -228,24 +228,33 @@ __global__ void __launch_bounds__(NT) rank_rows_kernel(const RankRowsArgs a) {
     pushed = 0;
     if (!any) return done;
     const unsigned total = ev_total;  // stable: nobody pushes before the barrier below
-    constexpr int U = 4;  // entries a wave rescores at a time: wave w takes w, w + 4, ...
-    for (unsigned x0 = done + wave; x0 < total; x0 += U * (NT / 64)) {
+    // wave w takes entries w, w + 4, ...: four at a time (four row loads in flight) while it has
+    // four left, then one by one
+    constexpr int U = 4, NWV = NT / 64;
+    unsigned x0 = done + wave;
+    for (; x0 + (U - 1) * NWV < total; x0 += U * NWV) {
       const float* rows_[U];
       float v[U];
 #pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const unsigned x = x0 + u * (NT / 64);
-        rows_[u] = a.t + (int64_t)ev[(x < total ? x : x0) % EV_CAP] * a.ldt;  // idle slots redo the first
-      }
+      for (int u = 0; u < U; ++u) rows_[u] = a.t + (int64_t)ev[(x0 + u * NWV) % EV_CAP] * a.ldt;
       exact_dots_wave<U>(qrow, rows_, a.d, v);
       if (lane == 0) {
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-          if (x0 + u * (NT / 64) >= total) continue;
           const float v_ = clean(v[u]);
           gt += sign * (v_ > t);
           eq += sign * (v_ == t);
         }
+      }
+    }
+    for (; x0 < total; x0 += NWV) {
+      const float* rows_[1] = {a.t + (int64_t)ev[x0 % EV_CAP] * a.ldt};
+      float v[1];
+      exact_dots_wave<1>(qrow, rows_, a.d, v);
+      if (lane == 0) {
+        const float v_ = clean(v[0]);
+        gt += sign * (v_ > t);
+        eq += sign * (v_ == t);
       }
     }
     __syncthreads();  // ring entries consumed before the next step overwrites them
