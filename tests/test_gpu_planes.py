@@ -81,7 +81,7 @@ def _planes(L, n, m, seed):
 
 
 @pytest.mark.parametrize("n,m,d", [(100, 501, 64), (300, 3001, 128), (2048, 14541, 512), (512, 40943, 512),
-                                   (1, 40, 8)])
+                                   (1, 40, 8), (64, 700, 1024), (50, 333, 104)])
 def test_bwd_q_planes_vs_float64(L, n, m, d):
     gp, g64 = _planes(L, n, m, n + m + d)
     gen = torch.Generator(device="cuda").manual_seed(d)
@@ -101,7 +101,7 @@ def test_bwd_q_planes_vs_float64(L, n, m, d):
 
 
 @pytest.mark.parametrize("n,m,d", [(100, 501, 64), (300, 3001, 128), (2048, 14541, 512), (512, 40943, 512),
-                                   (1, 40, 8)])
+                                   (1, 40, 8), (64, 700, 1024), (50, 333, 104)])
 def test_bwd_t_planes_vs_float64(L, n, m, d):
     gp, g64 = _planes(L, n, m, 3 * n + m + d)
     gen = torch.Generator(device="cuda").manual_seed(d + 1)
