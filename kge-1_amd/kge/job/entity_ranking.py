@@ -19,7 +19,7 @@ per-shard reduction of the row-sharded multi-GPU path (kge.sharded).
 from __future__ import annotations
 
 import time
-from typing import Dict, List, Optional
+from typing import Dict, List
 
 import numpy as np
 import torch

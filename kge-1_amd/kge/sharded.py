@@ -23,7 +23,6 @@ backend on CPU (tests/test_sharded_gloo.py); the default ops are the HIP engine.
 from __future__ import annotations
 
 import math
-from typing import Optional
 
 import torch
 import torch.distributed as dist
