@@ -85,8 +85,10 @@ int kge_prep_query(int model, int dir, const float* ent, int64_t ld_ent,
 
 /* kge_prep_query that can also (or only) emit the bf16 hi / lo planes of Q consumed by
  * kge_score_dot_split: q may be NULL; planes are [n][ldp], ldp >= d_e and a multiple of 8
- * (use round_up(d_e, 32)); columns d_e .. ldp-1 are zeroed.  Saves the separate
- * kge_split_rows pass on the score_sp / score_po path. */
+ * (use round_up(d_e, 32)); columns d_e .. min(ldp, round_up(d_e, 32)) - 1 -- the K padding the
+ * contraction reads -- are zeroed (so hi and lo may share rows of stride ldp = 2 round_up(d_e, 32):
+ * [hi | lo], one buffer to exchange between GPUs).  Saves the separate kge_split_rows pass on the
+ * score_sp / score_po path. */
 int kge_prep_query_split(int model, int dir, const float* ent, int64_t ld_ent,
                          const int64_t* eidx, const float* rel, int64_t ld_rel,
                          const int64_t* ridx, int64_t n, int d_e, int d_r, float* q,

@@ -21,13 +21,15 @@ __device__ __forceinline__ Rows fetch_rows(const float* ent, int64_t ld_ent, con
 }
 
 // Query-row sink: fp32 rows and/or bf16 hi / lo planes (the bf16x3 contraction's input),
-// planes zero-padded from d_e to ldp.
+// planes zero-padded from the query width up to padw columns (the K padding the contraction
+// reads: the width rounded up to 32, or the whole row when it is shorter than that).
 struct QOut {
   float* q;
   int64_t ldq;
   __bf16* hi;
   __bf16* lo;
   int64_t ldp;
+  int padw;
   __device__ __forceinline__ void put(int64_t i, int k, float v) const {
     if (q) q[i * ldq + k] = v;
     if (hi) {
@@ -39,7 +41,7 @@ struct QOut {
   }
   __device__ __forceinline__ void pad(int64_t i, int d) const {
     if (!hi) return;
-    for (int k = d + threadIdx.x; k < ldp; k += blockDim.x) {
+    for (int k = d + threadIdx.x; k < padw; k += blockDim.x) {
       hi[i * ldp + k] = (__bf16)0.f;
       lo[i * ldp + k] = (__bf16)0.f;
     }
@@ -131,7 +133,7 @@ __device__ __forceinline__ void prep_row_vec(const Rows rw, int64_t i, int lane,
   };
   const int qw = MODEL == KGE_CP ? d_e / 2 : d_e;
   if (out.hi)
-    for (int k = qw + lane * 4; k < out.ldp; k += 256) {  // zero padding to ldp (ldp % 8 == 0)
+    for (int k = qw + lane * 4; k < out.padw; k += 256) {  // zero K padding (padw % 4 == 0)
       *reinterpret_cast<bf16x4*>(out.hi + i * out.ldp + k) = bf16x4{};
       *reinterpret_cast<bf16x4*>(out.lo + i * out.ldp + k) = bf16x4{};
     }
@@ -518,7 +520,8 @@ extern "C" int kge_prep_query_split2(int model, int dir_a, int dir_b, int64_t n_
   KGE_REQUIRE((dir_a == KGE_DIR_SP || dir_a == KGE_DIR_PO) && (dir_b == KGE_DIR_SP || dir_b == KGE_DIR_PO));
   KGE_REQUIRE(n_a >= 0);
   if (n == 0) return 0;
-  QOut out{q, ldq, (__bf16*)q_hi, (__bf16*)q_lo, ldp};
+  const int qw = query_width(model, d_e);
+  QOut out{q, ldq, (__bf16*)q_hi, (__bf16*)q_lo, ldp, (int)std::min<int64_t>(ldp, (qw + 31) / 32 * 32)};
   return launch_prep(model, ent, ld_ent, eidx, rel, ld_rel, ridx, n, d_e, out, Dirs{dir_a, dir_b, n_a, n_a_dev},
                      as_stream(stream));
 }

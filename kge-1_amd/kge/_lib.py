@@ -196,12 +196,17 @@ def prep_query(model, direction, ent, eidx, rel, ridx, n, d_e, d_r, out=None):
     return q
 
 
-def prep_query_split(model, direction, ent, eidx, rel, ridx, n, d_e, d_r, want_fp32=True, out=None):
+def prep_query_split(model, direction, ent, eidx, rel, ridx, n, d_e, d_r, want_fp32=True, out=None, eidx_base=0):
     """Query rows as fp32 (optional) plus bf16 hi / lo planes [n, round32(width)] in one pass
-    (into out = (q or None, hi, lo) when given)."""
+    (into out = (q or None, hi, lo) when given).  eidx_base: the id of ent's first row -- eidx
+    then holds GLOBAL row ids of a table of which ent is the slice starting at that row (a
+    rank's shard), all of them inside the slice; saves the caller a subtraction kernel."""
     require_device(ent, rel)
     eidx, ridx = idx64(eidx), idx64(ridx)
-    check_index(eidx, ent.shape[0], "entity index")
+    if eidx_base and CHECK_INDEX and eidx is not None and not torch.cuda.is_current_stream_capturing():
+        check_index(eidx - eidx_base, ent.shape[0], "entity index")
+    elif not eidx_base:
+        check_index(eidx, ent.shape[0], "entity index")
     check_index(ridx, rel.shape[0], "relation index")
     qw = query_width(model, d_e)
     if out is not None:
@@ -212,10 +217,48 @@ def prep_query_split(model, direction, ent, eidx, rel, ridx, n, d_e, d_r, want_f
         q = torch.empty(n, qw, device=ent.device, dtype=torch.float32) if want_fp32 else None
         hi = torch.empty(n, ldp, device=ent.device, dtype=torch.bfloat16)
         lo = torch.empty_like(hi)
-    _check(lib().kge_prep_query_split(model, direction, ptr(ent), rows(ent), ptr(eidx), ptr(rel), rows(rel),
-                                      ptr(ridx), n, d_e, d_r, ptr(q), rows(q) if q is not None else 0, ptr(hi),
-                                      ptr(lo), ldp, stream()), "kge_prep_query_split")
+    ld_ent = rows(ent)
+    # the kernel addresses row eidx[i] as ent + eidx[i] * ld: shift the base by eidx_base rows
+    _check(lib().kge_prep_query_split(model, direction, ptr(ent) - 4 * ld_ent * int(eidx_base), ld_ent, ptr(eidx),
+                                      ptr(rel), rows(rel), ptr(ridx), n, d_e, d_r, ptr(q),
+                                      rows(q) if q is not None else 0, ptr(hi), ptr(lo), ldp, stream()),
+           "kge_prep_query_split")
     return q, hi, lo
+
+
+def prep_query_packed(model, direction, ent, eidx, rel, ridx, eidx_base=0):
+    """The bf16 hi / lo planes of the query rows packed per row, [n, 2 ldp] = [hi | lo] with
+    ldp = round32(width): what score_dot_packed reads, in one buffer (the row-sharded path
+    exchanges it between GPUs).  eidx_base as in prep_query_split.  A lean wrapper: this sits on
+    the per-step host path of the multi-GPU scoring loop."""
+    d_e = ent.shape[1]
+    n = eidx.numel()
+    ldp = (query_width(model, d_e) + 31) // 32 * 32
+    packed = torch.empty(n, 2 * ldp, device=ent.device, dtype=torch.bfloat16)
+    if CHECK_INDEX:
+        require_device(ent, rel, eidx, ridx)
+        check_index(eidx - eidx_base, ent.shape[0], "entity index")
+        check_index(ridx, rel.shape[0], "relation index")
+    eidx, ridx = idx64(eidx), idx64(ridx)
+    ld_ent = rows(ent)
+    base = packed.data_ptr()
+    _check(lib().kge_prep_query_split(model, direction, ent.data_ptr() - 4 * ld_ent * int(eidx_base), ld_ent,
+                                      eidx.data_ptr(), rel.data_ptr(), rows(rel), ridx.data_ptr(), n, d_e,
+                                      rel.shape[1], None, 0, base, base + 2 * ldp, 2 * ldp, stream()),
+           "kge_prep_query_split")
+    return packed
+
+
+def score_dot_packed(packed, t, d, out=None):
+    """kge_score_dot_split on planes packed [hi | lo] per row (prep_query_packed)."""
+    n = packed.shape[0]
+    ldp = packed.shape[1] // 2
+    m = t.shape[0]
+    s = out if out is not None else torch.empty(n, m, device=t.device, dtype=torch.float32)
+    base = packed.data_ptr()
+    _check(lib().kge_score_dot_split(base, base + 2 * ldp, packed.stride(0), t.data_ptr(), rows(t), None, n, m, d,
+                                     s.data_ptr(), rows(s), stream()), "kge_score_dot_split")
+    return s
 
 
 def prep_query_split2(model, dir_a, dir_b, n_a, n_a_dev, ent, eidx, rel, ridx, d_e, d_r, out):

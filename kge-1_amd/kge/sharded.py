@@ -92,6 +92,22 @@ class EngineOps:
         dk, sign = dist_kind(self.kind, self.l_norm)
         return self.L.score_dist(dk, sign, q, tab, None, out=out)
 
+    # ---- query rows as bf16 hi / lo planes packed [hi | lo] per row: what the split contraction
+    # reads, in ONE buffer to exchange (the same bytes as the fp32 rows, and no split pass after)
+    def planes_ok(self, ent, direction) -> bool:
+        from .engine import BILINEAR, window
+
+        qw = self.L.query_width(self.kind, ent.shape[1])
+        return (self.kind in BILINEAR and ent.dim() == 2 and ent.stride(1) == 1
+                and self.L.split_ok(qw, window(self.kind, direction, ent), self.precision))
+
+    def prep_planes(self, direction, ent, eidx, rel, ridx, eidx_base=0):
+        """eidx: global row ids of the table whose rows [eidx_base, eidx_base + len(ent)) ent holds."""
+        return self.L.prep_query_packed(self.kind, direction, ent, eidx, rel, ridx, eidx_base)
+
+    def score_planes(self, packed, tab, out=None):
+        return self.L.score_dot_packed(packed, tab, tab.shape[1], out=out)
+
     # ---- vocab-parallel 1vsAll training
     def row_stats(self, s, c0, labels):
         return self.L.softmax_row_stats(s, c0, labels)
@@ -236,17 +252,23 @@ class RowShardedScorer:
         the query rows are prepared on the current stream and their all_gather is issued
         asynchronously (RCCL runs it on its own stream), so the caller can score the previous
         batch meanwhile.  Returns a ticket for ``score_submitted``."""
-        owned, local = self._owned_rows(e)
-        q = self.ops.prep(direction, self.ent, local, self.rel, p)
+        # shard-affine by contract: every query entity is one of this rank's rows
+        planes = getattr(self.ops, "planes_ok", None) is not None and self.ops.planes_ok(self.ent, direction)
+        if planes:  # bf16 hi / lo planes, packed per row: no split pass on the receiving side
+            q = self.ops.prep_planes(direction, self.ent, e, self.rel, p, eidx_base=self.lo)
+        else:
+            q = self.ops.prep(direction, self.ent, e - self.lo, self.rel, p).contiguous()
         out = torch.empty((self.world * q.shape[0], q.shape[1]), dtype=q.dtype, device=q.device)
-        work = all_gather_into_tensor(out, q.contiguous(), group=self.group, async_op=True)
-        return (work, out, q, direction)  # q is kept alive until the gather has read it
+        work = all_gather_into_tensor(out, q, group=self.group, async_op=True)
+        return (work, out, q, direction, planes)  # q is kept alive until the gather has read it
 
     def score_submitted(self, ticket) -> torch.Tensor:
         """Local slice [W*B, hi - lo] of the scores of a batch started by submit_queries_local."""
-        work, q_all, _, direction = ticket
+        work, q_all, _, direction, planes = ticket
         if work is not None:
             work.wait()  # the current stream waits for the gather; the host does not block
+        if planes:
+            return self.ops.score_planes(q_all, self._win(direction, self.ent))
         return self.ops.score(q_all, self._win(direction, self.ent))
 
     def topk(self, scores_local: torch.Tensor, k: int):

@@ -139,3 +139,43 @@ def test_sharded_jobs_world1_rccl_match_unsharded_jobs(L):
         assert runs["on"][4] == pytest.approx(runs["off"][4], rel=1e-2)
     finally:
         dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("kind,prec,d", [("complex", "bf16x3", 64), ("distmult", "bf16x3", 40), ("complex", "fp32", 64),
+                                          ("transe", "bf16x3", 64)])
+def test_pipelined_exchange_world1_matches_direct_scoring(L, kind, prec, d):
+    """submit_queries_local / score_submitted (the N > 1 bench's step: query rows exchanged as
+    packed bf16 planes where the split contraction applies, as fp32 rows otherwise) at world
+    size 1 over RCCL against score_sp_local and against the engine's own score_all -- identical."""
+    from kge import engine
+    from kge.sharded import EngineOps, RowShardedScorer
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()))
+    dist.init_process_group("nccl", rank=0, world_size=1)
+    try:
+        E, R, B = 333, 5, 48
+        k = {"complex": L.COMPLEX, "distmult": L.DISTMULT, "transe": L.TRANSE}[kind]
+        g = torch.Generator().manual_seed(d)
+        ent = (torch.randn(E, d, generator=g) * 0.3).cuda()
+        rel = (torch.randn(R, d, generator=g) * 0.3).cuda()
+        ops = EngineOps(k, L.PRECISIONS[prec])
+        lo = 56  # this rank's rows start here: the queries carry GLOBAL entity ids
+        shard = ent[lo:]
+        sh = RowShardedScorer(shard, lo, E, E, rel, ops)
+        s = torch.randint(lo, E, (3, B), generator=g).cuda()
+        p = torch.randint(0, R, (3, B), generator=g).cuda()
+        assert ops.planes_ok(shard, L.DIR_SP) == (prec == "bf16x3" and kind != "transe")
+        tickets = [sh.submit_queries_local(s[0], p[0])]
+        outs = []
+        for i in range(3):  # batch i + 1 in flight while batch i is scored
+            if i + 1 < 3:
+                tickets.append(sh.submit_queries_local(s[i + 1], p[i + 1]))
+            outs.append(sh.score_submitted(tickets.pop(0)))
+        torch.cuda.synchronize()
+        for i in range(3):
+            direct = sh.score_sp_local(s[i], p[i])
+            assert torch.equal(outs[i], direct)
+            ref = engine.score_all(k, L.DIR_SP, L.PRECISIONS[prec], 1.0, ent, s[i], rel, p[i], shard, None)
+            assert torch.equal(outs[i], ref)
+    finally:
+        dist.destroy_process_group()
