@@ -152,8 +152,10 @@ __global__ void __launch_bounds__(NT) score_dist2_kernel(float sign, const float
     for (int half = 0; half < 2; ++half) {
       const int j = j0 + 64 * half + 4 * tx;
       float v[4] = {acc[a][2 * half].x, acc[a][2 * half].y, acc[a][2 * half + 1].x, acc[a][2 * half + 1].y};
-      if constexpr (KIND == KGE_DIST_L1)
+      if constexpr (KIND == KGE_DIST_L1) {
+#pragma unroll
         for (int e = 0; e < 4; ++e) v[e] = acc1[a][4 * half + e];
+      }
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         if (KIND == KGE_DIST_L2 || KIND == KGE_DIST_ROT_L2) v[e] = sqrtf(v[e]);
@@ -169,8 +171,8 @@ __global__ void __launch_bounds__(NT) score_dist2_kernel(float sign, const float
 
 }  // namespace
 
-// Packed-VALU launcher used by kge_score_dist when the layout allows; returns -1 when it
-// does not (the caller then takes the generic kernel).
+// Launcher of the register-tiled kernel, used by kge_score_dist when the layout allows; returns
+// -1 when it does not (the caller then takes score_dist.hip's kernel).
 int kge_score_dist2(int kind, float sign, const float* q, int64_t ldq, const float* t, int64_t ldt,
                     const int64_t* tidx, int64_t n, int64_t m, int d, float* s, int64_t lds, hipStream_t st) {
   const int kdim = kind >= KGE_DIST_ROT_L1 ? d / 2 : d;

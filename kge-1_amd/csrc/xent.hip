@@ -464,10 +464,14 @@ int launch_planes(float* s, int64_t lds, int64_t n, int64_t n_pad, int64_t m, co
     softmax_planes_kernel<1, 256><<<grid, dim3(256), 0, st>>>(s, lds, (int)n, (int)m, l_ptr, l_col, eps, scale, loss);
   else if (m4 <= 2 * 256 * 4 * U)
     softmax_planes_kernel<2, 256><<<grid, dim3(256), 0, st>>>(s, lds, (int)n, (int)m, l_ptr, l_col, eps, scale, loss);
-  else if (m4 <= 1024 * 4 * U)
-    softmax_planes_kernel<1, 1024><<<grid, dim3(1024), 0, st>>>(s, lds, (int)n, (int)m, l_ptr, l_col, eps, scale, loss);
-  else if (m4 <= 2 * 1024 * 4 * U)
-    softmax_planes_kernel<2, 1024><<<grid, dim3(1024), 0, st>>>(s, lds, (int)n, (int)m, l_ptr, l_col, eps, scale, loss);
+  // wider rows: 512 threads holding 2 .. 4 register slabs each (1,024-thread workgroups cap a
+  // thread at 128 VGPRs, which the two-slab row does not fit: it spilled 34 of them)
+  else if (m4 <= 2 * 512 * 4 * U)
+    softmax_planes_kernel<2, 512><<<grid, dim3(512), 0, st>>>(s, lds, (int)n, (int)m, l_ptr, l_col, eps, scale, loss);
+  else if (m4 <= 3 * 512 * 4 * U)
+    softmax_planes_kernel<3, 512><<<grid, dim3(512), 0, st>>>(s, lds, (int)n, (int)m, l_ptr, l_col, eps, scale, loss);
+  else if (m4 <= 4 * 512 * 4 * U)
+    softmax_planes_kernel<4, 512><<<grid, dim3(512), 0, st>>>(s, lds, (int)n, (int)m, l_ptr, l_col, eps, scale, loss);
   else
     return KGE_ERR_ARG;
   KGE_CHECK_LAUNCH();
@@ -508,7 +512,7 @@ extern "C" int kge_loss_sums(const float* loss, int64_t n, int64_t n_first, cons
   return 0;
 }
 
-extern "C" int64_t kge_softmax_planes_max_columns(void) { return 2LL * 1024 * 4 * U; }
+extern "C" int64_t kge_softmax_planes_max_columns(void) { return 4LL * 512 * 4 * U; }
 
 extern "C" int kge_softmax_xent_planes(float* s, int64_t lds, int64_t n, int64_t n_pad, int64_t m,
                                        const int64_t* labels, float scale, float* loss, void* stream) {
