@@ -56,12 +56,17 @@ __global__ void __launch_bounds__(NT) score_dist2_kernel(float sign, const float
       const int kk = k + 4 * sl;
       const bool ok = kk < kdim;
       const int kc = ok ? kk : 0;
-      const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
-      pf[0][0][sl] = ok ? *reinterpret_cast<const float4*>(qrow + kc) : z;
-      pf[1][0][sl] = ok ? *reinterpret_cast<const float4*>(trow + kc) : z;
+      // load from the clamped address first, select afterwards: `ok ? *p : z` compiles into a
+      // load through a selected pointer (global row or a zero on the stack), i.e. flat loads
+      auto ld4 = [&](const float* p) {
+        const float4 v = *reinterpret_cast<const float4*>(p);
+        return make_float4(ok ? v.x : 0.f, ok ? v.y : 0.f, ok ? v.z : 0.f, ok ? v.w : 0.f);
+      };
+      pf[0][0][sl] = ld4(qrow + kc);
+      pf[1][0][sl] = ld4(trow + kc);
       if constexpr (ROT) {
-        pf[0][1][sl] = ok ? *reinterpret_cast<const float4*>(qrow + h + kc) : z;
-        pf[1][1][sl] = ok ? *reinterpret_cast<const float4*>(trow + h + kc) : z;
+        pf[0][1][sl] = ld4(qrow + h + kc);
+        pf[1][1][sl] = ld4(trow + h + kc);
       }
     }
   };

@@ -56,3 +56,32 @@ k:
     lines = ok.split("\n")
     (sym, a, b), = A.functions(lines)
     assert A.audit(lines, a, b) == ([], 1)
+
+
+def test_no_kernel_uses_scratch_flat_or_packed_fp32(tmp_path):
+    """Every HIP source of the library, compiled as the Makefile compiles it: no kernel may spill
+    to or index scratch memory (register pressure, pointer-select loads), address through flat
+    instructions, or contain packed fp32 VALU instructions (the build switches them off)."""
+    import glob
+    import re
+    from concurrent.futures import ThreadPoolExecutor
+
+    if not os.path.exists(HIPCC):
+        pytest.skip("no hipcc")
+    srcs = sorted(glob.glob(os.path.join(ROOT, "kge-1_amd", "csrc", "*.hip")))
+    assert len(srcs) >= 10
+
+    def build(src):
+        out = tmp_path / (os.path.basename(src) + ".s")
+        subprocess.run([HIPCC] + FLAGS + [src, "-o", str(out)], check=True, capture_output=True)
+        return out
+
+    with ThreadPoolExecutor(max_workers=4) as pool:
+        outs = list(pool.map(build, srcs))
+    bad = {}
+    pat = re.compile(r"^\s*(scratch_\w+|flat_(load|store|atomic)\w*|v_pk_(add|mul|fma)_f32)\b")
+    for out in outs:
+        hits = [ln.strip() for ln in open(out) if pat.match(ln)]
+        if hits:
+            bad[os.path.basename(str(out))] = hits[:5]
+    assert not bad, bad
