@@ -235,3 +235,44 @@ def test_kvsall_graph_step_falls_back_when_labels_exceed_capacity():
     for b in range(4):
         job.train_step(b, job._collate(torch.arange(b * 64, b * 64 + 64)))
     assert job._graph_step.graph is None and not job._graph_step.disabled
+
+
+@pytest.mark.parametrize("train_type", ["1vsAll", "KvsAll"])
+def test_job_loop_memorises_its_training_triples(train_type):
+    """End to end through TrainingJob.run() with the default engine options (recorded graph
+    step, fused loss and optimizer, refined bf16x3 evaluation, validation every few epochs):
+    validation triples that are training triples must reach a filtered MRR near 1 -- the
+    evaluation reads the tables the replayed steps update."""
+    from kge import Config, Dataset
+    from kge.job import TrainingJob
+
+    E, R = 400, 6
+    c = Config()
+    c.set("model", "complex")
+    c._import("complex")
+    c.set("job.device", "cuda")
+    c.set("lookup_embedder.dim", 64)
+    c.set("lookup_embedder.initialize_args", {"mean": 0.0, "std": 0.1})
+    c.set("train.type", train_type)
+    c.set("train.batch_size", 128)
+    c.set("train.optimizer", "Adagrad")
+    c.set("train.optimizer_args", {"lr": 0.5})
+    c.set("train.max_epochs", 40)
+    c.set("valid.every", 20)
+    c.set("eval.batch_size", 100)
+    c.set("dataset.num_entities", E)
+    c.set("dataset.num_relations", R)
+    c.set("verbose", False)
+    g = torch.Generator().manual_seed(11)
+    tr = torch.stack([torch.randint(0, E, (1500,), generator=g), torch.randint(0, R, (1500,), generator=g),
+                      torch.randint(0, E, (1500,), generator=g)], 1).int()
+    ds = Dataset(c, None)
+    ds._triples = {"train": tr, "valid": tr[:250].clone(), "test": tr[250:300].clone()}
+    torch.manual_seed(0)
+    job = TrainingJob.create(c, ds)
+    traces = job.run()
+    assert job._graph_step is not None and job._graph_step.graph is not None, job._graph_step.error
+    assert traces[-1]["avg_loss"] < 0.5 * traces[0]["avg_loss"]
+    assert len(job.valid_trace) == 2
+    assert job.valid_trace[-1]["mean_reciprocal_rank_filtered"] > 0.9, job.valid_trace[-1]
+    assert job.valid_trace[-1]["hits_at_1_filtered"] > 0.85
