@@ -374,6 +374,12 @@ def score_all_xent2(kind: int, precision: int, ent: torch.Tensor, rel: torch.Ten
                              L.idx64(lptr_b), float(smoothing), float(scale))
 
 
+def stacked_xent_applicable(kind: int, precision: int, ent: torch.Tensor, dir_a: int, dir_b: int) -> bool:
+    """Whether score_all_xent_stacked serves this scorer / precision / table layout."""
+    return (kind in BILINEAR and not (kind == L.CP and dir_a != dir_b)
+            and _planes_applicable(kind, precision, _rows(ent), dir_a))
+
+
 def score_all_xent_stacked(kind: int, precision: int, ent: torch.Tensor, rel: torch.Tensor, dir_a: int, dir_b: int,
                            eidx: torch.Tensor, ridx: torch.Tensor, n_a_dev: torch.Tensor, labels: torch.Tensor,
                            l_ptr: Optional[torch.Tensor], scale: float, smoothing: float = 0.0):
@@ -381,10 +387,8 @@ def score_all_xent_stacked(kind: int, precision: int, ent: torch.Tensor, rel: to
     rest dir_b) with n_a an int64 device scalar -- nothing here depends on its value on the host,
     so the launches can be recorded once and replayed for batches whose split differs.  Served by
     the plane-fed path only: None when it does not apply to this scorer / precision / layout."""
-    if kind not in BILINEAR or (kind == L.CP and dir_a != dir_b):
-        return None
     L.require_device(ent, rel, eidx, ridx, n_a_dev)
-    if not _planes_applicable(kind, precision, ent, dir_a):
+    if not stacked_xent_applicable(kind, precision, ent, dir_a, dir_b):
         return None
     sq = StackedQueries(dir_a, dir_b, L.idx64(eidx), L.idx64(ridx), 0, L.idx64(n_a_dev))
     return _ScoreXentPlanes.apply(kind, ent, rel, sq, L.idx64(labels), L.idx64(l_ptr), float(smoothing), float(scale))

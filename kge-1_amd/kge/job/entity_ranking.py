@@ -213,7 +213,12 @@ class EntityRankingJob(EvaluationJob):
                 _lib.COMPLEX, _lib.DISTMULT, _lib.RESCAL, _lib.SIMPLE)
             if self._refine:
                 ent_rows = tabs[0].detach()
-            else:
+                # the rescoring reads the rows as float4 (kge_rank_rows): 16-B aligned rows of a
+                # multiple of 4 columns; any other layout ranks fp32 scores
+                self._refine = (ent_rows.dim() == 2 and ent_rows.stride(1) == 1 and ent_rows.shape[1] % 4 == 0
+                                and ent_rows.stride(0) % 4 == 0 and ent_rows.data_ptr() % 16 == 0)
+            if not self._refine:
+                ent_rows = None
                 self.model.get_scorer().precision_override = "fp32"
         ranks_out = {f"{d}{r}": [] for d in "so" for r in self.rankings}
         epoch_time = -time.time()

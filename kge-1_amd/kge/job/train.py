@@ -625,8 +625,20 @@ class TrainingJobKvsAll(TrainingJob):
                 and self.kge_lr_scheduler._lr_scheduler is None
                 and not self.pre_batch_hooks
                 and not sharding_enabled(self.config)
-                and self.model._lookup_tables() is not None):
+                and self._stacked_applicable()):
             self._graph_step = _KvsAllGraphStep(self)
+
+    def _stacked_applicable(self) -> bool:
+        """Whether the recorded step's engine pass (KgeModel.score_xent_stacked) serves this model."""
+        from .. import _lib, engine
+
+        tabs = self.model._lookup_tables()
+        scorer = self.model.get_scorer()
+        if tabs is None or scorer.engine_kind is None:
+            return False
+        dirs = [(_lib.DIR_SP if spec[0] == "sp_" else _lib.DIR_PO) for spec in self._part_spec]
+        return engine.stacked_xent_applicable(scorer.engine_kind, scorer.precision(), tabs[0].detach(), dirs[0],
+                                              dirs[-1])
 
     def _stacked_block(self, ex: np.ndarray):
         """The batch as ONE flat int64 block for the recorded step (_KvsAllGraphStep): stacked

@@ -276,3 +276,18 @@ def test_job_loop_memorises_its_training_triples(train_type):
     assert len(job.valid_trace) == 2
     assert job.valid_trace[-1]["mean_reciprocal_rank_filtered"] > 0.9, job.valid_trace[-1]
     assert job.valid_trace[-1]["hits_at_1_filtered"] > 0.85
+
+
+def test_kvsall_graph_step_not_used_when_the_plane_path_does_not_apply():
+    """dim 50 rows cannot feed the plane-fed kernels: no graph step is set up and every batch runs
+    eagerly, with the same losses as a job with engine.graph_step off."""
+    losses = {}
+    for graph in (True, False):
+        job = _kvsall_job(graph, "distmult", dim=50)
+        out = []
+        for b in range(5):
+            res, _, _ = job.train_step(b, job._collate(torch.arange(b * 64, b * 64 + 64)))
+            out.append(float(res.loss))
+        losses[graph] = out
+        assert job._graph_step is None
+    np.testing.assert_allclose(losses[True], losses[False], rtol=2e-5)

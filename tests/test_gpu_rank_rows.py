@@ -208,13 +208,14 @@ def test_rank_rows_refinement_equals_exact_scoring(L, d, m):
 
 
 @pytest.mark.parametrize("model,dim", [("distmult", 64), ("rescal", 16), ("simple", 64), ("complex", 64), ("cp", 64),
-                                       ("transe", 64), ("rotate", 64)])
+                                       ("transe", 64), ("rotate", 64), ("complex", 50), ("distmult", 37)])
 @pytest.mark.parametrize("chunk", [-1, 700])
 def test_refined_eval_job_every_model_vs_exact_scoring(model, dim, chunk):
     """EntityRankingJob with engine.eval_precision bf16x3_refined (the default) for every
     scorer against the oracle's job on float64 scores rounded to fp32 (entity_ranking.py:79-577
-    restated): DistMult / RESCAL / SimplE / ComplEx take the refined bf16x3 path, CP and the
-    distance models fall back to fp32 scoring.  The engine prepares its query rows in fp32, so
+    restated): DistMult / RESCAL / SimplE / ComplEx take the refined bf16x3 path, CP, the
+    distance models and row widths the rescoring cannot read as float4 (dim 50, 37) fall back to
+    fp32 scoring.  The engine prepares its query rows in fp32, so
     a rank may differ from exact scoring only at a near-tie at the level of fp32 rounding:
     every moved rank is checked against the float64 score row (1e-6 of the row maximum)."""
     from test_gpu_configs import base_config, set_tables
