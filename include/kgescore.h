@@ -279,7 +279,7 @@ int kge_softmax_kl_planes(float* s, int64_t lds, int64_t n, int64_t n_pad, int64
 int kge_loss_sums(const float* loss, int64_t n, int64_t n_first, const int64_t* n_first_dev, float scale,
                   float* parts, float* total, void* stream);
 
-/* Vocab-parallel 1vsAll (entity table row-sharded): S holds columns
+/* Vocab-parallel 1vsAll (entity table row-sharded over the GPUs): S holds columns
  * [c0, c0 + m) of the full score rows, labels are global column ids.
  * row_stats: row_max[i], row_sumexp[i] = sum_j exp(S[i, j] - row_max[i]) over the slice, and
  *            target[i] = S[i, labels[i] - c0] when the label is in the slice, else 0

@@ -1,5 +1,4 @@
-// Backward of the all-entities contraction S = Q . T^T (autograd of score_sp/score_po,
-// SURVEY.md §8a A12):
+// Backward of the all-entities contraction S = Q . T^T (autograd of score_sp/score_po):
 //   dQ = G . T        [n, d]  (K = m: long reduction, split over workgroups)
 //   dT += G^T . Q     [m, d]  (K = n), rows scattered through tidx when given
 // KGE_PREC_FP32 runs here on the exact fp32-input MFMA (v_mfma_f32_32x32x2_f32);

@@ -1,7 +1,7 @@
 // Query preparation (fused LookupEmbedder gather + per-model prologue) and its backward.
 //
 // Every in-scope scorer reduces to "per-query prep + one contraction (dot or distance)
-// against the entity table" (SURVEY.md §8a A6-A10).  These kernels produce the query
+// against the entity table".  These kernels produce the query
 // rows Q[n, d_e]; they are small (n * d work) next to the contraction.
 #include "common.h"
 

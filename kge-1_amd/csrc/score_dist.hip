@@ -1,4 +1,4 @@
-// All-entities distance scoring for TransE and RotatE (SURVEY.md §8a A9/A10): VALU
+// All-entities distance scoring for TransE and RotatE: VALU
 // work with no MFMA.  S[i, j] = sign * dist(Q[i], T[row(j)]).
 //
 // The reference materialises the pairwise difference tensor (rotate.py:41-60:

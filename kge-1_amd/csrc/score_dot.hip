@@ -1,5 +1,5 @@
 // All-entities contraction S = Q . T^T for the bilinear scorers (ComplEx, DistMult,
-// RESCAL): the hot kernel of score_sp / score_po (SURVEY.md §8a A1/A2, A6-A8).
+// RESCAL): the hot kernel of score_sp / score_po.
 //
 // Shape: Q [n, d] (prepared query rows), T [m, d] (entity table rows, optionally
 // gathered through tidx), S [n, m] fp32.  Both operands are K-contiguous, so every MFMA

@@ -13,7 +13,7 @@
 // Index labels (1vsAll, KLDivWithSoftmaxKgeLoss -> CrossEntropyLoss, loss.py:198-208) are
 // the case |P_i| = 1, eps = 0: loss_i = lse_i - S_i,label, G = scale (softmax - onehot).
 //
-// Column-sharded rows (vocab-parallel 1vsAll over the row-sharded entity table, SURVEY 8e):
+// Column-sharded rows (vocab-parallel 1vsAll over the row-sharded entity table):
 // kge_softmax_row_stats gives each shard's (max, sum exp(x - max), target score) for the
 // cross-shard reduction, kge_softmax_grad the shard's slice of G from the global lse.
 //

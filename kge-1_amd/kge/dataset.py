@@ -84,6 +84,37 @@ class KvsAllIndex:
         return ptr, col
 
 
+def _relation_types(train: np.ndarray, num_relations: int):
+    """Relation -> "1-1" / "1-N" / "M-1" / "M-N" (indexing.py:142-179): M when a (p, o) pair of the
+    relation has more than 1.5 subjects on average over the training triples, N likewise for
+    objects per (s, p) pair; fp32 ratios, duplicates counted, no training triples -> "1-1"."""
+    t = np.asarray(train, dtype=np.int64)
+    R = num_relations
+    n = np.bincount(t[:, 1], minlength=R).astype(np.float32)
+    big = int(t[:, [0, 2]].max(initial=0)) + 1
+    distinct_po = np.bincount(np.unique(t[:, 1] * big + t[:, 2]) // big, minlength=R).astype(np.float32)
+    distinct_sp = np.bincount(np.unique(t[:, 1] * big + t[:, 0]) // big, minlength=R).astype(np.float32)
+    with np.errstate(invalid="ignore", divide="ignore"):
+        is_m = n / distinct_po > 1.5
+        is_n = n / distinct_sp > 1.5
+    return ["{}-{}".format("M" if m else "1", "N" if k else "1") for m, k in zip(is_m, is_n)]
+
+
+PERCENTILES = (("25%", 0.0, 0.25), ("50%", 0.25, 0.5), ("75%", 0.5, 0.75), ("top", 0.75, 1.0))
+
+
+def _frequency_percentiles(train: np.ndarray, num_entities: int, num_relations: int):
+    """{"subject" | "relation" | "object": {"25%" | "50%" | "75%" | "top": set of ids}}: the ids of a
+    slot ordered by training frequency (ties in id order), cut at int(fraction * count)
+    (indexing.py:200-263)."""
+    t = np.asarray(train, dtype=np.int64)
+    out = {}
+    for arg, col, num in (("subject", 0, num_entities), ("relation", 1, num_relations), ("object", 2, num_entities)):
+        order = np.argsort(np.bincount(t[:, col], minlength=num), kind="stable")
+        out[arg] = {name: set(order[int(b * num):int(e * num)].tolist()) for name, b, e in PERCENTILES}
+    return out
+
+
 class Dataset(Configurable):
     def __init__(self, config: Config, folder: Optional[str] = None):
         super().__init__(config, "dataset")
@@ -194,9 +225,20 @@ class Dataset(Configurable):
         return self._triples[split]
 
     def index(self, key: str):
-        """"<split>_sp_to_o" or "<split>_po_to_s" (indexing.py:287-301)."""
+        """"<split>_sp_to_o" / "<split>_po_to_s" (indexing.py:287-301), "relation_types",
+        "relations_per_type" and "frequency_percentiles" (indexing.py:142-263)."""
         if key not in self._indexes:
-            if key.endswith("_sp_to_o"):
+            if key == "relation_types":
+                self._indexes[key] = _relation_types(self.split("train").numpy(), self.num_relations())
+            elif key == "relations_per_type":
+                per_type: Dict[str, set] = {}
+                for i, k in enumerate(self.index("relation_types")):
+                    per_type.setdefault(k, set()).add(i)
+                self._indexes[key] = per_type
+            elif key == "frequency_percentiles":
+                self._indexes[key] = _frequency_percentiles(
+                    self.split("train").numpy(), self.num_entities(), self.num_relations())
+            elif key.endswith("_sp_to_o"):
                 t = self.split(key[: -len("_sp_to_o")]).numpy()
                 self._indexes[key] = KvsAllIndex(t, (0, 1), 2)
             elif key.endswith("_po_to_s"):

@@ -88,10 +88,10 @@ class EntityRankingJob(EvaluationJob):
         #: additional metrics per slot: "..._head" ranks the subject of (?, p, o), "..._tail" the
         #: object of (s, p, ?) (eval.py:125-146)
         self.head_and_tail = config.get("entity_ranking.metrics_per.head_and_tail")
-        for k in ("relation_type", "argument_frequency"):
-            if config.get("entity_ranking.metrics_per." + k):
-                raise NotImplementedError(
-                    f"entity_ranking.metrics_per.{k} (eval.py:149-224) is not implemented; set it to False")
+        #: metrics per relation class and per training-frequency quartile of the ranked slot's
+        #: query arguments (eval.py:174-224)
+        self.per_relation_type = config.get("entity_ranking.metrics_per.relation_type")
+        self.per_argument_frequency = config.get("entity_ranking.metrics_per.argument_frequency")
         #: compute ops of the row-sharded path; None: the engine (kge.sharded.EngineOps)
         self.sharded_ops = None
         self.capture_ranks = False  # keep per-query ranks in self.ranks (tests / tracing)
@@ -144,6 +144,54 @@ class EntityRankingJob(EvaluationJob):
             sp += [t[:, 1], t[:, 1]]
         self._stack_e = torch.cat(se).contiguous().to(dev) if se else torch.zeros(0, dtype=torch.int64, device=dev)
         self._stack_p = torch.cat(sp).contiguous().to(dev) if sp else torch.zeros(0, dtype=torch.int64, device=dev)
+
+        self._prepare_groups(tri, dev)
+
+    def _prepare_groups(self, tri: np.ndarray, dev):
+        """Per evaluation triple and ranking direction (0: object of (s, p, ?), 1: subject of
+        (?, p, o)) the group of each requested breakdown; -1 leaves the rank out of it.
+        self._groups: name -> (group names, ids [2, N] on the device)."""
+        from ..dataset import PERCENTILES
+
+        self._groups = {}
+        s, p, o = tri[:, 0].astype(np.int64), tri[:, 1].astype(np.int64), tri[:, 2].astype(np.int64)
+        if self.per_relation_type:
+            names = list(self.dataset.index("relations_per_type"))
+            of_type = {k: i for i, k in enumerate(names)}
+            type_of_rel = np.array([of_type[k] for k in self.dataset.index("relation_types")], np.int64)
+            g = type_of_rel[p] if len(p) else p
+            self._groups["relation_type"] = (names, torch.from_numpy(np.stack([g, g])).to(dev))
+        if self.per_argument_frequency:
+            percs = self.dataset.index("frequency_percentiles")
+            names = [name for name, _, _ in PERCENTILES]
+
+            def quartile_of(arg, num, ids):
+                q = np.full(num, -1, np.int64)
+                for gi, name in enumerate(names):
+                    members = np.fromiter(percs[arg][name], np.int64, len(percs[arg][name]))
+                    q[members] = gi
+                return q[ids] if len(ids) else ids
+
+            E, R = self.dataset.num_entities(), self.dataset.num_relations()
+            none = np.full(len(p), -1, np.int64)
+            gp = quartile_of("relation", R, p)
+            for arg, ids in (("subject", np.stack([none, quartile_of("subject", E, s)])),
+                             ("relation", np.stack([gp, gp])),
+                             ("object", np.stack([quartile_of("object", E, o), none]))):
+                self._groups[arg] = (names, torch.from_numpy(ids).to(dev))
+
+    def _count_groups(self, group_hists, rk, b0, B):
+        """Adds the ranks rk [ranking, direction, B] of the batch at b0 to every breakdown's
+        histograms [ranking, direction, group (+ one unused slot for left-out ranks), rank]."""
+        nrank = rk.shape[0]
+        for name, (names, ids) in self._groups.items():
+            h = group_hists[name]
+            G1, E = h.shape[2], h.shape[3]
+            g = ids[:, b0:b0 + B]
+            g = torch.where(g < 0, G1 - 1, g)
+            slot = torch.arange(nrank * 2, device=rk.device).view(nrank, 2, 1)
+            idx = ((slot * G1 + g.unsqueeze(0)) * E + rk).view(-1)
+            h.view(-1).index_add_(0, idx, torch.ones(idx.numel(), device=rk.device))
 
     @staticmethod
     def _stack_csr(csr, dev):
@@ -203,6 +251,8 @@ class EntityRankingJob(EvaluationJob):
         hists_d = torch.zeros(nrank, 2, E, device=dev)
         hists_flat = hists_d.view(nrank * 2, E)
         hists_sharded = torch.zeros(2, nrank, E, device=dev) if sharded is not None else None
+        group_hists = {name: torch.zeros(nrank, 2, len(names) + 1, E, device=dev)
+                       for name, (names, _) in self._groups.items()}
         tmax = None
         ent_rows = None
         if self._refine:
@@ -237,13 +287,15 @@ class EntityRankingJob(EvaluationJob):
                     (tf["sp"][0][b0:], tf["sp"][1]) if tf is not None else None,
                     (tf["po"][0][b0:], tf["po"][1]) if tf is not None else None,
                     p_inverse=(p + self.dataset.num_relations()) if self._two_sided else None)
+                rk = torch.empty(2, nrank, B, dtype=torch.int64, device=dev)
                 for di, d in enumerate("os"):
-                    rk = torch.empty(nrank * B, dtype=torch.int64, device=dev)
                     sharded.ops.rank_hist_multi(counts[di, 0, :nrank * B], counts[di, 1, :nrank * B], B,
-                                                self.tie_handling, rk, hists_sharded[di])
+                                                self.tie_handling, rk[di].view(-1), hists_sharded[di])
                     if self.capture_ranks:
                         for ri, r in enumerate(self.rankings):
-                            ranks_out[f"{d}{r}"].append(rk[ri * B:(ri + 1) * B])
+                            ranks_out[f"{d}{r}"].append(rk[di, ri])
+                if group_hists:
+                    self._count_groups(group_hists, rk.permute(1, 0, 2), b0, B)
                 continue
             o_true = self.model.score_spo(s, p, o, "o").view(-1).float().contiguous()
             # score_spo(.., "s") is the same triple score unless the model scores the two
@@ -277,8 +329,10 @@ class EntityRankingJob(EvaluationJob):
                 del scores
             if not single:
                 _lib.rank_hist_multi(counts[0], counts[1], B, self.tie_handling, rk, hists_flat)
+            rk = rk.view(nrank, 2, B)
+            if group_hists:
+                self._count_groups(group_hists, rk, b0, B)
             if self.capture_ranks:
-                rk = rk.view(nrank, 2, B)
                 for di, d in enumerate("os"):
                     for ri, r in enumerate(self.rankings):
                         ranks_out[f"{d}{r}"].append(rk[ri, di])
@@ -286,12 +340,23 @@ class EntityRankingJob(EvaluationJob):
         metrics = {}
         if hists_sharded is not None:
             hists_d += hists_sharded.permute(1, 0, 2)
-        hists = hists_d.sum(1)  # counts are small integers: the fp32 sum is exact
-        for ri, r in enumerate(self.rankings):
-            metrics.update(self._compute_metrics(hists[ri], RANKING_SUFFIX[r]))
-            if self.head_and_tail:  # entity_ranking.py:376-387 (suffix order: ranking, then slot)
-                metrics.update(self._compute_metrics(hists_d[ri, 1], RANKING_SUFFIX[r] + "_head"))
-                metrics.update(self._compute_metrics(hists_d[ri, 0], RANKING_SUFFIX[r] + "_tail"))
+        # key -> [ranking, rank] histograms in the order of the reference's hooks (eval.py:148-224);
+        # counts are small integers: the fp32 sums are exact
+        keyed = {"all": hists_d.sum(1)}
+        if self.head_and_tail:
+            keyed["head"], keyed["tail"] = hists_d[:, 1], hists_d[:, 0]
+        for name, (names, _) in self._groups.items():
+            h = group_hists[name]
+            for gi, g in enumerate(names):
+                if name == "relation_type":
+                    keyed[g] = h[:, :, gi].sum(1)
+                    if self.head_and_tail:
+                        keyed[g + "_head"], keyed[g + "_tail"] = h[:, 1, gi], h[:, 0, gi]
+                else:
+                    keyed[f"{name}_{g}"] = h[:, :, gi].sum(1)
+        for key, h in keyed.items():  # entity_ranking.py:376-387: per key, every ranking
+            for ri, r in enumerate(self.rankings):
+                metrics.update(self._compute_metrics(h[ri], RANKING_SUFFIX[r] + ("_" + key if key != "all" else "")))
         if self.capture_ranks:
             self.ranks = {k: torch.cat(v).cpu().numpy() if v else np.zeros(0, np.int64)
                           for k, v in ranks_out.items()}

@@ -1,4 +1,4 @@
-"""Entity-table row sharding over the GPUs of one node (SURVEY.md §8e).
+"""Entity-table row sharding over the GPUs of one node.
 
 One process per GPU (torch.distributed, backend "nccl" = RCCL over xGMI).  GPU k owns
 entity rows [k*ceil(E/W), (k+1)*ceil(E/W)) -- exactly the reference's
@@ -290,7 +290,7 @@ class RowShardedScorer:
 
     # ---------------------------------------------------------------- training
     def train_1vsall_grads(self, s: torch.Tensor, p: torch.Tensor, o: torch.Tensor):
-        """Vocab-parallel 1vsAll (SURVEY.md 8e "training collectives"): every rank passes its
+        """Vocab-parallel 1vsAll: every rank passes its
         own B triples; the global batch is the W*B gathered triples and the objective is
         the reference's  sum over (sp_, _po) of CE(scores, target) / (W*B)
         (train.py:1032-1062 with batch W*B).  Per direction:

@@ -8,7 +8,7 @@ imports this module and fails loudly when its HIP library is missing.
 Pinning: every function here is checked against the golden vectors in
 ``tests/golden/*.npz`` (``tests/test_oracle_golden.py``), which were produced by running
 the reference itself (``tests/golden/make_golden.py``).  The reference's own unit tests
-(tests/test_dataset.py) pin nothing on this path (SURVEY.md section 4), so the captured
+(tests/test_dataset.py) pin nothing on this path, so the captured
 fixtures are the pin.
 
 All citations are ``file:line`` into the reference checkout (kge/...).
@@ -427,11 +427,96 @@ def sp_po_index(triples: np.ndarray):
     return sp, po
 
 
+def relation_types(train: np.ndarray, num_relations: int) -> List[str]:
+    """index_relation_types (indexing.py:142-179): per relation, the mean number of subjects per
+    distinct (p, o) and of objects per distinct (s, p) over the training triples (duplicates
+    counted, as the index's value lists keep them, indexing.py:37-53), each compared with 1.5 in
+    fp32; a relation without training triples gives nan > 1.5 = False, i.e. "1-1"."""
+    stats = np.zeros((num_relations, 4), np.float32)  # num_s, distinct po, num_o, distinct sp
+    seen_po, seen_sp = set(), set()
+    for s, p, o in train.tolist():
+        stats[p, 0] += 1
+        stats[p, 2] += 1
+        if (p, o) not in seen_po:
+            seen_po.add((p, o))
+            stats[p, 1] += 1
+        if (s, p) not in seen_sp:
+            seen_sp.add((s, p))
+            stats[p, 3] += 1
+    with np.errstate(invalid="ignore", divide="ignore"):
+        is_m = stats[:, 0] / stats[:, 1] > 1.5
+        is_n = stats[:, 2] / stats[:, 3] > 1.5
+    return ["{}-{}".format("M" if m else "1", "N" if n else "1") for m, n in zip(is_m, is_n)]
+
+
+def relations_per_type(types: Sequence[str]) -> Dict[str, set]:
+    """index_relations_per_type (indexing.py:182-197): type -> set of relations, in order of
+    each type's first relation."""
+    out: Dict[str, set] = {}
+    for i, k in enumerate(types):
+        out.setdefault(k, set()).add(i)
+    return out
+
+
+PERCENTILES = (("25%", 0.0, 0.25), ("50%", 0.25, 0.5), ("75%", 0.5, 0.75), ("top", 0.75, 1.0))
+
+
+def frequency_percentiles(train: np.ndarray, num_entities: int, num_relations: int) -> Dict[str, Dict[str, set]]:
+    """index_frequency_percentiles (indexing.py:200-263): ids sorted by their training frequency
+    in the slot (stable, so ties stay in id order), cut at int(fraction * num)."""
+    out = {}
+    for arg, col, num in (("subject", 0, num_entities), ("relation", 1, num_relations), ("object", 2, num_entities)):
+        freq = [0] * num
+        for x in train[:, col].tolist():
+            freq[x] += 1
+        order = [i for i, _ in sorted(enumerate(freq), key=lambda x: x[1])]
+        out[arg] = {name: set(order[int(b * num):int(e * num)]) for name, b, e in PERCENTILES}
+    return out
+
+
+def grouped_histograms(ranks_s, ranks_o, triples, num_entities, head_and_tail=False, rel_types=None,
+                       freq_percs=None) -> Dict[str, np.ndarray]:
+    """The histogram hooks of the evaluation job for one ranking: hist_all, hist_per_relation_type
+    and hist_per_frequency_percentile (eval.py:148-224).  Returns key -> rank histogram in the
+    reference's key order; ranks_s rank the subject of (?, p, o), ranks_o the object of (s, p, ?)."""
+    E = num_entities
+    s, p, o = (triples[:, i] for i in range(3))
+
+    def hist(ranks, mask=None):
+        r = ranks if mask is None else ranks[mask]
+        return np.bincount(r, minlength=E)[:E].astype(np.float32)
+
+    h = {"all": hist(ranks_o) + hist(ranks_s)}
+    if head_and_tail:
+        h["head"], h["tail"] = hist(ranks_s), hist(ranks_o)
+    if rel_types is not None:
+        for t, rels in relations_per_type(rel_types).items():
+            m = np.array([int(x) in rels for x in p], bool)
+            h[t] = hist(ranks_o, m) + hist(ranks_s, m)
+            if head_and_tail:
+                h[t + "_head"], h[t + "_tail"] = hist(ranks_s, m), hist(ranks_o, m)
+    if freq_percs is not None:
+        def member(arg, perc, ids):
+            return np.array([int(x) in freq_percs[arg][perc] for x in ids], bool)
+
+        for arg in ("subject", "relation", "object"):
+            for perc, _, _ in PERCENTILES:
+                if arg == "subject":
+                    h[f"{arg}_{perc}"] = hist(ranks_s, member(arg, perc, s))
+                elif arg == "object":
+                    h[f"{arg}_{perc}"] = hist(ranks_o, member(arg, perc, o))
+                else:
+                    m = member(arg, perc, p)
+                    h[f"{arg}_{perc}"] = hist(ranks_s, m) + hist(ranks_o, m)
+    return h
+
+
 def entity_ranking(model, ent, rel, splits: Dict[str, np.ndarray], eval_split="valid",
                    filter_splits=("train", "valid"), filter_with_test=True,
                    batch_size=100, chunk_size=-1, tie_handling="rounded_mean_rank",
                    hits_at_k_s=(1, 3, 10, 50, 100, 200, 300, 400, 500, 1000),
-                   l_norm=1.0, score_dtype=np.float32):
+                   l_norm=1.0, score_dtype=np.float32, head_and_tail=False, relation_type=False,
+                   argument_frequency=False):
     """EntityRankingJob._run (entity_ranking.py:79-426), hist_all (eval.py:148-171).
 
     Scores are computed in float64 and rounded to ``score_dtype``; true scores come
@@ -494,9 +579,15 @@ def entity_ranking(model, ent, rel, splits: Dict[str, np.ndarray], eval_split="v
     ranks = {k: np.concatenate(v) for k, v in out.items()}
     metrics = {}
     names = {"_raw": "", "_filt": "_filtered", "_filt_test": "_filtered_with_test"}
-    for r in rankings:
-        hist = np.bincount(np.concatenate([ranks["o" + r], ranks["s" + r]]), minlength=E)
-        metrics.update(compute_metrics(hist[:E], hits_at_k_s, names[r]))
+    R = rel.shape[0]
+    types = relation_types(splits["train"], R) if relation_type else None
+    percs = frequency_percentiles(splits["train"], E, R) if argument_frequency else None
+    grouped = {r: grouped_histograms(ranks["s" + r], ranks["o" + r], triples, E, head_and_tail, types, percs)
+               for r in rankings}
+    for key in grouped["_raw"]:  # entity_ranking.py:376-387: per key, every ranking
+        for r in rankings:
+            metrics.update(compute_metrics(grouped[r][key], hits_at_k_s,
+                                           names[r] + ("_" + key if key != "all" else "")))
     return ranks, metrics
 
 

@@ -7,7 +7,7 @@ reference's outputs as ``.npz`` fixtures next to this file.  Only data is writte
 reference source text is copied.  The committed fixtures are what ``tests/`` and the
 oracle are pinned against.
 
-Import shims (SURVEY.md App. A).  The reference imports four things this image lacks
+Import shims.  The reference imports four things this image lacks
 or that changed in Python 3.10; none of them is on the scoring path:
 
 * ``numba`` -- ``njit`` becomes the identity (used by kge/indexing.py:304-317 and
@@ -16,7 +16,7 @@ or that changed in Python 3.10; none of them is on the scoring path:
 * ``ax*`` -- empty modules (kge/job/ax_search.py:3-9 only);
 * ``collections.Mapping`` -- aliased to ``collections.abc.Mapping`` (kge/config.py:56).
 
-Fixtures written (see tests/golden/README.md for the schema):
+Fixtures written:
 
 * ``scorer_<model>_<regime>.npz`` -- F1: embedding tables, index vectors and the
   outputs of score_spo / score_sp / score_po / score_sp_po (all and subset) for
@@ -42,7 +42,11 @@ Fixtures written (see tests/golden/README.md for the schema):
   BASELINE config words them (1vsAll, dim 128, Adagrad 0.2, ReduceLROnPlateau, lp penalty
   0.8e-7, N(0, 0.1)) run through the reference's TrainingJob._run on a small synthetic
   dataset with the batch order recorded: per-epoch loss / penalty / lr and every validation;
-* ``score_so.npz`` -- the "s_o" combine (KgeModel.score_so, all relations and a subset).
+* ``score_so.npz`` -- the "s_o" combine (KgeModel.score_so, all relations and a subset);
+* ``eval_metrics_per.npz`` -- the reference EntityRankingJob with every entity_ranking.metrics_per
+  option on (head_and_tail, relation_type, argument_frequency) over a synthetic dataset whose
+  relations cover all four cardinality classes: every metric of the epoch trace, and the
+  reference's relation_types / frequency_percentiles indexes.
 
 Run:  PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden.py [case,case,...]
 """
@@ -644,6 +648,66 @@ def gen_score_so_fixture():
     return fn
 
 
+def typed_triples(rng, E, R, n):
+    """Unique triples whose relations differ in cardinality: relation r draws its subjects from
+    the first ns[r % 4] entities and its objects from the first no[r % 4] (few subjects and many
+    objects gives 1-N, and so on), and relation ids are skewed so that frequencies differ."""
+    ns = (12, E, 40, E)
+    no = (E, 12, 40, E)
+    wr = 1.0 / np.arange(1, R + 1) ** 0.8
+    wr /= wr.sum()
+    seen, out = set(), []
+    while len(out) < n:
+        p = int(rng.choice(R, p=wr))
+        s = int(rng.integers(ns[p % 4]))
+        o = int(rng.integers(no[p % 4]))
+        if (s, p, o) not in seen:
+            seen.add((s, p, o))
+            out.append((s, p, o))
+    return np.array(out, dtype=np.int64)
+
+
+def gen_eval_metrics_per():
+    from kge.job import EvaluationJob
+
+    E, R, dim = 300, 12, 32
+    rng = np.random.default_rng(11)
+    allt = typed_triples(rng, E, R, 3300)
+    splits = dict(train=allt[:3000], valid=allt[3000:3150], test=allt[3150:])
+    folder = os.path.join(TMP, "ds_eval_metrics_per")
+    write_dataset(folder, E, R, splits)
+    gen = torch.Generator().manual_seed(13)
+    ent = torch.randn(E, dim, generator=gen) * 0.1
+    rel = torch.randn(R, dim, generator=gen) * 0.1
+    config = ds_config("complex", dim, folder, E, R)
+    config.set("eval.batch_size", 64)
+    config.set("eval.split", "valid")
+    config.set("entity_ranking.filter_splits", ["train", "valid"])
+    config.set("entity_ranking.filter_with_test", True)
+    for k in ("head_and_tail", "relation_type", "argument_frequency"):
+        config.set("entity_ranking.metrics_per." + k, True)
+    ds = Dataset.create(config, folder=folder)
+    model = KgeModel.create(config, ds)
+    set_tables(model, ent, rel)
+    job = EvaluationJob.create(config, ds, model=model)
+    trace = job.run()
+    metrics = {k: v for k, v in trace.items() if isinstance(v, (int, float)) and ("rank" in k or "hits" in k)}
+    ds.index("frequency_percentiles")
+    percs = {arg: {perc: sorted(int(i) for i in ids) for perc, ids in d.items()}
+             for arg, d in ds._indexes["frequency_percentiles"].items()}
+    out = dict(ent=ent.numpy(), rel=rel.numpy(), **{f"tri_{k}": v for k, v in splits.items()},
+               metrics=np.array(json.dumps(metrics)), metric_order=np.array(json.dumps(list(metrics))),
+               relation_types=np.array(json.dumps(list(ds.index("relation_types")))),
+               frequency_percentiles=np.array(json.dumps(percs)),
+               meta=np.array(json.dumps(dict(
+                   E=E, R=R, dim=dim, model="complex", eval_split="valid", filter_splits=["train", "valid"],
+                   filter_with_test=True, batch_size=64, tie_handling="rounded_mean_rank",
+                   torch=torch.__version__))))
+    fn = os.path.join(OUT, "eval_metrics_per.npz")
+    np.savez_compressed(fn, **out)
+    return fn
+
+
 def gen_shapes():
     rows = []
     for model, d in [("rotate", 64), ("rotate", 1024), ("rescal", 16), ("rescal", 32),
@@ -674,7 +738,7 @@ def main():
         written.append(gen_shapes())
     extra = {"eval_fullsize": gen_eval_fullsize, "kvsall": gen_kvsall_fixture,
              "ns_rotate": lambda: gen_ns_fixture("rotate"), "ns_complex": lambda: gen_ns_fixture("complex"),
-             "toy": gen_toy_fixture, "score_so": gen_score_so_fixture}
+             "toy": gen_toy_fixture, "score_so": gen_score_so_fixture, "eval_metrics_per": gen_eval_metrics_per}
     for name, fn in extra.items():
         if only is None or name in only:
             written.append(fn())

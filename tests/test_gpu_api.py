@@ -137,7 +137,7 @@ def test_fused_xent_matches_unfused(fn, prec):
     assert np.abs(gr1 - gr0).max() <= tol * np.abs(gr0).max()
 
 
-def eval_job(f, tag, precision):
+def eval_job(f, tag, precision, extra=None):
     from kge import Config, Dataset
     from kge.job import EntityRankingJob
 
@@ -154,6 +154,8 @@ def eval_job(f, tag, precision):
     c.set("entity_ranking.chunk_size", -1 if tag == "full" else meta["chunk8"])
     c.set("dataset.num_entities", meta["E"])
     c.set("dataset.num_relations", meta["R"])
+    for k, v in (extra or {}).items():
+        c.set(k, v)
     ds = Dataset(c, None)
     ds._triples = {k: torch.from_numpy(f["tri_" + k].astype(np.int32)) for k in ("train", "valid", "test")}
     m = make_model("complex", meta["dim"], meta["E"], meta["R"], f["ent"], f["rel"],
@@ -175,6 +177,30 @@ def test_entity_ranking_vs_golden(regime, precision, tag):
     job, trace = eval_job(f, tag, precision)
     for k, v in job.ranks.items():
         np.testing.assert_array_equal(v, f[f"{tag}_{k}"], err_msg=k)
+    for k, v in ref_metrics.items():
+        assert trace[k] == pytest.approx(v, rel=1e-6, abs=1e-9), k
+
+
+@pytest.mark.parametrize("tag", ["full", "chunk8"])
+def test_entity_ranking_metrics_per_group_vs_golden(tag):
+    """entity_ranking.metrics_per.{head_and_tail, relation_type, argument_frequency}: the
+    dataset's relation classes and frequency quartiles and every metric of the reference's
+    epoch trace (729 of them), in the reference's order, unchunked and in 8 entity chunks."""
+    f = np.load(os.path.join(GOLDEN, "eval_metrics_per.npz"))
+    f = dict(f)
+    meta = json.loads(str(f["meta"]))
+    meta["chunk8"] = -(-meta["E"] // 8)
+    f["meta"] = np.array(json.dumps(meta))
+    job, trace = eval_job(f, tag, "bf16x3_refined",
+                          {"entity_ranking.metrics_per." + k: True
+                           for k in ("head_and_tail", "relation_type", "argument_frequency")})
+    assert job.dataset.index("relation_types") == json.loads(str(f["relation_types"]))
+    percs = job.dataset.index("frequency_percentiles")
+    assert {a: {q: sorted(v) for q, v in d.items()} for a, d in percs.items()} == json.loads(
+        str(f["frequency_percentiles"]))
+    ref_metrics = json.loads(str(f["metrics"]))
+    order = json.loads(str(f["metric_order"]))
+    assert [k for k in trace if k in ref_metrics] == order
     for k, v in ref_metrics.items():
         assert trace[k] == pytest.approx(v, rel=1e-6, abs=1e-9), k
 

@@ -1,4 +1,4 @@
-"""GPU parity of the negative-sampling path:
+"""GPU parity of the negative-sampling path (RotatE-1024 with 1,024 negatives at FB15K-237 size included):
 
 * kge_score_cand (+ backward) against the oracle's score_spo semantics on the expanded
   B x (1 + N) triples, for all five scorers, both corrupted slots, duplicate candidates;

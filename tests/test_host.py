@@ -193,3 +193,40 @@ def test_kvsall_batch_queries_host_csr():
             key = tuple(q[i].tolist())
             got = sorted(l_col[int(l_ptr[i]):int(l_ptr[i + 1])].tolist())
             assert got == sorted(answers[qi][key]), (qi, key)
+
+
+def test_dataset_relation_types_and_frequency_percentiles():
+    """Dataset.index("relation_types" / "relations_per_type" / "frequency_percentiles") against the
+    reference's own indexes (captured in eval_metrics_per.npz) and against the oracle's loops on a
+    set with duplicate triples, an unused relation and unused entities."""
+    import json
+
+    from kge import Config, Dataset
+    from oracle import kge_oracle as K
+
+    f = np.load(os.path.join(os.path.dirname(__file__), "golden", "eval_metrics_per.npz"))
+    meta = json.loads(str(f["meta"]))
+
+    def dataset(train, E, R):
+        c = Config()
+        c.set("dataset.num_entities", E)
+        c.set("dataset.num_relations", R)
+        ds = Dataset(c, None)
+        ds._triples = {"train": torch.from_numpy(train.astype(np.int32))}
+        return ds
+
+    ds = dataset(f["tri_train"], meta["E"], meta["R"])
+    assert ds.index("relation_types") == json.loads(str(f["relation_types"]))
+    got = {a: {q: sorted(v) for q, v in d.items()} for a, d in ds.index("frequency_percentiles").items()}
+    assert got == json.loads(str(f["frequency_percentiles"]))
+    assert list(ds.index("relations_per_type")) == ["M-N", "1-N", "M-1", "1-1"]
+
+    rng = np.random.default_rng(3)
+    E, R = 57, 7
+    t = np.stack([rng.integers(0, 50, 400), rng.integers(0, R - 1, 400), rng.integers(0, 9, 400)], 1)
+    t = np.concatenate([t, t[:60]])  # duplicates count in both indexes
+    ds = dataset(t, E, R)
+    types = K.relation_types(t, R)
+    assert ds.index("relation_types") == types and types[R - 1] == "1-1"
+    assert ds.index("relations_per_type") == K.relations_per_type(types)
+    assert ds.index("frequency_percentiles") == K.frequency_percentiles(t, E, R)

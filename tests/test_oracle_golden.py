@@ -67,6 +67,25 @@ def test_entity_ranking(regime, tag):
         assert v == pytest.approx(ref_metrics[k], rel=1e-6, abs=1e-9), k
 
 
+def test_entity_ranking_metrics_per_group():
+    """Every entity_ranking.metrics_per breakdown of the reference job: the relation classes, the
+    frequency quartiles and all 729 metrics of the epoch trace, in the reference's key order."""
+    f = np.load(os.path.join(GOLDEN, "eval_metrics_per.npz"))
+    meta = json.loads(str(f["meta"]))
+    splits = {k: f["tri_" + k] for k in ("train", "valid", "test")}
+    assert K.relation_types(splits["train"], meta["R"]) == json.loads(str(f["relation_types"]))
+    assert set(json.loads(str(f["relation_types"]))) == {"1-1", "1-N", "M-1", "M-N"}
+    percs = K.frequency_percentiles(splits["train"], meta["E"], meta["R"])
+    ref_percs = json.loads(str(f["frequency_percentiles"]))
+    assert {a: {q: sorted(v) for q, v in d.items()} for a, d in percs.items()} == ref_percs
+    _, metrics = K.entity_ranking("complex", f["ent"], f["rel"], splits, batch_size=meta["batch_size"],
+                                  head_and_tail=True, relation_type=True, argument_frequency=True)
+    ref_metrics = json.loads(str(f["metrics"]))
+    assert list(metrics) == json.loads(str(f["metric_order"]))
+    for k, v in metrics.items():
+        assert v == pytest.approx(ref_metrics[k], rel=1e-6, abs=1e-9), k
+
+
 def test_train_1vsall():
     f = np.load(os.path.join(GOLDEN, "train1vsall_complex.npz"))
     losses, e1, r1 = K.train_1vsall("complex", f["ent0"], f["rel0"], f["batches"], lr=0.2)

@@ -2,7 +2,7 @@
 ops the reference composes them from -- CrossEntropyLoss / KLDivLoss(log_softmax,
 normalize(labels, p=1)) with reduction "sum" (kge/util/loss.py:192-213), label smoothing
 as in kge/job/train.py:715-721.  torch is the reference's own third-party dependency for
-this arithmetic (SURVEY.md 8c), so this pins the restatement."""
+this arithmetic, so this pins the restatement."""
 import numpy as np
 import pytest
 import torch

@@ -113,6 +113,8 @@ def _worker(rank, world, port, out_q):
         lo, hi = job._sharded.lo, job._sharded.hi
         state_rows = [tuple(st["sum"].shape) for st in job.optimizer.state.values()]
         job._sharded.sync_model()
+        for k in ("head_and_tail", "relation_type", "argument_frequency"):
+            c.set("entity_ranking.metrics_per." + k, True)
         ev = EntityRankingJob(c, ds, model=job.model)
         ev.sharded_ops = JobOps()
         ev.capture_ranks = True
@@ -183,7 +185,9 @@ def test_sharded_training_and_eval_jobs_world2_match_unsharded():
         np.testing.assert_allclose(rel, ref_rel, atol=2e-5)
     # the sharded evaluation job on the trained model vs the oracle on the same tables
     oranks, ometrics = K.entity_ranking("complex", res[0][6].astype(np.float64), res[0][7].astype(np.float64),
-                                        splits, eval_split="valid", filter_splits=("train", "valid"), batch_size=7)
+                                        splits, eval_split="valid", filter_splits=("train", "valid"), batch_size=7,
+                                        head_and_tail=True, relation_type=True, argument_frequency=True)
+    assert any(k.endswith("_object_top") for k in ometrics) and any(k.endswith("_tail") for k in ometrics)
     for rank, *_, ranks, metrics in res:
         assert set(ranks) == set(oranks)
         for k, v in oranks.items():
