@@ -120,6 +120,45 @@ def kernel_time_ms(kern, reps=100, settle=20):
     return a.elapsed_time(b) / reps
 
 
+def machine_ceilings(device):
+    """What this GPU sustains on the two roofline axes, measured with libkgeprobe.so (built next
+    to the scoring library): a 1-GiB streaming copy and register-resident 16x16x32 bf16 MFMA
+    chains on every SIMD -- with zero operands (little power: the clock stays up) and with random
+    operands (the power limit sets the clock), 2-ms launches and a sustained 25-ms launch.  None
+    when the probe library is not built."""
+    import ctypes
+
+    path = os.path.join(ROOT, "kge-1_amd", "kge", "libkgeprobe.so")
+    if not os.path.exists(path):
+        return None
+    lib = ctypes.CDLL(path)
+    lib.kge_probe_copy.restype = ctypes.c_int
+    lib.kge_probe_copy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p]
+    lib.kge_probe_mfma.restype = ctypes.c_int64
+    lib.kge_probe_mfma.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p]
+    stream = torch.cuda.current_stream(device).cuda_stream
+    nbytes = 1 << 30
+    src = torch.empty(nbytes // 4, device=device).normal_()
+    dst = torch.empty_like(src)
+    copy_ms = kernel_time_ms(lambda: lib.kge_probe_copy(dst.data_ptr(), src.data_ptr(), nbytes, stream), reps=10,
+                             settle=2)
+    del src, dst
+    out = torch.empty(lib.kge_probe_cus() * 512, device=device)
+    res = {"hbm_copy_GBs": round(2 * nbytes / (copy_ms / 1e3) / 1e9, 1), "hbm_copy_bytes": 2 * nbytes}
+    for name, iters, random, reps, settle in (("mfma_bf16_zero_operands", 8000, 0, 10, 3),
+                                              ("mfma_bf16_random_operands", 8000, 1, 10, 3),
+                                              ("mfma_bf16_random_operands_25ms", 100000, 1, 2, 1)):
+        flops = []
+        ms = kernel_time_ms(lambda: flops.append(lib.kge_probe_mfma(iters, random, out.data_ptr(), out.numel(),
+                                                                    stream)), reps=reps, settle=settle)
+        if not flops or flops[-1] <= 0:
+            return None
+        res[name + "_TFLOPs"] = round(flops[-1] / (ms / 1e3) / 1e12, 1)
+    res["what"] = ("libkgeprobe.so: 1-GiB float4 copy (read + write bytes); v_mfma_f32_16x16x32_bf16 from registers, "
+                   "two waves per SIMD, 8 independent accumulators per wave, no LDS or memory in the loop")
+    return res
+
+
 # --------------------------------------------------------------------------------- CPU baseline
 
 
@@ -336,6 +375,16 @@ def main():
                 "alg_bytes_per_launch": int(alg_bytes), "alg_flops_per_launch": int(alg_flops), "note": note,
                 "exact_fp32_kernel_us": round(k32_ms * 1e3, 2),
                 "exact_fp32_kernel_frac_of_fp32_mfma_peak": round(alg_flops / (k32_ms / 1e3) / 1e12 / FP32_MFMA_TFLOPS, 4)}
+
+    if world == 1:
+        ceil = machine_ceilings(device)
+        if ceil is not None:
+            roofline["measured_ceilings"] = ceil
+            if args.precision == "bf16x3":
+                # the same three-pass bf16 work against what the MFMA pipes sustain on random data
+                roofline["frac_of_measured_mfma_random"] = round(
+                    3.0 * achieved / ceil["mfma_bf16_random_operands_TFLOPs"], 4)
+            roofline["hbm_frac_of_measured_copy"] = round(alg_bytes / k_s / 1e9 / ceil["hbm_copy_GBs"], 4)
 
     value = scored_per_step / sec
     out = {"metric": "1vsAll scored triples/sec (score_sp, ComplEx-512, FB15K-237 shape, B=1024 per GPU)",

@@ -34,7 +34,9 @@ struct PCfg {
 // ABL: dev-only ablation / probe switches (kge_dev_score_dot_persist): 1 = no score stores,
 // 2 = no staging after the prologue, 4 = per-workgroup clock probe written to row n of s,
 // 8 = no barrier inside the K loop (timing only: the waves race on the LDS image).
-template <int BM, int BN, int WM, int WN, int ABL = 0>
+// PIPE: the K loop software-pipelined inside each wave (see the loop): same barriers, same
+// in-flight counts, same MFMA order per accumulator (bit-identical scores).
+template <int BM, int BN, int WM, int WN, int ABL = 0, bool PIPE = false>
 __global__ void __launch_bounds__(64 * WM * WN, 1)
     score_dot_persist16_kernel(const __bf16* __restrict__ qhi, const __bf16* __restrict__ qlo, int64_t ldq,
                                const float* __restrict__ t, int64_t ldt, const int64_t* __restrict__ tidx, int n,
@@ -91,7 +93,7 @@ __global__ void __launch_bounds__(64 * WM * WN, 1)
       const int row = min((tid >> 3) + i * (C::NT / 8), BN - 1);
       const int ej = n0 + row;  // rows past m read row 0: their scores are never stored
       const int64_t er = ej < m ? (tidx ? tidx[ej] : (int64_t)ej) : 0;
-      b_src[i] = t + er * ldt + b_col;
+      b_src[i] = t + ((ABL & 64) ? (er & 63) : er) * ldt + b_col;  // dev 64: every panel reads rows 0 .. 63
     }
     u32x4 rv[C::B_PER_T];
 
@@ -193,6 +195,85 @@ __global__ void __launch_bounds__(64 * WM * WN, 1)
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
+    if constexpr (PIPE) {
+      // Inside a wave nothing but the matrix pipe should ever be waited for, so every LDS read
+      // is issued a band (12 MFMAs) before its use: band x + 1's A fragments while band x runs,
+      // and across the barrier the last band of a stage is held back -- its operands are in
+      // registers -- and runs while the next stage's first fragments are fetched (each B
+      // fragment is replaced as soon as the held band has used it).  The split of the entity
+      // rows is spread, one float4 slot at a time, over the bands from XS on, each slot's
+      // register load for stage st + 2 issued right behind it.
+      static_assert(TM >= 4 && TM % 2 == 0 && !B_RAGGED && (ABL & 8) == 0, "band pipeline");
+      constexpr int PXS = TM >= 8 ? 2 : 1;      // first band that stages
+      constexpr int PNB = TM - 1 - PXS;         // bands that stage
+      bf16x8 ah[2], al[2];
+      auto read_a = [&](const unsigned char* stg, int x, int slot) {
+        const int ra = wr * (BM / WM) + x * 16 + fr;
+        ah[slot] = *reinterpret_cast<const bf16x8*>(stg + sw16_off(ra, fs));
+        al[slot] = *reinterpret_cast<const bf16x8*>(stg + C::PLANE_A + sw16_off(ra, fs));
+      };
+      auto read_b = [&](const unsigned char* stg, int y) {
+        const int rb_ = wc * WCOLS + y * 16 + fr;
+        b_h[y] = *reinterpret_cast<const bf16x8*>(stg + 2 * C::PLANE_A + sw16_off(rb_, fs));
+        b_l[y] = *reinterpret_cast<const bf16x8*>(stg + 2 * C::PLANE_A + C::PLANE_B + sw16_off(rb_, fs));
+      };
+      auto mfma3 = [&](int x, int y, int slot) {
+        acc[x][y] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al[slot], b_h[y], acc[x][y], 0, 0, 0);
+        acc[x][y] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[slot], b_l[y], acc[x][y], 0, 0, 0);
+        acc[x][y] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[slot], b_h[y], acc[x][y], 0, 0, 0);
+      };
+      // same issue order as at the end of the loop body: the waits at the loop head then only
+      // cover what the first MFMAs need
+      read_a(smem, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int y = 0; y < TN; ++y) {
+        read_b(smem, y);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      for (int st = 0; st < nst; ++st) {
+        const int nb = (st + 1) & 1;
+        const unsigned char* cur = smem + (st & 1) * C::STAGE;
+        unsigned char* nxt = smem + nb * C::STAGE;
+        const int k1 = min(st + 1, nst - 1) * BK;
+        const int koff = min(min(st + 2, nst - 1) * BK, d - 4 - b_col);
+        const unsigned mk = (k1 + b_col < d) ? 0xffffffffu : 0u;  // zero past the K tail
+        // dev ablations (timing only): 2 = no staging at all, 16 = no A DMA, 32 = no B staging
+        if constexpr (!(ABL & (2 | 16))) glds_a(nb, k1);
+#pragma unroll
+        for (int x = 0; x < TM - 1; ++x) {
+          read_a(cur, x + 1, (x + 1) & 1);
+          if (x == PXS && !(ABL & (2 | 32))) KGE_WAIT_VM((ABL & 16) ? 0 : 2 * A_G);  // B(st + 1) has landed
+#pragma unroll
+          for (int i = 0; i < C::B_PER_T; ++i) {
+            if (PXS + i * PNB / C::B_PER_T != x || (ABL & (2 | 32))) continue;
+            const float4 v = make_float4(__uint_as_float(rv[i].x & mk), __uint_as_float(rv[i].y & mk),
+                                         __uint_as_float(rv[i].z & mk), __uint_as_float(rv[i].w & mk));
+            bf16x4 h, l;
+            split_bf16x4_pk(v, h, l);
+            *reinterpret_cast<bf16x4*>(nxt + 2 * C::PLANE_A + b_off0 + i * (C::NT / 8) * 64) = h;
+            *reinterpret_cast<bf16x4*>(nxt + 2 * C::PLANE_A + C::PLANE_B + b_off0 + i * (C::NT / 8) * 64) = l;
+            rv[i] = gload16_asm(b_src[i] + koff);
+          }
+#pragma unroll
+          for (int y = 0; y < TN; ++y) mfma3(x, y, x & 1);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+        KGE_WAIT_VM((ABL & 32) ? 0 : C::B_PER_T);  // A(st + 1) has landed
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        read_a(nxt, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int y = 0; y < TN; ++y) {
+          mfma3(TM - 1, y, (TM - 1) & 1);
+          __builtin_amdgcn_sched_barrier(0);
+          read_b(nxt, y);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      }
+    } else
     // One barrier per stage.  Stage st + 1 is staged into the other buffer between the first
     // XS bands of stage st's MFMAs and the rest (measured: 8 % over staging ahead of them).
     // The stage body is branch-free: the last stage re-stages its own K chunk into the idle
@@ -261,7 +342,7 @@ __global__ void __launch_bounds__(64 * WM * WN, 1)
   }
 }
 
-template <int BM, int BN, int WM, int WN, int ABL = 0>
+template <int BM, int BN, int WM, int WN, int ABL = 0, bool PIPE = false>
 int launch_persist16(const __bf16* qhi, const __bf16* qlo, int64_t ldq, const float* t, int64_t ldt,
                      const int64_t* tidx, int64_t n, int64_t m, int d, float* s, int64_t lds, hipStream_t st) {
   using C = PCfg<BM, BN, WM, WN>;
@@ -270,12 +351,12 @@ int launch_persist16(const __bf16* qhi, const __bf16* qlo, int64_t ldq, const fl
   if (ntiles > 0x7fffffff) return KGE_ERR_ARG;
   const size_t shmem = 2 * C::STAGE;
   static std::atomic<bool> lds_ok[KGE_MAX_DEVICES];
-  if (const int e = kge_allow_lds((const void*)score_dot_persist16_kernel<BM, BN, WM, WN, ABL>, (int)shmem, lds_ok))
+  if (const int e = kge_allow_lds((const void*)score_dot_persist16_kernel<BM, BN, WM, WN, ABL, PIPE>, (int)shmem, lds_ok))
     return e;
   int grid = kge_num_cus();
   grid = (int)std::min<int64_t>(grid, (ntiles + 7) / 8 * 8);
   grid = std::max(8, grid / 8 * 8);
-  score_dot_persist16_kernel<BM, BN, WM, WN, ABL><<<dim3(grid), dim3(C::NT), shmem, st>>>(
+  score_dot_persist16_kernel<BM, BN, WM, WN, ABL, PIPE><<<dim3(grid), dim3(C::NT), shmem, st>>>(
       qhi, qlo, ldq, t, ldt, tidx, (int)n, (int)m, d, s, lds, nrt, (int)ntiles);
   KGE_CHECK_LAUNCH();
   return 0;
@@ -318,8 +399,8 @@ extern "C" int kge_score_dot_split(const void* qhi, const void* qlo, int64_t ldq
   hipStream_t st = as_stream(stream);
   const __bf16* h = (const __bf16*)qhi;
   const __bf16* l = (const __bf16*)qlo;
-  if (n > 128) return launch_persist16<256, 256, 2, 4>(h, l, ldq, t, ldt, tidx, n, m, d, s, lds, st);
-  return launch_persist16<128, 256, 2, 4>(h, l, ldq, t, ldt, tidx, n, m, d, s, lds, st);
+  if (n > 128) return launch_persist16<256, 256, 2, 4, 0, true>(h, l, ldq, t, ldt, tidx, n, m, d, s, lds, st);
+  return launch_persist16<128, 256, 2, 4, 0, true>(h, l, ldq, t, ldt, tidx, n, m, d, s, lds, st);
 }
 
 #ifdef KGE_DEV_BUILD  // libkgescore_dev.so only: ablation / probe variants for scripts/dev
@@ -343,6 +424,19 @@ extern "C" int kge_dev_score_dot_persist(int variant, const void* qhi, const voi
     // one wave per SIMD, 128 x 128 wave tiles (accumulators in AGPRs)
     case 20: return launch_persist16<256, 256, 2, 2>(h, l, ldq, t, ldt, tidx, n, m, d, s, lds, st);
     case 24: return launch_persist16<256, 256, 2, 2, 4>(h, l, ldq, t, ldt, tidx, n, m, d, s, lds, st);
+    // K loop software-pipelined inside each wave
+    case 30: return launch_persist16<256, 256, 2, 4, 0, true>(h, l, ldq, t, ldt, tidx, n, m, d, s, lds, st);
+    case 31: return launch_persist16<128, 256, 2, 4, 0, true>(h, l, ldq, t, ldt, tidx, n, m, d, s, lds, st);
+    case 34: return launch_persist16<256, 256, 2, 4, 4, true>(h, l, ldq, t, ldt, tidx, n, m, d, s, lds, st);
+    // one wave per SIMD, 128 x 128 wave tiles, pipelined
+    case 35: return launch_persist16<256, 256, 2, 2, 0, true>(h, l, ldq, t, ldt, tidx, n, m, d, s, lds, st);
+    case 36: return launch_persist16<256, 256, 2, 2, 4, true>(h, l, ldq, t, ldt, tidx, n, m, d, s, lds, st);
+    case 41: return launch_persist16<256, 256, 2, 4, 1, true>(h, l, ldq, t, ldt, tidx, n, m, d, s, lds, st);
+    case 42: return launch_persist16<256, 256, 2, 4, 2, true>(h, l, ldq, t, ldt, tidx, n, m, d, s, lds, st);
+    case 43: return launch_persist16<256, 256, 2, 4, 3, true>(h, l, ldq, t, ldt, tidx, n, m, d, s, lds, st);
+    case 44: return launch_persist16<256, 256, 2, 4, 16, true>(h, l, ldq, t, ldt, tidx, n, m, d, s, lds, st);
+    case 45: return launch_persist16<256, 256, 2, 4, 32, true>(h, l, ldq, t, ldt, tidx, n, m, d, s, lds, st);
+    case 46: return launch_persist16<256, 256, 2, 4, 64, true>(h, l, ldq, t, ldt, tidx, n, m, d, s, lds, st);
     default: return KGE_ERR_ARG;
   }
 }

@@ -54,7 +54,10 @@ for v in variants:
     o = outa if v.endswith('a') else out
     o.zero_(); run(v); torch.cuda.synchronize()
     err = ((o.double() - ref).abs().amax(1) / ref.abs().amax(1)).max().item()
-    print(f"variant {v}: max rel err {err:.2e}", flush=True)
+    if v == variants[0]:
+        first = o.clone()
+    same = bool((o == first).all().item()) if o.shape == first.shape else None
+    print(f"variant {v}: max rel err {err:.2e}  bit-identical to {variants[0]}: {same}", flush=True)
 for rnd in range(5):
     for v in variants:
         for _ in range(3): run(v)

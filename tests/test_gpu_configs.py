@@ -248,10 +248,12 @@ def test_eval_precision_is_applied_and_restored():
         EntityRankingJob(c, ds, model=KgeModel.create(c, ds)).run()
 
 
-def test_metrics_per_head_and_tail_and_unimplemented_keys():
+def test_metrics_per_head_and_tail_and_group_keys():
     """entity_ranking.metrics_per.head_and_tail: the head (subject) and tail (object)
     histograms of eval.py:125-146 -- checked against the metrics recomputed from the
-    reference-captured per-direction ranks; the other metrics_per keys raise."""
+    reference-captured per-direction ranks; each of the other metrics_per keys adds its
+    groups' metrics, whose query counts add up to the ungrouped ones (the reference-pinned
+    values are checked in test_gpu_api.test_entity_ranking_metrics_per_group_vs_golden)."""
     from kge import KgeModel
     from kge.job import EntityRankingJob
 
@@ -271,10 +273,24 @@ def test_metrics_per_head_and_tail_and_unimplemented_keys():
             assert trace[f"mean_reciprocal_rank{suffix}_{slot}"] == pytest.approx((1 / (r + 1)).mean(), rel=1e-5)
             assert trace[f"hits_at_10{suffix}_{slot}"] == pytest.approx((r < 10).mean(), abs=1e-7)
     assert E > 10
-    for key in ("relation_type", "argument_frequency"):
-        c2 = base_config("complex", meta["dim"], meta["E"], meta["R"], {"entity_ranking.metrics_per." + key: True})
-        with pytest.raises(NotImplementedError):
-            EntityRankingJob(c2, ds, model=model)
+    n_q = 2 * len(f["tri_valid"])
+    for key, groups in (("relation_type", ds.index("relations_per_type")),
+                        ("argument_frequency", ["relation_" + q for q in ("25%", "50%", "75%", "top")])):
+        c2 = base_config("complex", meta["dim"], meta["E"], meta["R"],
+                         {"eval.batch_size": meta["batch_size"], "entity_ranking.metrics_per." + key: True})
+        t2 = EntityRankingJob(c2, ds, model=model).run()
+        assert t2["mean_rank_filtered"] == trace["mean_rank_filtered"]
+        # mean rank is a per-group average: weighting by the group sizes gives the overall mean back
+        sizes = {}
+        p = f["tri_valid"][:, 1]
+        for g in groups:
+            if key == "relation_type":
+                sizes[g] = 2 * int(np.isin(p, list(ds.index("relations_per_type")[g])).sum())
+            else:
+                sizes[g] = 2 * int(np.isin(p, list(ds.index("frequency_percentiles")["relation"][g[9:]])).sum())
+        assert sum(sizes.values()) == n_q
+        total = sum(t2[f"mean_rank_filtered_{g}"] * k for g, k in sizes.items())
+        assert total / n_q == pytest.approx(trace["mean_rank_filtered"], rel=1e-5)
 
 
 # ------------------------------------------------------------------------------ C1 toy
