@@ -79,6 +79,7 @@ __device__ __forceinline__ void store_tile(const f32x4 (&acc)[TM][TN], unsigned 
 // ---------------------------------------------------------------------------------------
 // dQ partial slabs: slab[z][i][j] = sum_{e in K chunk z} G[i, e] * T[e, j]
 // ghi / glo: G planes, row stride ldgp (bf16 elements), columns [K, round_up(K, 32)) zero.
+template <bool PIPE>
 __global__ void __launch_bounds__(NT, 1)
     bwd3p_q_kernel(const __bf16* __restrict__ ghi, const __bf16* __restrict__ glo, int64_t ldgp,
                    const float* __restrict__ t, int64_t ldt, int n, int N, int K, int kchunk, int nrt, int nct,
@@ -200,6 +201,67 @@ __global__ void __launch_bounds__(NT, 1)
   // One barrier per stage; the stage body is branch-free (the last stage re-stages its own K
   // chunk into the idle buffer) so that every path keeps the same in-flight counts: per stage a
   // wave issues 2 A_G DMAs (stage st + 1), then 2 register loads (stage st + 2).
+  if constexpr (PIPE) {
+    // The same loop software-pipelined inside each wave (as the forward kernel's): A fragments
+    // fetched a band ahead, the last band held across the barrier while the next stage's first
+    // fragments arrive, the split of the entity rows inside band 1.
+    bf16x8 ah[2], al[2];
+    auto read_a = [&](const unsigned char* stg, int x, int slot) {
+      const int ra = wr * (BM / WM) + x * 16 + fr;
+      ah[slot] = *reinterpret_cast<const bf16x8*>(stg + sw16_off(ra, fs));
+      al[slot] = *reinterpret_cast<const bf16x8*>(stg + PLANE_A + sw16_off(ra, fs));
+    };
+    auto read_b = [&](const unsigned char* stg, int y) {
+      const int rb_ = wc * WCOLS + y * 16 + fr;
+      b_h[y] = *reinterpret_cast<const bf16x8*>(stg + 2 * PLANE_A + sw16_off(rb_, fs));
+      b_l[y] = *reinterpret_cast<const bf16x8*>(stg + 2 * PLANE_A + PLANE_B + sw16_off(rb_, fs));
+    };
+    auto mfma3 = [&](int x, int y, int slot) {
+      acc[x][y] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al[slot], b_h[y], acc[x][y], 0, 0, 0);
+      acc[x][y] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[slot], b_l[y], acc[x][y], 0, 0, 0);
+      acc[x][y] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[slot], b_h[y], acc[x][y], 0, 0, 0);
+    };
+    static_assert(TM % 2 == 0 && TM >= 4, "held band in fragment slot 1");
+    read_a(smem, 0, 0);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int y = 0; y < TN; ++y) {
+      read_b(smem, y);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    for (int st = 0; st < nst; ++st) {
+      const int nb = (st + 1) & 1;
+      const unsigned char* cur = smem + (st & 1) * STAGE;
+      unsigned char* nxt = smem + nb * STAGE;
+      const int k1 = min(st + 1, nst - 1) * BK;
+      glds_a(nb, k1);
+#pragma unroll
+      for (int x = 0; x < TM - 1; ++x) {
+        read_a(cur, x + 1, (x + 1) & 1);
+        if (x == 1) {
+          KGE_WAIT_VM(2 * A_G);  // B(st + 1) has landed
+          store_b(nxt);
+          load_b(min(st + 2, nst - 1) * BK);
+        }
+#pragma unroll
+        for (int y = 0; y < TN; ++y) mfma3(x, y, x & 1);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      KGE_WAIT_VM(2);  // A(st + 1) has landed
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      read_a(nxt, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int y = 0; y < TN; ++y) {
+        mfma3(TM - 1, y, (TM - 1) & 1);
+        __builtin_amdgcn_sched_barrier(0);
+        read_b(nxt, y);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+  } else
   for (int st = 0; st < nst; ++st) {
     const int nb = (st + 1) & 1;
     const unsigned char* cur = smem + (st & 1) * STAGE;
@@ -385,6 +447,8 @@ __global__ void __launch_bounds__(NT, 1)
   store_tile(acc, smem, wave, lane, wr, wc, dt, lddt, m0, n0, M, N, alpha, accumulate != 0);
 }
 
+int g_bwdp_pipe = 1;  // dev builds can switch the dQ kernel back to its plain loop (kge_dev_bwdp_pipe)
+
 int splits_q(int64_t n, int64_t m, int d, int cus) {
   const int64_t tiles = ((n + BM - 1) / BM) * ((d + BN - 1) / BN);
   const int64_t by_k = std::max<int64_t>(1, (m + 8 * BK - 1) / (8 * BK));
@@ -424,12 +488,17 @@ extern "C" int kge_score_dot_bwd_q_planes(const void* g_hi, const void* g_lo, in
   KGE_REQUIRE(ws_elems >= (int64_t)splits * n * d);
   hipStream_t st = as_stream(stream);
   static std::atomic<bool> lds_ok[KGE_MAX_DEVICES];
-  if (const int e = kge_allow_lds((const void*)bwd3p_q_kernel, 2 * STAGE, lds_ok)) return e;
+  static std::atomic<bool> lds_ok_plain[KGE_MAX_DEVICES];
+  const bool pipe = g_bwdp_pipe != 0;
+  if (const int e = pipe ? kge_allow_lds((const void*)bwd3p_q_kernel<true>, 2 * STAGE, lds_ok)
+                         : kge_allow_lds((const void*)bwd3p_q_kernel<false>, 2 * STAGE, lds_ok_plain))
+    return e;
   const int nrt = (int)((n + BM - 1) / BM), nct = (d + BN - 1) / BN;
   const int64_t blocks = (int64_t)nrt * nct * splits;
   if (blocks > 0x7fffffff) return KGE_ERR_ARG;
-  bwd3p_q_kernel<<<dim3((unsigned)blocks), dim3(NT), 2 * STAGE, st>>>((const __bf16*)g_hi, (const __bf16*)g_lo, ldgp, t,
-                                                                      ldt, (int)n, d, (int)m, kchunk, nrt, nct, ws);
+  auto kern = pipe ? bwd3p_q_kernel<true> : bwd3p_q_kernel<false>;
+  kern<<<dim3((unsigned)blocks), dim3(NT), 2 * STAGE, st>>>((const __bf16*)g_hi, (const __bf16*)g_lo, ldgp, t, ldt, (int)n,
+                                                            d, (int)m, kchunk, nrt, nct, ws);
   KGE_CHECK_LAUNCH();
   const int64_t total = n * (d / 4);
   const int sblocks = (int)std::min<int64_t>((total + 255) / 256, (int64_t)kge_num_cus() * 4);
@@ -461,3 +530,7 @@ extern "C" int kge_score_dot_bwd_t_planes(const void* g_hi, const void* g_lo, in
   KGE_CHECK_LAUNCH();
   return 0;
 }
+
+#ifdef KGE_DEV_BUILD  // libkgescore_dev.so only
+extern "C" void kge_dev_bwdp_pipe(int on) { g_bwdp_pipe = on; }
+#endif

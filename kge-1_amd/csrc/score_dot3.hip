@@ -377,6 +377,11 @@ __global__ void split_rows_kernel(const float* __restrict__ x, int64_t ldx, int 
 
 }  // namespace
 
+#ifdef KGE_DEV_BUILD
+static int g_dot3_pipe = 1;
+extern "C" void kge_dev_dot3_pipe(int on) { g_dot3_pipe = on; }
+#endif
+
 extern "C" int kge_split_rows(const float* x, int64_t ldx, int64_t n, int d, void* hi, void* lo, int64_t ldo,
                               void* stream) {
   KGE_REQUIRE(n >= 0 && d > 0 && x && hi && lo && ldx >= d && ldo >= d && ldo % 8 == 0);
@@ -399,6 +404,12 @@ extern "C" int kge_score_dot_split(const void* qhi, const void* qlo, int64_t ldq
   hipStream_t st = as_stream(stream);
   const __bf16* h = (const __bf16*)qhi;
   const __bf16* l = (const __bf16*)qlo;
+#ifdef KGE_DEV_BUILD  // A/B against the plain K loop (kge_dev_dot3_pipe)
+  if (!g_dot3_pipe) {
+    if (n > 128) return launch_persist16<256, 256, 2, 4>(h, l, ldq, t, ldt, tidx, n, m, d, s, lds, st);
+    return launch_persist16<128, 256, 2, 4>(h, l, ldq, t, ldt, tidx, n, m, d, s, lds, st);
+  }
+#endif
   if (n > 128) return launch_persist16<256, 256, 2, 4, 0, true>(h, l, ldq, t, ldt, tidx, n, m, d, s, lds, st);
   return launch_persist16<128, 256, 2, 4, 0, true>(h, l, ldq, t, ldt, tidx, n, m, d, s, lds, st);
 }
@@ -437,6 +448,9 @@ extern "C" int kge_dev_score_dot_persist(int variant, const void* qhi, const voi
     case 44: return launch_persist16<256, 256, 2, 4, 16, true>(h, l, ldq, t, ldt, tidx, n, m, d, s, lds, st);
     case 45: return launch_persist16<256, 256, 2, 4, 32, true>(h, l, ldq, t, ldt, tidx, n, m, d, s, lds, st);
     case 46: return launch_persist16<256, 256, 2, 4, 64, true>(h, l, ldq, t, ldt, tidx, n, m, d, s, lds, st);
+    case 51: return launch_persist16<256, 256, 2, 4, 5, true>(h, l, ldq, t, ldt, tidx, n, m, d, s, lds, st);
+    case 52: return launch_persist16<256, 256, 2, 4, 6, true>(h, l, ldq, t, ldt, tidx, n, m, d, s, lds, st);
+    case 53: return launch_persist16<256, 256, 2, 4, 7, true>(h, l, ldq, t, ldt, tidx, n, m, d, s, lds, st);
     default: return KGE_ERR_ARG;
   }
 }

@@ -1,6 +1,7 @@
 """Dev timing: plane-fed backward GEMMs and loss kernel vs the fp32-G kernels at the stacked
 C2 training shape (2,048 queries x 14,541 entities x 512); interleaved rounds in one process."""
 import sys
+import os as _os; _os.environ.setdefault('KGE_LIBRARY', _os.path.join(_os.path.dirname(_os.path.dirname(_os.path.dirname(_os.path.abspath(__file__)))), 'kge-1_amd', 'csrc', 'build_dev', 'libkgescore_dev.so'))  # `make dev`
 import os as _os; _R = _os.path.dirname(_os.path.dirname(_os.path.dirname(_os.path.abspath(__file__)))); sys.path.insert(0, _R); sys.path.insert(0, _os.path.join(_R, 'kge-1_amd'))
 import numpy as np, torch
 from kge import _lib as L
@@ -29,7 +30,20 @@ def run(name, fn, reps=20):
     for _ in range(reps): fn()
     b.record(); torch.cuda.synchronize()
     return a.elapsed_time(b) / reps * 1e3
+def plain(fn):  # the same entry point with the kernels' plain (not software-pipelined) loops
+    def run_plain():
+        L.lib().kge_dev_bwdp_pipe(0)
+        fn()
+        L.lib().kge_dev_bwdp_pipe(1)
+    return run_plain
+dq2 = torch.empty_like(dq); de2 = torch.empty_like(de)
+L.score_dot_bwd_q_planes(gp, ent, dq=dq); L.score_dot_bwd_t_planes(gp, qh, ql, de)
+plain(lambda: L.score_dot_bwd_q_planes(gp, ent, dq=dq2))(); plain(lambda: L.score_dot_bwd_t_planes(gp, qh, ql, de2))()
+torch.cuda.synchronize()
+print("pipelined == plain bitwise: dQ", bool((dq == dq2).all()), " dE", bool((de == de2).all()), flush=True)
 variants = {
+    "dQ planes plain loop": plain(lambda: L.score_dot_bwd_q_planes(gp, ent, dq=dq)),
+    "dE planes plain loop": plain(lambda: L.score_dot_bwd_t_planes(gp, qh, ql, de)),
     "dQ old (fp32 G, ws)": lambda: L.score_dot_bwd_q(s4, ent, None, L.PREC_BF16X3, dq=dq),
     "dQ planes": lambda: L.score_dot_bwd_q_planes(gp, ent, dq=dq),
     "dE old (fp32 G)": lambda: L.score_dot_bwd_t(s4, q, None, de, L.PREC_BF16X3, accumulate=False),
