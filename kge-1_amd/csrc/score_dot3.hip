@@ -63,6 +63,7 @@ __global__ void __launch_bounds__(64 * WM * WN, 1)
   const int64_t lo_off = qlo - qhi;
   const uint64_t t_clk0 = (ABL & 4) ? __builtin_amdgcn_s_memtime() : 0;
   const uint64_t t_rt0 = (ABL & 4) ? __builtin_amdgcn_s_memrealtime() : 0;
+  uint64_t t_loop0 = 0, t_loop1 = 0;  // dev probe: K loop entry / exit of the last tile
 
   for (int it = 0;; ++it) {
     const int tile = it * G + xcd * per_xcd + local;
@@ -195,6 +196,7 @@ __global__ void __launch_bounds__(64 * WM * WN, 1)
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
+    if (ABL & 4) t_loop0 = __builtin_amdgcn_s_memtime();
     if constexpr (PIPE) {
       // Inside a wave nothing but the matrix pipe should ever be waited for, so every LDS read
       // is issued a band (12 MFMAs) before its use: band x + 1's A fragments while band x runs,
@@ -217,10 +219,13 @@ __global__ void __launch_bounds__(64 * WM * WN, 1)
         b_h[y] = *reinterpret_cast<const bf16x8*>(stg + 2 * C::PLANE_A + sw16_off(rb_, fs));
         b_l[y] = *reinterpret_cast<const bf16x8*>(stg + 2 * C::PLANE_A + C::PLANE_B + sw16_off(rb_, fs));
       };
+      // the entity fragment goes first: the 16 x 16 result comes out transposed (same sums, bit
+      // for bit), a lane holding four CONSECUTIVE entities of one query row -- the epilogue
+      // then moves whole float4s through its LDS scratch
       auto mfma3 = [&](int x, int y, int slot) {
-        acc[x][y] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al[slot], b_h[y], acc[x][y], 0, 0, 0);
-        acc[x][y] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[slot], b_l[y], acc[x][y], 0, 0, 0);
-        acc[x][y] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[slot], b_h[y], acc[x][y], 0, 0, 0);
+        acc[x][y] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b_h[y], al[slot], acc[x][y], 0, 0, 0);
+        acc[x][y] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b_l[y], ah[slot], acc[x][y], 0, 0, 0);
+        acc[x][y] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b_h[y], ah[slot], acc[x][y], 0, 0, 0);
       };
       // same issue order as at the end of the loop body: the waits at the loop head then only
       // cover what the first MFMAs need
@@ -300,6 +305,7 @@ __global__ void __launch_bounds__(64 * WM * WN, 1)
     }
     KGE_WAIT_VM(0);
 #undef KGE_WAIT_VM
+    if (ABL & 4) t_loop1 = __builtin_amdgcn_s_memtime();
 
     // epilogue: C/D of 16x16 -- lane holds column (lane & 15), rows 4 (lane >> 4) + r
     __syncthreads();  // stage buffers free: per-wave scratch of 16 rows x WCOLS (+4) floats
@@ -308,9 +314,14 @@ __global__ void __launch_bounds__(64 * WM * WN, 1)
 #pragma unroll
     for (int x = 0; x < TM; ++x) {
 #pragma unroll
-      for (int y = 0; y < TN; ++y)
+      for (int y = 0; y < TN; ++y) {
+        if constexpr (PIPE) {  // transposed accumulators: row (lane & 15), columns 4 (lane >> 4) .. + 3
+          *reinterpret_cast<f32x4*>(scr + fr * SCR_LD + y * 16 + 4 * fs) = acc[x][y];
+        } else {
 #pragma unroll
-        for (int r = 0; r < 4; ++r) scr[(4 * fs + r) * SCR_LD + y * 16 + fr] = acc[x][y][r];
+          for (int r = 0; r < 4; ++r) scr[(4 * fs + r) * SCR_LD + y * 16 + fr] = acc[x][y][r];
+        }
+      }
       const int i0 = m0 + wr * (BM / WM) + x * 16;
 #pragma unroll
       for (int pass = 0; pass < (16 * LPR + 63) / 64; ++pass) {
@@ -337,8 +348,10 @@ __global__ void __launch_bounds__(64 * WM * WN, 1)
   }
   if ((ABL & 4) && tid == 0) {  // dev: shader clocks and 100-MHz ticks spent by this workgroup
     const uint64_t c = __builtin_amdgcn_s_memtime() - t_clk0, r = __builtin_amdgcn_s_memrealtime() - t_rt0;
-    s[(int64_t)n * lds + 2 * blockIdx.x] = (float)c;  // the caller allocates row n
+    s[(int64_t)n * lds + 2 * blockIdx.x] = (float)c;  // the caller allocates rows n, n + 1
     s[(int64_t)n * lds + 2 * blockIdx.x + 1] = (float)r;
+    s[(int64_t)(n + 1) * lds + 2 * blockIdx.x] = (float)(t_loop0 - t_clk0);
+    s[(int64_t)(n + 1) * lds + 2 * blockIdx.x + 1] = (float)(t_loop1 - t_clk0);
   }
 }
 
