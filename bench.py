@@ -59,6 +59,7 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=8.0)
     ap.add_argument("--no-extras", action="store_true")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-probe", action="store_true", help="skip the machine-ceiling probes (profiling runs)")
     ap.add_argument("--c5", action="store_true", help="N = 1: also time one rank's Wikidata5M shard (configs[4])")
     ap.add_argument("--no-c5", action="store_true", help="N > 1: skip the row-sharded Wikidata5M step")
     return ap.parse_args()
@@ -376,7 +377,7 @@ def main():
                 "exact_fp32_kernel_us": round(k32_ms * 1e3, 2),
                 "exact_fp32_kernel_frac_of_fp32_mfma_peak": round(alg_flops / (k32_ms / 1e3) / 1e12 / FP32_MFMA_TFLOPS, 4)}
 
-    if world == 1:
+    if world == 1 and not args.no_probe:
         ceil = machine_ceilings(device)
         if ceil is not None:
             roofline["measured_ceilings"] = ceil

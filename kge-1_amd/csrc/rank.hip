@@ -229,18 +229,23 @@ __global__ void __launch_bounds__(NT) rank_rows_kernel(const RankRowsArgs a) {
     if (!any) return done;
     const unsigned total = ev_total;  // stable: nobody pushes before the barrier below
     // wave w takes entries w, w + 4, ...: four at a time (four row loads in flight) while it has
-    // four left, then one by one
+    // at least two left -- a round's idle slots recompute its first entry (same cache lines) and
+    // are not counted -- then a last single one
     constexpr int U = 4, NWV = NT / 64;
     unsigned x0 = done + wave;
-    for (; x0 + (U - 1) * NWV < total; x0 += U * NWV) {
+    for (; x0 + NWV < total; x0 += U * NWV) {
       const float* rows_[U];
       float v[U];
 #pragma unroll
-      for (int u = 0; u < U; ++u) rows_[u] = a.t + (int64_t)ev[(x0 + u * NWV) % EV_CAP] * a.ldt;
+      for (int u = 0; u < U; ++u) {
+        const unsigned x = x0 + u * NWV < total ? x0 + u * NWV : x0;
+        rows_[u] = a.t + (int64_t)ev[x % EV_CAP] * a.ldt;
+      }
       exact_dots_wave<U>(qrow, rows_, a.d, v);
       if (lane == 0) {
 #pragma unroll
         for (int u = 0; u < U; ++u) {
+          if (x0 + u * NWV >= total) continue;
           const float v_ = clean(v[u]);
           gt += sign * (v_ > t);
           eq += sign * (v_ == t);
@@ -261,34 +266,64 @@ __global__ void __launch_bounds__(NT) rank_rows_kernel(const RankRowsArgs a) {
     return total;
   };
 
-  unsigned done = 0;
-  if (VEC) {
-    const int64_t m4 = m & ~(int64_t)3;
-    for (int64_t base = 0; base < m4; base += 8 * NT) {  // uniform trip count
+  // The scan of the row.  step_drain: rescore the deferred entries after every step of 8 NT
+  // columns (the ring holds one step's worth whatever the row looks like); otherwise they all
+  // wait in the ring for ONE drain after the scan (all their row loads in flight together).
+  auto scan = [&](bool step_drain) {
+    unsigned done = 0;
+    if (VEC) {
+      const int64_t m4 = m & ~(int64_t)3;
+      for (int64_t base = 0; base < m4; base += 8 * NT) {  // uniform trip count
 #pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        const int64_t j = base + 4 * (int64_t)(threadIdx.x + h * NT);
-        if (j < m4) {
-          const float4 v4 = *reinterpret_cast<const float4*>(row + j);
-          count(j, v4.x, 1);
-          count(j + 1, v4.y, 1);
-          count(j + 2, v4.z, 1);
-          count(j + 3, v4.w, 1);
+        for (int h = 0; h < 2; ++h) {
+          const int64_t j = base + 4 * (int64_t)(threadIdx.x + h * NT);
+          if (j < m4) {
+            const float4 v4 = *reinterpret_cast<const float4*>(row + j);
+            count(j, v4.x, 1);
+            count(j + 1, v4.y, 1);
+            count(j + 2, v4.z, 1);
+            count(j + 3, v4.w, 1);
+          }
         }
+        if (REFINE && step_drain) done = drain(done, 1);
       }
-      if (REFINE) done = drain(done, 1);
-    }
-    if (m4 + threadIdx.x < m) count(m4 + threadIdx.x, row[m4 + threadIdx.x], 1);
-    if (REFINE) done = drain(done, 1);
-  } else {
-    for (int64_t base = 0; base < m; base += 8 * NT) {
+      if (m4 + threadIdx.x < m) count(m4 + threadIdx.x, row[m4 + threadIdx.x], 1);
+      if (REFINE && step_drain) done = drain(done, 1);
+    } else {
+      for (int64_t base = 0; base < m; base += 8 * NT) {
 #pragma unroll
-      for (int h = 0; h < 8; ++h) {
-        const int64_t j = base + threadIdx.x + h * NT;
-        if (j < m) count(j, row[j], 1);
+        for (int h = 0; h < 8; ++h) {
+          const int64_t j = base + threadIdx.x + h * NT;
+          if (j < m) count(j, row[j], 1);
+        }
+        if (REFINE && step_drain) done = drain(done, 1);
       }
-      if (REFINE) done = drain(done, 1);
     }
+    return done;
+  };
+  unsigned done = 0;  // ring entries rescored so far
+  if (REFINE) {
+    // Rows with at most EV_CAP entries inside the band (all but degenerate ones: thousands of
+    // candidates tied with the true score) are scanned without a barrier and drained once.  A
+    // row with more has overwritten ring slots: its counts are discarded and the row is scanned
+    // again, draining after every step.
+    scan(false);
+    __syncthreads();  // every push is visible; nobody pushes again before the next barrier
+    const bool overflow = ev_total > (unsigned)EV_CAP;
+    if (!overflow) {
+      pushed = 1;
+      done = drain(0, 1);
+    } else {
+      __syncthreads();  // ev_total has been read by every thread
+      if (threadIdx.x == 0) ev_total = 0;
+      gt = 0;
+      eq = 0;
+      pushed = 0;
+      __syncthreads();
+      done = scan(true);
+    }
+  } else {
+    scan(false);
   }
   block_sum2(gt, eq, sm);
   auto emit = [&](int r, int64_t g, int64_t e) {  // thread 0 only

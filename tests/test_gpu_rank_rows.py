@@ -207,6 +207,49 @@ def test_rank_rows_refinement_equals_exact_scoring(L, d, m):
     assert (err / bound).max() < 0.25e-4
 
 
+@pytest.mark.parametrize("m,near", [(6000, 5000), (6000, 2048), (6000, 2049), (9001, 9000)])
+def test_rank_rows_refinement_rows_with_thousands_of_near_ties(L, m, near):
+    """More entries inside the band than the kernel's near-tie ring holds (2,048): such a row is
+    scanned a second time, rescoring after every step.  `near` candidate rows are copies of the
+    true row up to a 1e-6 relative perturbation; refined counts must equal exact scoring, raw and
+    filtered, on rows of both kinds in the same launch."""
+    rng = np.random.default_rng(m + near)
+    n, d = 6, 128
+    q = (rng.standard_normal((n, d)) * 0.3).astype(np.float32)
+    t = (rng.standard_normal((m, d)) * 0.3).astype(np.float32)
+    true_idx = np.arange(n, dtype=np.int64) * 7
+    crowded = [3]  # this query's true row is copied `near` times
+    pool = np.setdiff1d(np.arange(m), true_idx)
+    for i in crowded:
+        js = rng.choice(pool, size=min(near, len(pool)), replace=False)
+        eps = rng.uniform(-1e-6, 1e-6, size=(len(js), 1))
+        t[js] = (t[true_idx[i]].astype(np.float64)[None] * (1.0 + eps)).astype(np.float32)
+        # make them near-ties of query i only by giving query i a large component along its true row
+        q[i] = (t[true_idx[i]] * 2.0 + q[i] * 0.01).astype(np.float32)
+    exact = (q.astype(np.float64) @ t.astype(np.float64).T).astype(np.float32)
+    true_score = exact[np.arange(n), true_idx].copy()
+    f_ptr, f_col = _csr(rng, n, m, 40)
+    exp = _oracle_counts(exact, 0, true_idx, true_score, [(f_ptr, f_col)])
+    qd, td = _dev(q), _dev(t)
+    hi, lo = L.split_rows(qd)
+    buf = torch.empty(n, (m + 3) // 4 * 4, device="cuda")
+    s = L.score_dot_split(hi, lo, td, None, d, out=buf[:, :m])
+    part = (_dev(true_idx), _dev(true_score), _dev(f_ptr), None)
+    g = torch.empty(2 * n, dtype=torch.int64, device="cuda")
+    tt = torch.empty(2 * n, dtype=torch.int64, device="cuda")
+    tmax = L.row_norm_max(td)
+    band = 1e-4
+    L.rank_rows(s, n, 0, part, None, _dev(np.concatenate([f_col, [0]])), None, g, tt, accumulate=False,
+                refine=(qd, td, band, tmax))
+    in_band = (np.abs(s.cpu().numpy() - true_score[:, None])
+               <= band * np.linalg.norm(q, axis=1)[:, None] * float(tmax)).sum(1)
+    assert (in_band[crowded] >= min(near, len(pool))).all() and in_band[1] < 2048
+    g, tt = g.view(2, n).cpu().numpy(), tt.view(2, n).cpu().numpy()
+    for r in range(2):
+        assert np.array_equal(g[r], exp[r][0]), (r, g[r], exp[r][0])
+        assert np.array_equal(tt[r], exp[r][1]), (r, tt[r], exp[r][1])
+
+
 @pytest.mark.parametrize("model,dim", [("distmult", 64), ("rescal", 16), ("simple", 64), ("complex", 64), ("cp", 64),
                                        ("transe", 64), ("rotate", 64), ("complex", 50), ("distmult", 37)])
 @pytest.mark.parametrize("chunk", [-1, 700])
