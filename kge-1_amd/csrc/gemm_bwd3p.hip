@@ -352,6 +352,10 @@ __device__ __forceinline__ bf16x8 tr_frag16(const unsigned char* img, int c0, in
   return f;
 }
 
+// NSTG LDS stage buffers: 2 = the next stage's transfers are in flight during a stage's MFMAs;
+// 3 = the next two stages' (144 KB of LDS), which covers HBM latency when the G planes are not
+// resident in the memory-side cache.
+template <int NSTG>
 __global__ void __launch_bounds__(NT, 1)
     bwd3p_t_kernel(const __bf16* __restrict__ ghi, const __bf16* __restrict__ glo, int64_t ldgp, int64_t gcols,
                    const __bf16* __restrict__ qhi, const __bf16* __restrict__ qlo, int64_t ldqp, int64_t qcols,
@@ -432,22 +436,48 @@ __global__ void __launch_bounds__(NT, 1)
 
   // Every vector-memory operation of the loop is an LDS-DMA issued from inline asm: the stage
   // st + 1 transfers are issued before stage st's MFMAs and waited for (vmcnt(0)) after them.
-  stage(0, 0);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-  asm volatile("" ::: "memory");
-  for (int st = 0; st < nst; ++st) {
-    if (st + 1 < nst) stage((st + 1) & 1, st + 1);  // uniform branch; no register loads in flight
-    compute(smem + (st & 1) * STAGE);
-    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  if constexpr (NSTG == 3) {
+    // Three buffers, branch-free: iteration st issues the transfers of stage st + 2 (the last K
+    // chunk again once there is none: it lands in a buffer nobody reads any more) into the
+    // buffer that stage st - 1 was read from, and waits until at most those 6 instructions are
+    // outstanding -- vector-memory operations retire in order, so stage st + 1 has landed.
+    stage(0, 0);
+    stage(1, min(1, nst - 1));
+    asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
+    int cur = 0, nxt2 = 2;  // buffer of stage st, buffer for stage st + 2
+    for (int st = 0; st < nst; ++st) {
+      stage(nxt2, min(st + 2, nst - 1));
+      compute(smem + cur * STAGE);
+      asm volatile("s_waitcnt vmcnt(6) lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      nxt2 = cur;
+      cur = cur == 2 ? 0 : cur + 1;
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the redundant tail transfers target LDS too
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  } else {
+    stage(0, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    for (int st = 0; st < nst; ++st) {
+      if (st + 1 < nst) stage((st + 1) & 1, st + 1);  // uniform branch; no register loads in flight
+      compute(smem + (st & 1) * STAGE);
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+    }
   }
   const float alpha = alpha_ptr ? *alpha_ptr : 1.f;
   store_tile(acc, smem, wave, lane, wr, wc, dt, lddt, m0, n0, M, N, alpha, accumulate != 0);
 }
 
-int g_bwdp_pipe = 1;  // dev builds can switch the dQ kernel back to its plain loop (kge_dev_bwdp_pipe)
+int g_bwdp_pipe = 1;    // dev builds can switch the dQ kernel back to its plain loop (kge_dev_bwdp_pipe)
+int g_bwdp_stages = 3;  // ... and the dE kernel back to two LDS stage buffers (kge_dev_bwdp_stages)
 
 int splits_q(int64_t n, int64_t m, int d, int cus) {
   const int64_t tiles = ((n + BM - 1) / BM) * ((d + BN - 1) / BN);
@@ -520,11 +550,16 @@ extern "C" int kge_score_dot_bwd_t_planes(const void* g_hi, const void* g_lo, in
     return KGE_ERR_ALIGN;
   hipStream_t st = as_stream(stream);
   static std::atomic<bool> lds_ok[KGE_MAX_DEVICES];
-  if (const int e = kge_allow_lds((const void*)bwd3p_t_kernel, 2 * STAGE, lds_ok)) return e;
+  static std::atomic<bool> lds_ok2[KGE_MAX_DEVICES];
+  const bool three = g_bwdp_stages == 3;
+  if (const int e = three ? kge_allow_lds((const void*)bwd3p_t_kernel<3>, 3 * STAGE, lds_ok)
+                          : kge_allow_lds((const void*)bwd3p_t_kernel<2>, 2 * STAGE, lds_ok2))
+    return e;
   const int nrt = (int)((m + BM - 1) / BM), nct = (d + BN - 1) / BN;
   const int64_t blocks = (int64_t)nrt * nct;
   if (blocks > 0x7fffffff) return KGE_ERR_ARG;
-  bwd3p_t_kernel<<<dim3((unsigned)blocks), dim3(NT), 2 * STAGE, st>>>(
+  auto kern = three ? bwd3p_t_kernel<3> : bwd3p_t_kernel<2>;
+  kern<<<dim3((unsigned)blocks), dim3(NT), (three ? 3 : 2) * STAGE, st>>>(
       (const __bf16*)g_hi, (const __bf16*)g_lo, ldgp, gcols, (const __bf16*)q_hi, (const __bf16*)q_lo, ldqp, qcols,
       (int)m, d, (int)n_pad, nct, dt, lddt, accumulate, gscale);
   KGE_CHECK_LAUNCH();
@@ -533,4 +568,5 @@ extern "C" int kge_score_dot_bwd_t_planes(const void* g_hi, const void* g_lo, in
 
 #ifdef KGE_DEV_BUILD  // libkgescore_dev.so only
 extern "C" void kge_dev_bwdp_pipe(int on) { g_bwdp_pipe = on; }
+extern "C" void kge_dev_bwdp_stages(int n) { g_bwdp_stages = n == 2 ? 2 : 3; }
 #endif

@@ -12,9 +12,10 @@ model = sys.argv[1] if len(sys.argv) > 1 else "complex"
 ttype = sys.argv[2] if len(sys.argv) > 2 else "1vsAll"
 
 
-def run(fwd, dq, steps=30, warmup=6):
+def run(fwd, dq, stages=3, steps=30, warmup=6):
     _lib.lib().kge_dev_dot3_pipe(fwd)
     _lib.lib().kge_dev_bwdp_pipe(dq)
+    _lib.lib().kge_dev_bwdp_stages(stages)
     c = Config()
     c.set("model", model); c._import(model)
     c.set("job.device", "cuda")
@@ -33,9 +34,9 @@ def run(fwd, dq, steps=30, warmup=6):
     for i in range(warmup, warmup + steps):
         job.train_step(i, job._collate(perm[i * B:(i + 1) * B]))
     torch.cuda.synchronize()
-    print(f"{model} {ttype} forward pipe {fwd} dQ pipe {dq}: {(time.perf_counter() - t0) / steps * 1e3:.3f} ms/step", flush=True)
+    print(f"{model} {ttype} forward pipe {fwd} dQ pipe {dq} dE stage buffers {stages}: {(time.perf_counter() - t0) / steps * 1e3:.3f} ms/step", flush=True)
 
 
-for _ in range(2):
-    for fwd, dq in ((0, 0), (1, 0), (0, 1), (1, 1)):
-        run(fwd, dq)
+for _ in range(3):
+    for fwd, dq, stages in ((0, 0, 2), (1, 1, 2), (1, 1, 3)):
+        run(fwd, dq, stages)

@@ -51,6 +51,23 @@ variants = {
     "loss old (in place fp32)": lambda: L.softmax_xent(s4, labels, 1.0 / n, g=s4),
     "loss planes": lambda: L.softmax_planes(bufp, n, m, labels, None, 0.0, 1.0 / n),
 }
+big = torch.empty(96 * 1024 * 1024, device="cuda")  # 384 MB: more than the 256-MB memory-side cache
+variants["dQ then dE (pair)"] = lambda: (L.score_dot_bwd_q_planes(gp, ent, dq=dq), L.score_dot_bwd_t_planes(gp, qh, ql, de))
+variants["loss planes then dQ then dE"] = lambda: (L.softmax_planes(bufp, n, m, labels, None, 0.0, 1.0 / n), L.score_dot_bwd_q_planes(gp, ent, dq=dq), L.score_dot_bwd_t_planes(gp, qh, ql, de))
+def two_stage(fn):
+    def run2():
+        L.lib().kge_dev_bwdp_stages(2)
+        fn()
+        L.lib().kge_dev_bwdp_stages(3)
+    return run2
+de3 = torch.empty_like(de)
+two_stage(lambda: L.score_dot_bwd_t_planes(gp, qh, ql, de3))(); L.score_dot_bwd_t_planes(gp, qh, ql, de); torch.cuda.synchronize()
+print("dE 3 stage buffers == 2 stage buffers bitwise:", bool((de == de3).all()), flush=True)
+variants["dE planes, 2 stage buffers"] = two_stage(lambda: L.score_dot_bwd_t_planes(gp, qh, ql, de))
+variants["384-MB fill then dE, 2 stage buffers"] = two_stage(lambda: (big.fill_(1.0), L.score_dot_bwd_t_planes(gp, qh, ql, de)))
+variants["384-MB fill"] = lambda: big.fill_(1.0)
+variants["384-MB fill then dE"] = lambda: (big.fill_(1.0), L.score_dot_bwd_t_planes(gp, qh, ql, de))
+variants["384-MB fill then dQ"] = lambda: (big.fill_(1.0), L.score_dot_bwd_q_planes(gp, ent, dq=dq))
 res = {k: [] for k in variants}
 for r in range(5):
     for k, fn in variants.items():
