@@ -347,6 +347,13 @@ int kge_adagrad_step(float* param, const float* grad, float* state_sum, int64_t 
                      float minus_clr, float eps, float weight_decay, int maximize,
                      void* stream);
 
+/* The same step for up to 8 tensors in ONE launch (the entity and the relation table of a
+ * training step): host arrays of `count` device pointers / element counts / per-tensor
+ * minus_clr; eps, weight_decay and maximize are shared (one torch param group). */
+int kge_adagrad_step_multi(int count, float* const* params, const float* const* grads,
+                           float* const* state_sums, const int64_t* ns, const float* minus_clrs,
+                           float eps, float weight_decay, int maximize, void* stream);
+
 /* Copy n int64 from host-pinned, device-visible memory (hipHostMalloc) into device memory
  * with a kernel on `stream`: the per-batch index upload of the replayed 1vsAll training
  * step (engine.graph_step).  Internal plumbing; no reference counterpart (the reference

@@ -51,6 +51,7 @@ SIGNATURES = {
     "kge_score_dot_bwd_q_noalloc": ([_P, _I64, _P, _I64, _P, _I64, _I64, _I, _P, _I64, _I, _P], _I),
     "kge_score_dot_bwd_t": ([_P, _I64, _P, _I64, _P, _I64, _I64, _I, _P, _I64, _I, _P], _I),
     "kge_adagrad_step": ([_P, _P, _P, _I64, ctypes.c_float, ctypes.c_float, ctypes.c_float, _I, _P], _I),
+    "kge_adagrad_step_multi": ([_I, _P, _P, _P, _P, _P, ctypes.c_float, ctypes.c_float, _I, _P], _I),
     "kge_score_dot_bwd_t_ex": ([_P, _I64, _P, _I64, _P, _I64, _I64, _I, _P, _I64, _I, _I, _P], _I),
     "kge_score_dist": ([_I, _F, _P, _I64, _P, _I64, _P, _I64, _I64, _I, _P, _I64, _P], _I),
     "kge_score_dist_bwd": ([_I, _F, _P, _I64, _P, _I64, _P, _I64, _P, _I64, _I64, _I, _P, _I64, _P,
@@ -717,6 +718,27 @@ def stage_i64(src_pinned, dst):
             and src_pinned.is_contiguous() and dst.is_contiguous() and src_pinned.numel() == dst.numel()):
         raise ValueError("stage_i64: needs a contiguous pinned int64 source and a same-size CUDA int64 target")
     _check(lib().kge_stage_i64(ptr(src_pinned), ptr(dst), dst.numel(), stream()), "kge_stage_i64")
+
+
+ADAGRAD_MULTI_MAX = 8
+
+
+def adagrad_step_multi(items, eps, weight_decay, maximize):
+    """One fused Adagrad step on several tensors in a single launch (kge_adagrad_step_multi).
+    items: up to ADAGRAD_MULTI_MAX tuples (param, grad, state_sum, minus_clr) of contiguous fp32
+    CUDA tensors."""
+    k = len(items)
+    if k == 0:
+        return
+    if k > ADAGRAD_MULTI_MAX:
+        raise ValueError(f"at most {ADAGRAD_MULTI_MAX} tensors per launch")
+    arr_p = (ctypes.c_void_p * k)(*[ptr(p) for p, _, _, _ in items])
+    arr_g = (ctypes.c_void_p * k)(*[ptr(g) for _, g, _, _ in items])
+    arr_s = (ctypes.c_void_p * k)(*[ptr(s) for _, _, s, _ in items])
+    arr_n = (ctypes.c_int64 * k)(*[p.numel() for p, _, _, _ in items])
+    arr_c = (ctypes.c_float * k)(*[float(c) for _, _, _, c in items])
+    _check(lib().kge_adagrad_step_multi(k, arr_p, arr_g, arr_s, arr_n, arr_c, float(eps), float(weight_decay),
+                                        int(bool(maximize)), stream()), "kge_adagrad_step_multi")
 
 
 def adagrad_step(param, grad, state_sum, minus_clr, eps, weight_decay, maximize):

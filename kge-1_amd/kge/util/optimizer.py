@@ -8,8 +8,9 @@ import torch
 
 class FusedAdagrad(torch.optim.Adagrad):
     """torch.optim.Adagrad (same arguments, state_dict layout and per-element arithmetic)
-    whose step runs one engine kernel per parameter (kge_adagrad_step: a single pass over
-    param, grad and state sum) instead of the five-pass multi-tensor sequence.  Parameters
+    whose step runs one engine kernel per param group (kge_adagrad_step_multi: a single pass
+    over param, grad and state sum of up to 8 tensors per launch) instead of the five-pass
+    multi-tensor sequence.  Parameters
     the kernel does not take (not CUDA fp32 contiguous, sparse or complex gradients,
     differentiable mode) are stepped by torch."""
 
@@ -24,6 +25,7 @@ class FusedAdagrad(torch.optim.Adagrad):
         rest = []
         for group in self.param_groups:
             fallback = []
+            items = []  # (param, grad, state sum, minus_clr) of this group: one launch per 8
             for p in group["params"]:
                 if p.grad is None:
                     continue
@@ -38,7 +40,10 @@ class FusedAdagrad(torch.optim.Adagrad):
                 step = float(st["step"])
                 lr = float(group["lr"])
                 minus_clr = -lr / (1 + (step - 1) * group["lr_decay"])
-                _lib.adagrad_step(p, g, st["sum"], minus_clr, group["eps"], group["weight_decay"], group["maximize"])
+                items.append((p, g, st["sum"], minus_clr))
+            for i in range(0, len(items), _lib.ADAGRAD_MULTI_MAX):
+                _lib.adagrad_step_multi(items[i:i + _lib.ADAGRAD_MULTI_MAX], group["eps"], group["weight_decay"],
+                                        group["maximize"])
             if fallback:
                 rest.append((group, fallback))
         for group, params in rest:  # torch's own step for what the kernel does not take

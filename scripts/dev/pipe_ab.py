@@ -12,7 +12,16 @@ model = sys.argv[1] if len(sys.argv) > 1 else "complex"
 ttype = sys.argv[2] if len(sys.argv) > 2 else "1vsAll"
 
 
-def run(fwd, dq, stages=3, steps=30, warmup=6):
+_multi = _lib.adagrad_step_multi
+
+
+def _single(items, eps, wd, maximize):  # one launch per tensor, as before the multi-tensor launch
+    for p, g, s, c in items:
+        _lib.adagrad_step(p, g, s, c, eps, wd, maximize)
+
+
+def run(fwd, dq, stages=3, steps=30, warmup=6, multi=True):
+    _lib.adagrad_step_multi = _multi if multi else _single
     _lib.lib().kge_dev_dot3_pipe(fwd)
     _lib.lib().kge_dev_bwdp_pipe(dq)
     _lib.lib().kge_dev_bwdp_stages(stages)
@@ -34,9 +43,9 @@ def run(fwd, dq, stages=3, steps=30, warmup=6):
     for i in range(warmup, warmup + steps):
         job.train_step(i, job._collate(perm[i * B:(i + 1) * B]))
     torch.cuda.synchronize()
-    print(f"{model} {ttype} forward pipe {fwd} dQ pipe {dq} dE stage buffers {stages}: {(time.perf_counter() - t0) / steps * 1e3:.3f} ms/step", flush=True)
+    print(f"{model} {ttype} forward pipe {fwd} dQ pipe {dq} dE stage buffers {stages} adagrad multi {multi}: {(time.perf_counter() - t0) / steps * 1e3:.3f} ms/step", flush=True)
 
 
 for _ in range(3):
-    for fwd, dq, stages in ((0, 0, 2), (1, 1, 2), (1, 1, 3)):
-        run(fwd, dq, stages)
+    for fwd, dq, stages, multi in ((0, 0, 2, False), (1, 1, 3, False), (1, 1, 3, True)):
+        run(fwd, dq, stages, multi=multi)
