@@ -65,6 +65,12 @@ two_stage(lambda: L.score_dot_bwd_t_planes(gp, qh, ql, de3))(); L.score_dot_bwd_
 print("dE 3 stage buffers == 2 stage buffers bitwise:", bool((de == de3).all()), flush=True)
 variants["dE planes, 2 stage buffers"] = two_stage(lambda: L.score_dot_bwd_t_planes(gp, qh, ql, de))
 variants["384-MB fill then dE, 2 stage buffers"] = two_stage(lambda: (big.fill_(1.0), L.score_dot_bwd_t_planes(gp, qh, ql, de)))
+qh1, ql1 = L.split_rows(q)
+variants["forward"] = lambda: L.score_dot_split(qh1, ql1, ent, None, d, out=bufp[:n, :m])
+variants["forward, loss planes, dQ, dE"] = lambda: (L.score_dot_split(qh1, ql1, ent, None, d, out=bufp[:n, :m]), L.softmax_planes(bufp, n, m, labels, None, 0.0, 1.0 / n), L.score_dot_bwd_q_planes(gp, ent, dq=dq), L.score_dot_bwd_t_planes(gp, qh, ql, de))
+state = torch.zeros(m, d, device="cuda"); wts = ent.clone()
+variants["forward, loss planes, dQ, dE, adagrad"] = lambda: (L.score_dot_split(qh1, ql1, ent, None, d, out=bufp[:n, :m]), L.softmax_planes(bufp, n, m, labels, None, 0.0, 1.0 / n), L.score_dot_bwd_q_planes(gp, ent, dq=dq), L.score_dot_bwd_t_planes(gp, qh, ql, de), L.adagrad_step(wts, de, state, -0.0, 1e-10, 0.0, False))
+variants["adagrad"] = lambda: L.adagrad_step(wts, de, state, -0.0, 1e-10, 0.0, False)
 variants["384-MB fill"] = lambda: big.fill_(1.0)
 variants["384-MB fill then dE"] = lambda: (big.fill_(1.0), L.score_dot_bwd_t_planes(gp, qh, ql, de))
 variants["384-MB fill then dQ"] = lambda: (big.fill_(1.0), L.score_dot_bwd_q_planes(gp, ent, dq=dq))
