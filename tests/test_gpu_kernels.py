@@ -238,6 +238,41 @@ def test_score_dot_split_shapes(L, n, m, d):
     assert torch.equal(s.double(), qd.double() @ td[tidx].double().T)
 
 
+@pytest.mark.parametrize("n,m,d", [(1024, 14541, 512), (512, 40943, 512), (300, 100003, 128)])
+def test_score_dot_split_fullsize_properties(L, n, m, d):
+    """Size-independent properties of the production contraction at the BASELINE shapes, on
+    real-valued N(0, 0.1) operands, all BITWISE (the K order of every element's accumulation does
+    not depend on where the element sits in a tile or in the launch):
+      * scoring a row-permuted entity table gives the column-permuted score matrix, and the same
+        through a candidate index vector (with duplicates);
+      * scoring a permutation / a slice of the query rows gives those rows;
+      * an entity chunk [c0, c1) scores to the corresponding column slice (the chunked / sharded
+        evaluation's decomposition);
+      * a second launch reproduces the first."""
+    g = torch.Generator().manual_seed(n + m + d)
+    t = (torch.randn(m, d, generator=g) * 0.1).cuda()
+    q = (torch.randn(n, d, generator=g) * 0.1).cuda()
+    hi, lo = L.split_rows(q)
+    s = L.score_dot_split(hi, lo, t, None, d)
+    assert torch.equal(s, L.score_dot_split(hi, lo, t, None, d))
+    perm = torch.randperm(m, generator=g).cuda()
+    assert torch.equal(L.score_dot_split(hi, lo, t[perm].contiguous(), None, d), s[:, perm])
+    tidx = torch.cat([perm[:m // 2], perm[:m // 3]])  # a subset with duplicates
+    assert torch.equal(L.score_dot_split(hi, lo, t, tidx, d), s[:, tidx])
+    qperm = torch.randperm(n, generator=g).cuda()
+    hp, lp = L.split_rows(q[qperm].contiguous())
+    assert torch.equal(L.score_dot_split(hp, lp, t, None, d), s[qperm])
+    k = max(1, n // 3)
+    hs, ls = L.split_rows(q[:k].contiguous())
+    assert torch.equal(L.score_dot_split(hs, ls, t, None, d), s[:k])
+    c0, c1 = m // 5 + 3, m // 5 + 3 + (m // 8 + 1)
+    assert torch.equal(L.score_dot_split(hi, lo, t[c0:c1], None, d), s[:, c0:c1])
+    # and the values themselves, on sampled rows, against float64
+    rows = torch.arange(0, n, max(1, n // 32), device="cuda")
+    ref = (q[rows].double() @ t.double().T).cpu().numpy()
+    assert rel_err(s[rows].cpu().numpy(), ref) < 2e-5
+
+
 def test_score_dot_split_multitile(L):
     """Persistent schedule with many tiles per workgroup (m = 200,003: 782 column tiles x 4
     row tiles over <= 256 workgroups), launched repeatedly: the schedule under which an

@@ -119,6 +119,16 @@ def test_bwd_t_planes_vs_float64(L, n, m, d):
     L.score_dot_bwd_t_planes(gp, qh, ql, dt)
     torch.cuda.synchronize()
     assert float((dt.double() - ref).abs().max() / ref.abs().max()) < 1e-4
+    # reproducible bit for bit, and a column permutation of the query planes permutes dT's columns
+    dt2 = torch.full((m, d), float("nan"), device="cuda")
+    L.score_dot_bwd_t_planes(gp, qh, ql, dt2)
+    assert torch.equal(dt, dt2)
+    if d % 8 == 0:
+        cperm = torch.randperm(d, generator=torch.Generator().manual_seed(d)).cuda()
+        qhp, qlp = torch.zeros_like(qh), torch.zeros_like(ql)
+        qhp[:, :d], qlp[:, :d] = qh[:, :d][:, cperm], ql[:, :d][:, cperm]
+        L.score_dot_bwd_t_planes(gp, qhp, qlp, dt2)
+        assert torch.equal(dt2, dt[:, cperm])
     alpha = torch.tensor([-2.0], device="cuda")
     seed = torch.randn(m, d, device="cuda", generator=gen)
     acc = seed.clone()
