@@ -536,6 +536,33 @@ def score_cand(kind: int, direction: int, l_norm: float, ent: torch.Tensor, eidx
                             cand.long() if cand.dtype != torch.int64 else cand)
 
 
+class _XentColumn0(torch.autograd.Function):
+    """scale * sum_i CE(scores[i, :], label 0): the negative-sampling loss of a [n, 1 + N] score
+    block whose column 0 is the positive -- KLDivWithSoftmaxKgeLoss on the one-hot label matrix
+    (loss.py:192-213: the normalised labels stay one-hot, so KL == CE), one engine kernel for
+    loss and gradient instead of torch's log_softmax / normalize / kl_div chain."""
+
+    @staticmethod
+    def forward(ctx, scores, scale):
+        s = _rows(scores.float())
+        n = s.shape[0]
+        labels = torch.zeros(n, dtype=torch.int64, device=s.device)
+        g = torch.empty_like(s)
+        loss_rows = L.softmax_xent(s, labels, scale, g=g)
+        ctx.save_for_backward(g)
+        return loss_rows.sum() * scale
+
+    @staticmethod
+    def backward(ctx, grad):
+        (g,) = ctx.saved_tensors
+        return g * grad, None
+
+
+def xent_column0(scores: torch.Tensor, scale: float) -> torch.Tensor:
+    L.require_device(scores)
+    return _XentColumn0.apply(scores, float(scale))
+
+
 def score_spo_emb(kind: int, l_norm: float, s_emb, p_emb, o_emb) -> torch.Tensor:
     """combine="spo" on embedding rows: s, o stacked into one table."""
     n = p_emb.shape[0]

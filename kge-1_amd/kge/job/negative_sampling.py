@@ -38,6 +38,12 @@ class TrainingJobNegativeSampling(TrainingJob):
         self._implementation = impl
         self._max_chunk_size = config.get("negative_sampling.chunk_size")
         self.type_str = "negative_sampling"
+        from ..util.loss import KLDivWithSoftmaxKgeLoss
+
+        #: "kl" on the one-hot label matrix of a [chunk, 1 + N] block == cross entropy against
+        #: column 0: one engine kernel (engine.xent_column0) instead of torch's loss chain
+        self._fused_loss = (type(self.loss) is KLDivWithSoftmaxKgeLoss and bool(config.get("engine.fused_loss"))
+                            and str(self.device).startswith("cuda"))
 
     def _prepare(self):
         super()._prepare()
@@ -108,7 +114,12 @@ class TrainingJobNegativeSampling(TrainingJob):
                     labels[:, 0] = 1.0
                 fwd -= time.time()
                 scores = self._scores(tr, slot, negs[slot][lo:hi])
-                loss = self.loss(scores, labels, num_negatives=ns) / bs
+                if self._fused_loss and scores.is_cuda:
+                    from .. import engine
+
+                    loss = engine.xent_column0(scores, 1.0 / bs)
+                else:
+                    loss = self.loss(scores, labels, num_negatives=ns) / bs
                 fwd += time.time()
                 bwd -= time.time()
                 loss.backward()
