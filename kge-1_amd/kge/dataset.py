@@ -2,7 +2,7 @@
 need.  Mirrors the parts of LibKGE's kge/dataset.py the path uses: ``Dataset.create``
 (dataset.py:87-108), the ``.del`` triple loader (tab-separated, int32, dataset.py:168-182),
 ``num_entities`` / ``num_relations``, ``split`` and ``index("<split>_sp_to_o" /
-"<split>_po_to_s")`` (indexing.py:8-98, 287-301).  No pickle cache (Q13: the reference's
+"<split>_po_to_s")`` (indexing.py:8-98, 287-301).  No pickle cache (the reference's
 pickles do not reload under torch >= 2.6 anyway).
 
 ``Dataset.synthetic`` builds the published dataset shapes offline (no data ships with

@@ -51,7 +51,7 @@ def _timed(fn, *args, **kwargs):
 
 def dist_kind(kind: int, l_norm: float):
     """(kernel distance kind, sign) for TransE (-dist, transe.py:16-21) and RotatE
-    (+dist, quirk Q1, rotate.py:28-60)."""
+    (+dist, a quirk of the reference, rotate.py:28-60)."""
     if l_norm not in (1.0, 2.0):
         raise ValueError(f"l_norm={l_norm} not supported (1 or 2)")
     if kind == L.TRANSE:

@@ -3,7 +3,7 @@ and TrainingJobKvsAll (train.py:493-756) over the TrainingJob epoch loop (train.
 
 Per batch they call KgeModel.score_sp / score_po exactly as the reference does; the
 engine runs the fused gather + contraction forward and the MFMA backward.  Difference
-from the reference, by design (Q11): the per-direction ``loss.item()`` host syncs are
+from the reference, by design: the per-direction ``loss.item()`` host syncs are
 replaced by an asynchronous copy of each batch loss that the epoch loop reads one batch
 later, so the host never drains the device queue inside the epoch.
 """
@@ -187,7 +187,7 @@ class TrainingJob(Job):
             opt_t += t_opt
             # The batch loss is read one batch late (an async copy + event): the host queues
             # batch b + 1 while the device still runs batch b, instead of draining the queue
-            # every batch as loss.item() would (the reference's per-batch sync, Q11).  A NaN
+            # every batch as loss.item() would (the reference's per-batch sync).  A NaN
             # aborts one optimizer step later than in the reference.
             if torch.is_tensor(res.loss) and res.loss.is_cuda:
                 buf = torch.empty((), dtype=res.loss.dtype, pin_memory=True)
@@ -407,7 +407,7 @@ class _KvsAllGraphStep(_GraphStep):
 
     def _loss_of(self, block):
         # the recording returns both query types' losses; the reference reports the last query
-        # type that has examples in the batch (Q10), which the host knows from the split point
+        # type that has examples in the batch, which the host knows from the split point
         B = self.job.batch_size
         two = len(self.job._part_spec) == 2 and int(block[3 * B + 1]) < B
         return self.loss[1 if two else 0]
@@ -686,7 +686,7 @@ class TrainingJobKvsAll(TrainingJob):
         bwd = -time.time()
         total.backward()
         bwd += time.time()
-        # both query types' losses: the caller picks the one the reference would report (Q10)
+        # both query types' losses: the caller picks the one the reference would report
         return TrainingJob._ProcessBatchResult(per_type, bs, 0.0, fwd, bwd)
 
     def _collate(self, example_ids):
@@ -764,13 +764,13 @@ class TrainingJobKvsAll(TrainingJob):
             bwd -= time.time()
             loss.backward()
             bwd += time.time()
-            total = loss.detach()  # reference keeps the last query type's value (Q10)
+            total = loss.detach()  # reference keeps the last query type's value
         return TrainingJob._ProcessBatchResult(total if total is not None else 0.0, bs, t, fwd, bwd)
 
     def _process_batch_fused2(self, ex, bs):
         """Both query types of the batch in one engine pass (KgeModel.score_xent_parts):
         one contraction, one KL launch and one backward for the stacked sp_ and _po query
-        rows; the reported loss is the last query type's, as in the reference (Q10).
+        rows; the reported loss is the last query type's, as in the reference.
         None when a query type has no example in this batch or the scorer cannot fuse."""
         t = -time.time()
         parts, start = [], 0

@@ -3,7 +3,7 @@
 The table is an ``nn.Embedding`` so checkpoints keep the reference's state_dict keys
 (``_entity_embedder._embeddings.weight``).  On the fused scoring path the table is not
 gathered here at all: KgeModel hands the weight to the engine, whose prep kernel gathers
-the query rows and whose contraction streams the whole table (no embed_all copy, Q3).
+the query rows and whose contraction streams the whole table (no embed_all copy).
 """
 from __future__ import annotations
 

@@ -1,6 +1,6 @@
 """RotatE (rotate.py:11-145): score = || |s * rot(r) - o| ||_p over the d/2 complex
 components, rot(r) = cos r + i sin r.  Scores are POSITIVE distances, as in the
-reference (quirk Q1).  sp_ and _po stream through the engine's VALU distance kernel
+reference.  sp_ and _po stream through the engine's VALU distance kernel
 instead of materialising n x E x d/2 tensors; _po is restated as
 |e * rot(r) - o| = |e - o * conj(rot(r))| (|rot| = 1)."""
 from .. import _lib

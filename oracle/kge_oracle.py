@@ -157,7 +157,7 @@ def score_emb(model: str, s, p, o, combine: str, l_norm: float = 1.0) -> np.ndar
         if combine == "_po":
             return -_lp((o - p)[:, None, :] - s[None, :, :], l_norm)
     elif model == "rotate":
-        # rotate.py:28-60.  Scores are POSITIVE distances (quirk Q1).
+        # rotate.py:28-60.  Scores are POSITIVE distances.
         if combine == "spo":
             q = rotate_q_sp(s, p)
             d_re, d_im = _halves(q - o)

@@ -2,7 +2,7 @@
 # HBM traffic of the headline contraction kernel per launch, as MI355X_MICROARCH.md §HBM
 # prescribes: separate --pmc passes for FETCH_SIZE and WRITE_SIZE (kernel-trace only, no
 # sys/runtime trace), FETCH_SIZE doubled for the 16-B-per-lane streaming reads on gfx950.
-# Writes gpurun_out/pmc_traffic/pmc_traffic.json: copy it into this round's profiles/
+# Writes gpurun_out/pmc_traffic/pmc_traffic.json: copy it into the profiles/ directory being collected
 # directory, where bench.py reads roofline.traffic from.
 set -o pipefail
 export TMPDIR=/tmp
