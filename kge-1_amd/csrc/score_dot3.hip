@@ -66,8 +66,22 @@ __global__ void __launch_bounds__(64 * WM * WN, 1)
   uint64_t t_loop0 = 0, t_loop1 = 0;  // dev probe: K loop entry / exit of the last tile
 
   for (int it = 0;; ++it) {
-    const int tile = it * G + xcd * per_xcd + local;
-    if (tile >= ntiles) break;
+    // Round `it` covers tiles [it G, it G + count): XCD x takes the x-th eighth of them,
+    // consecutive tiles (the query tiles of one entity panel) staying on one XCD.  A last,
+    // partial round is spread evenly too: 228 tiles on 256 CUs leave 3-4 CUs idle on EVERY XCD
+    // (and use all eight L2s and fabric ports) instead of 28 on one.
+    int tile;
+    if constexpr (ABL & 128) {  // dev: the last round fills XCD after XCD
+      tile = it * G + xcd * per_xcd + local;
+      if (tile >= ntiles) break;
+    } else {
+      const int base = it * G;
+      if (base >= ntiles) break;
+      const int count = min(G, ntiles - base);
+      const int lo = (int)((int64_t)xcd * count / 8), hi = (int)((int64_t)(xcd + 1) * count / 8);
+      if (local >= hi - lo) break;  // only in the last round: no later tile either
+      tile = base + lo + local;
+    }
     const int m0 = (tile % nrt) * BM, n0 = (tile / nrt) * BN;
 
     // A planes by LDS-DMA: wave-instruction c fills rows 16c .. 16c+15 of a plane (64 B
@@ -455,6 +469,8 @@ extern "C" int kge_dev_score_dot_persist(int variant, const void* qhi, const voi
     // one wave per SIMD, 128 x 128 wave tiles, pipelined
     case 35: return launch_persist16<256, 256, 2, 2, 0, true>(h, l, ldq, t, ldt, tidx, n, m, d, s, lds, st);
     case 36: return launch_persist16<256, 256, 2, 2, 4, true>(h, l, ldq, t, ldt, tidx, n, m, d, s, lds, st);
+    case 37: return launch_persist16<256, 256, 2, 4, 128, true>(h, l, ldq, t, ldt, tidx, n, m, d, s, lds, st);
+    case 38: return launch_persist16<256, 256, 2, 4, 128 + 4, true>(h, l, ldq, t, ldt, tidx, n, m, d, s, lds, st);
     case 41: return launch_persist16<256, 256, 2, 4, 1, true>(h, l, ldq, t, ldt, tidx, n, m, d, s, lds, st);
     case 42: return launch_persist16<256, 256, 2, 4, 2, true>(h, l, ldq, t, ldt, tidx, n, m, d, s, lds, st);
     case 43: return launch_persist16<256, 256, 2, 4, 3, true>(h, l, ldq, t, ldt, tidx, n, m, d, s, lds, st);
