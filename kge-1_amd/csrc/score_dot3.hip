@@ -431,7 +431,11 @@ extern "C" int kge_score_dot_split(const void* qhi, const void* qlo, int64_t ldq
   hipStream_t st = as_stream(stream);
   const __bf16* h = (const __bf16*)qhi;
   const __bf16* l = (const __bf16*)qlo;
-#ifdef KGE_DEV_BUILD  // A/B against the plain K loop (kge_dev_dot3_pipe)
+#ifdef KGE_DEV_BUILD  // A/B against the XCD-after-XCD last round (2) and the plain K loop (0)
+  if (g_dot3_pipe == 2) {
+    if (n > 128) return launch_persist16<256, 256, 2, 4, 128, true>(h, l, ldq, t, ldt, tidx, n, m, d, s, lds, st);
+    return launch_persist16<128, 256, 2, 4, 128, true>(h, l, ldq, t, ldt, tidx, n, m, d, s, lds, st);
+  }
   if (!g_dot3_pipe) {
     if (n > 128) return launch_persist16<256, 256, 2, 4>(h, l, ldq, t, ldt, tidx, n, m, d, s, lds, st);
     return launch_persist16<128, 256, 2, 4>(h, l, ldq, t, ldt, tidx, n, m, d, s, lds, st);

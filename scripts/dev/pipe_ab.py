@@ -47,5 +47,6 @@ def run(fwd, dq, stages=3, steps=30, warmup=6, multi=True):
 
 
 for _ in range(3):
-    for fwd, dq, stages, multi in ((0, 0, 2, False), (1, 1, 3, False), (1, 1, 3, True)):
+    # forward: 0 = plain K loop, 1 = production, 2 = production loop with the XCD-after-XCD last round
+    for fwd, dq, stages, multi in ((0, 0, 2, False), (2, 1, 3, True), (1, 1, 3, True)):
         run(fwd, dq, stages, multi=multi)
