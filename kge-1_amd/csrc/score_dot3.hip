@@ -441,7 +441,16 @@ extern "C" int kge_score_dot_split(const void* qhi, const void* qlo, int64_t ldq
     return launch_persist16<128, 256, 2, 4>(h, l, ldq, t, ldt, tidx, n, m, d, s, lds, st);
   }
 #endif
-  if (n > 128) return launch_persist16<256, 256, 2, 4, 0, true>(h, l, ldq, t, ldt, tidx, n, m, d, s, lds, st);
+  // 256- or 128-row tiles (bit-identical scores): the workgroups take whole rounds of tiles and a
+  // partial last round costs a full tile time, so the cheaper of the two schedules is chosen --
+  // a 128-row tile measures 0.55 of a 256-row tile (its MFMA work is half, its entity staging the
+  // same).  E.g. 512 x 40,943: 320 tiles = 2 rounds vs 640 half tiles = 3 rounds * 0.55.
+  const int64_t slots = std::max(8, kge_num_cus() / 8 * 8);
+  const int64_t panels = (m + 255) / 256;
+  const double cost256 = (double)((((n + 255) / 256) * panels + slots - 1) / slots);
+  const double cost128 = 0.55 * (double)((((n + 127) / 128) * panels + slots - 1) / slots);
+  if (n > 128 && cost256 <= cost128)
+    return launch_persist16<256, 256, 2, 4, 0, true>(h, l, ldq, t, ldt, tidx, n, m, d, s, lds, st);
   return launch_persist16<128, 256, 2, 4, 0, true>(h, l, ldq, t, ldt, tidx, n, m, d, s, lds, st);
 }
 

@@ -39,7 +39,8 @@ def run(v):
         finally:
             out = o
         return
-    if v == 'old': L.score_dot(q, ent, None, 1, out=out)
+    if v == 'split': L.score_dot_split(qh, ql, ent, None, d, out=out)  # the production entry point (picks the tile height)
+    elif v == 'old': L.score_dot(q, ent, None, 1, out=out)
     elif v == 'old32': L.score_dot(q, ent, None, 0, out=out)
     elif isinstance(v, str) and v.startswith('p'):
         assert lib.kge_dev_score_dot_persist(int(v[1:]), qh.data_ptr(), ql.data_ptr(), ldo, ent.data_ptr(), d, None, B, E, d,
