@@ -11,7 +11,9 @@ ent = (torch.randn(m, d) * 0.1).cuda()
 q = (torch.randn(n, d) * 0.1).cuda()
 labels = torch.randint(0, m, (n,)).cuda()
 n_pad, ld = L.planes_layout(n, m)
-S = torch.randn(n_pad, ld, device="cuda")
+# KGE_S_SCALE: spread of the scores.  1 (default): peaky softmax, most gradient entries ~0;
+# 0.01: the near-uniform softmax of an untrained model (every entry ~1/m) -- denser operand bits
+S = torch.randn(n_pad, ld, device="cuda") * float(_os.environ.get("KGE_S_SCALE", "1"))
 bufp = S.clone()
 _, gp = L.softmax_planes(bufp, n, m, labels, None, 0.0, 1.0 / n)
 buf4 = torch.empty(n, (m + 3) // 4 * 4, device="cuda"); s4 = buf4[:, :m]; s4.copy_(S[:n, :m])
