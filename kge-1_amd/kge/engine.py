@@ -14,6 +14,7 @@ accumulated into ONE dense buffer, the layout torch's embedding_dense_backward p
 """
 from __future__ import annotations
 
+import contextlib
 from typing import Optional
 
 import torch
@@ -47,6 +48,53 @@ def _timed(fn, *args, **kwargs):
     b.record()
     KERNEL_EVENTS.append((a, b))
     return out
+
+
+class BatchStreams:
+    """Round-robin HIP streams for batches that do not depend on one another (scoring and
+    evaluation batches; never the steps of a training run).
+
+    One all-entities contraction seldom fills the chip to the end: its tiles come in rounds of
+    one per CU and the last round is partial, and the small launches around it (query
+    preparation, true scores, rank counting) wait behind it on the same stream.  With the next
+    batch on another stream its preparation and first tiles run on the CUs the previous batch
+    has already left.  All streams have the default priority.
+
+        with BatchStreams(device, 2) as bs:
+            for i, batch in enumerate(batches):
+                with bs.batch(i):
+                    scores = model.score_sp(s, p)      # launched on stream i % 2
+
+    Entering makes every stream wait for the caller's current stream, leaving makes the
+    caller's stream wait for all of them.  A tensor made inside ``batch(i)`` belongs to that
+    stream: use it there, or after the block has been left (and call ``record_stream`` on it
+    if it is then freed while another stream may still read it).  ``count`` <= 1 or a CPU
+    device: every batch stays on the caller's stream."""
+
+    def __init__(self, device, count: int):
+        self.device = torch.device(device)
+        self.streams = []
+        if count > 1 and self.device.type == "cuda":
+            self.streams = [torch.cuda.Stream(device=self.device) for _ in range(count)]
+
+    def __enter__(self):
+        if self.streams:
+            cur = torch.cuda.current_stream(self.device)
+            for st in self.streams:
+                st.wait_stream(cur)
+        return self
+
+    def __exit__(self, *exc):
+        if self.streams:
+            cur = torch.cuda.current_stream(self.device)
+            for st in self.streams:
+                cur.wait_stream(st)
+        return False
+
+    def batch(self, i: int):
+        if not self.streams:
+            return contextlib.nullcontext()
+        return torch.cuda.stream(self.streams[i % len(self.streams)])
 
 
 def dist_kind(kind: int, l_norm: float):

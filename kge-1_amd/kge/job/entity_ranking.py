@@ -18,6 +18,7 @@ per-shard reduction of the row-sharded multi-GPU path (kge.sharded).
 """
 from __future__ import annotations
 
+import contextlib
 import time
 from typing import Dict, List
 
@@ -96,6 +97,8 @@ class EntityRankingJob(EvaluationJob):
         self.sharded_ops = None
         self.capture_ranks = False  # keep per-query ranks in self.ranks (tests / tracing)
         self._refine = False  # set per run from engine.eval_precision
+        self._streams = None  # engine.BatchStreams, made by the first run
+        self._rank_weights = None  # [2, E] fp64: ranks 1..E and their fp32 reciprocals
         self.ranks: Dict[str, np.ndarray] = {}
 
     # ---------------------------------------------------------------- preparation
@@ -273,69 +276,18 @@ class EntityRankingJob(EvaluationJob):
         ranks_out = {f"{d}{r}": [] for d in "so" for r in self.rankings}
         epoch_time = -time.time()
         N = len(self.triples)
-        for b0 in range(0, N, self.batch_size):
-            b1 = min(N, b0 + self.batch_size)
-            B = b1 - b0
-            s, o = self._stack_e[2 * b0:2 * b0 + B], self._stack_e[2 * b0 + B:2 * b0 + 2 * B]
-            p, p_po = self._stack_p[2 * b0:2 * b0 + B], self._stack_p[2 * b0 + B:2 * b0 + 2 * B]
-            if sharded is not None:
-                # each rank counts over its own rows; one all_reduce of the int64 counts makes
-                # them global (the reference's chunk_size decomposition, entity_ranking.py:153-216)
-                tf = self._t
-                counts = sharded.rank_counts(
-                    s, p, o, (self._f["sp"][0][b0:], self._f["sp"][1]), (self._f["po"][0][b0:], self._f["po"][1]),
-                    (tf["sp"][0][b0:], tf["sp"][1]) if tf is not None else None,
-                    (tf["po"][0][b0:], tf["po"][1]) if tf is not None else None,
-                    p_inverse=(p + self.dataset.num_relations()) if self._two_sided else None)
-                rk = torch.empty(2, nrank, B, dtype=torch.int64, device=dev)
-                for di, d in enumerate("os"):
-                    sharded.ops.rank_hist_multi(counts[di, 0, :nrank * B], counts[di, 1, :nrank * B], B,
-                                                self.tie_handling, rk[di].view(-1), hists_sharded[di])
-                    if self.capture_ranks:
-                        for ri, r in enumerate(self.rankings):
-                            ranks_out[f"{d}{r}"].append(rk[di, ri])
-                if group_hists:
-                    self._count_groups(group_hists, rk.permute(1, 0, 2), b0, B)
-                continue
-            o_true = self.model.score_spo(s, p, o, "o").view(-1).float().contiguous()
-            # score_spo(.., "s") is the same triple score unless the model scores the two
-            # directions differently (reciprocal relations): skip the second launch then
-            s_true = o_true if not self._two_sided else self.model.score_spo(s, p, o, "s").view(-1).float().contiguous()
-            (fp_sp, fp_po, f_col), tstack = self._stacked
-            tp_sp, tp_po, t_col = tstack if tstack is not None else (None, None, None)
-            part_a = (o, o_true, fp_sp[b0:], tp_sp[b0:] if tp_sp is not None else None)
-            part_b = (s, s_true, fp_po[b0:], tp_po[b0:] if tp_po is not None else None)
-            single = chunk >= E
-            counts = (torch.empty if single else torch.zeros)(2, nrank * 2 * B, dtype=torch.int64, device=dev)
-            rk = torch.empty(nrank * 2 * B, dtype=torch.int64, device=dev)
-            for c0 in range(0, E, chunk):
-                c1 = min(E, c0 + chunk)
-                subset = None if single else torch.arange(c0, c1, device=dev)
-                # [2B, C]: the (s, p, ?) rows on top of the (?, p, o) rows, one engine pass
-                scores, q = self.model.score_sp_po_rows(s, p, o, subset, want_q=self._refine, p_po=p_po)
-                refine = None
-                if q is not None:
-                    if tmax is None:
-                        tmax = _lib.row_norm_max(ent_rows)
-                    refine = (q, ent_rows[c0:c1], refine_band(q.shape[1]), tmax)
-                elif self._refine:
-                    raise RuntimeError("engine.eval_precision bf16x3_refined: the engine returned no fp32 query "
-                                       "rows to rescore near-ties with")
-                # a single chunk finishes the batch in the same launch: ranks + histograms
-                _lib.rank_rows(scores, B, c0, part_a, part_b, f_col, t_col, counts[0], counts[1],
-                               accumulate=not single, tie_handling=self.tie_handling if single else None,
-                               ranks=rk if single else None, hists=hists_flat if single else None,
-                               rows_per_hist=B, refine=refine)
-                del scores
-            if not single:
-                _lib.rank_hist_multi(counts[0], counts[1], B, self.tie_handling, rk, hists_flat)
-            rk = rk.view(nrank, 2, B)
-            if group_hists:
-                self._count_groups(group_hists, rk, b0, B)
-            if self.capture_ranks:
-                for di, d in enumerate("os"):
-                    for ri, r in enumerate(self.rankings):
-                        ranks_out[f"{d}{r}"].append(rk[ri, di])
+        if self._refine:
+            tmax = _lib.row_norm_max(ent_rows)  # ahead of the batches: every stream reads it
+        # independent batches take turns on engine.eval_streams HIP streams; every accumulation
+        # across batches (histograms, group counts) is an atomic add of exact small integers.
+        # The row-sharded path stays on one stream: its collectives are ordered per process.
+        if self._streams is None:
+            from ..engine import BatchStreams
+
+            self._streams = BatchStreams(dev, self.config.get("engine.eval_streams"))
+        with self._streams if sharded is None else contextlib.nullcontext():
+            self._rank_batches(N, E, chunk, sharded, nrank, hists_flat, hists_sharded, group_hists, ranks_out,
+                               ent_rows, tmax)
         epoch_time += time.time()
         metrics = {}
         if hists_sharded is not None:
@@ -354,9 +306,10 @@ class EntityRankingJob(EvaluationJob):
                         keyed[g + "_head"], keyed[g + "_tail"] = h[:, 1, gi], h[:, 0, gi]
                 else:
                     keyed[f"{name}_{g}"] = h[:, :, gi].sum(1)
-        for key, h in keyed.items():  # entity_ranking.py:376-387: per key, every ranking
-            for ri, r in enumerate(self.rankings):
-                metrics.update(self._compute_metrics(h[ri], RANKING_SUFFIX[r] + ("_" + key if key != "all" else "")))
+        # entity_ranking.py:376-387: per key, every ranking -- all of them in one device pass
+        suffixes = [RANKING_SUFFIX[r] + ("_" + key if key != "all" else "")
+                    for key in keyed for r in self.rankings]
+        metrics.update(self._compute_metrics_stacked(torch.cat(list(keyed.values())), suffixes))
         if self.capture_ranks:
             self.ranks = {k: torch.cat(v).cpu().numpy() if v else np.zeros(0, np.int64)
                           for k, v in ranks_out.items()}
@@ -369,16 +322,103 @@ class EntityRankingJob(EvaluationJob):
             self.model.train()
         return trace
 
+    def _rank_batches(self, N, E, chunk, sharded, nrank, hists_flat, hists_sharded, group_hists, ranks_out,
+                      ent_rows, tmax):
+        """The batch loop of _run_ranking: adds every batch's ranks to the histograms."""
+        dev = self.device
+        for bi, b0 in enumerate(range(0, N, self.batch_size)):
+            with (self._streams.batch(bi) if sharded is None else contextlib.nullcontext()):
+                b1 = min(N, b0 + self.batch_size)
+                B = b1 - b0
+                s, o = self._stack_e[2 * b0:2 * b0 + B], self._stack_e[2 * b0 + B:2 * b0 + 2 * B]
+                p, p_po = self._stack_p[2 * b0:2 * b0 + B], self._stack_p[2 * b0 + B:2 * b0 + 2 * B]
+                if sharded is not None:
+                    # each rank counts over its own rows; one all_reduce of the int64 counts makes
+                    # them global (the reference's chunk_size decomposition, entity_ranking.py:153-216)
+                    tf = self._t
+                    counts = sharded.rank_counts(
+                        s, p, o, (self._f["sp"][0][b0:], self._f["sp"][1]), (self._f["po"][0][b0:], self._f["po"][1]),
+                        (tf["sp"][0][b0:], tf["sp"][1]) if tf is not None else None,
+                        (tf["po"][0][b0:], tf["po"][1]) if tf is not None else None,
+                        p_inverse=(p + self.dataset.num_relations()) if self._two_sided else None)
+                    rk = torch.empty(2, nrank, B, dtype=torch.int64, device=dev)
+                    for di, d in enumerate("os"):
+                        sharded.ops.rank_hist_multi(counts[di, 0, :nrank * B], counts[di, 1, :nrank * B], B,
+                                                    self.tie_handling, rk[di].view(-1), hists_sharded[di])
+                        if self.capture_ranks:
+                            for ri, r in enumerate(self.rankings):
+                                ranks_out[f"{d}{r}"].append(rk[di, ri])
+                    if group_hists:
+                        self._count_groups(group_hists, rk.permute(1, 0, 2), b0, B)
+                    continue
+                o_true = self.model.score_spo(s, p, o, "o").view(-1).float().contiguous()
+                # score_spo(.., "s") is the same triple score unless the model scores the two
+                # directions differently (reciprocal relations): skip the second launch then
+                s_true = o_true if not self._two_sided else self.model.score_spo(s, p, o, "s").view(-1).float().contiguous()
+                (fp_sp, fp_po, f_col), tstack = self._stacked
+                tp_sp, tp_po, t_col = tstack if tstack is not None else (None, None, None)
+                part_a = (o, o_true, fp_sp[b0:], tp_sp[b0:] if tp_sp is not None else None)
+                part_b = (s, s_true, fp_po[b0:], tp_po[b0:] if tp_po is not None else None)
+                single = chunk >= E
+                counts = (torch.empty if single else torch.zeros)(2, nrank * 2 * B, dtype=torch.int64, device=dev)
+                rk = torch.empty(nrank * 2 * B, dtype=torch.int64, device=dev)
+                for c0 in range(0, E, chunk):
+                    c1 = min(E, c0 + chunk)
+                    subset = None if single else torch.arange(c0, c1, device=dev)
+                    # [2B, C]: the (s, p, ?) rows on top of the (?, p, o) rows, one engine pass
+                    scores, q = self.model.score_sp_po_rows(s, p, o, subset, want_q=self._refine, p_po=p_po)
+                    refine = None
+                    if q is not None:
+                        if tmax is None:
+                            tmax = _lib.row_norm_max(ent_rows)
+                        refine = (q, ent_rows[c0:c1], refine_band(q.shape[1]), tmax)
+                    elif self._refine:
+                        raise RuntimeError("engine.eval_precision bf16x3_refined: the engine returned no fp32 query "
+                                           "rows to rescore near-ties with")
+                    # a single chunk finishes the batch in the same launch: ranks + histograms
+                    _lib.rank_rows(scores, B, c0, part_a, part_b, f_col, t_col, counts[0], counts[1],
+                                   accumulate=not single, tie_handling=self.tie_handling if single else None,
+                                   ranks=rk if single else None, hists=hists_flat if single else None,
+                                   rows_per_hist=B, refine=refine)
+                    del scores
+                if not single:
+                    _lib.rank_hist_multi(counts[0], counts[1], B, self.tie_handling, rk, hists_flat)
+                rk = rk.view(nrank, 2, B)
+                if group_hists:
+                    self._count_groups(group_hists, rk, b0, B)
+                if self.capture_ranks:
+                    for di, d in enumerate("os"):
+                        for ri, r in enumerate(self.rankings):
+                            ranks_out[f"{d}{r}"].append(rk[ri, di])
+
     def _compute_metrics(self, rank_hist: torch.Tensor, suffix: str = "") -> Dict[str, float]:
-        """entity_ranking.py:553-577 (fp32 histogram arithmetic like the reference)."""
-        metrics = {}
-        n = torch.sum(rank_hist).item()
-        ranks = torch.arange(1, self.dataset.num_entities() + 1, device=rank_hist.device).float()
-        metrics["mean_rank" + suffix] = (torch.sum(rank_hist * ranks).item() / n) if n > 0.0 else 0.0
-        rr = 1.0 / ranks
-        metrics["mean_reciprocal_rank" + suffix] = (torch.sum(rank_hist * rr).item() / n) if n > 0.0 else 0.0
+        """entity_ranking.py:553-577 for one rank histogram."""
+        return self._compute_metrics_stacked(rank_hist.view(1, -1), [suffix])
+
+    def _compute_metrics_stacked(self, rank_hists: torch.Tensor, suffixes: List[str]) -> Dict[str, float]:
+        """entity_ranking.py:553-577 for a stack of rank histograms [K, E] (one suffix each):
+        mean rank, mean reciprocal rank and hits@k of every histogram in one device pass and ONE
+        device-to-host copy instead of three host round trips per histogram.  The operands are
+        the reference's fp32 ones (counts, ranks, fp32 reciprocals, fp32 hits quotients); the two
+        weighted sums accumulate in fp64, which differs from an fp32 sum only by that sum's own
+        rounding."""
+        E = self.dataset.num_entities()
+        K = rank_hists.shape[0]
         kmax = max(self.hits_at_k_s)
-        hits = (torch.cumsum(rank_hist[:kmax], dim=0) / n).tolist() if n > 0.0 else [0.0] * kmax
-        for k in self.hits_at_k_s:
-            metrics["hits_at_{}{}".format(k, suffix)] = hits[k - 1]
+        if self._rank_weights is None or self._rank_weights.device != rank_hists.device:
+            ranks = torch.arange(1, E + 1, device=rank_hists.device).float()
+            self._rank_weights = torch.stack([ranks.double(), (1.0 / ranks).double()])  # fp32 values
+        h64 = rank_hists.double()
+        n = rank_hists.sum(1, keepdim=True)  # exact: integer counts far below 2^24
+        hits = torch.cumsum(rank_hists[:, :kmax], dim=1) / n  # fp32 quotients
+        table = torch.cat([n.double(), (h64 * self._rank_weights[0]).sum(1, keepdim=True),
+                           (h64 * self._rank_weights[1]).sum(1, keepdim=True), hits.double()], dim=1).tolist()
+        metrics = {}
+        for row, suffix in zip(table, suffixes):
+            cnt = row[0]
+            metrics["mean_rank" + suffix] = row[1] / cnt if cnt > 0.0 else 0.0
+            metrics["mean_reciprocal_rank" + suffix] = row[2] / cnt if cnt > 0.0 else 0.0
+            for k in self.hits_at_k_s:
+                metrics["hits_at_{}{}".format(k, suffix)] = row[3 + k - 1] if cnt > 0.0 else 0.0
+        assert len(table) == K == len(suffixes)
         return metrics
