@@ -205,6 +205,55 @@ def test_entity_ranking_metrics_per_group_vs_golden(tag):
         assert trace[k] == pytest.approx(v, rel=1e-6, abs=1e-9), k
 
 
+@pytest.mark.parametrize("streams", [1, 2, 3])
+def test_entity_ranking_same_ranks_on_any_number_of_streams(streams):
+    """engine.eval_streams: the evaluation batches take turns on that many HIP streams; the
+    ranks and every metric are the reference's whatever the number, twice in a row (the second
+    run reuses the job's streams and their cached buffers)."""
+    f = np.load(os.path.join(GOLDEN, "eval_normal.npz"))
+    ref_metrics = json.loads(str(f["metrics"]))["full"]
+    meta = json.loads(str(f["meta"]))
+    assert len(f["tri_valid"]) > 2 * meta["batch_size"]  # three batches
+    job, trace = eval_job(f, "full", "bf16x3_refined", {"engine.eval_streams": streams})
+    assert len(job._streams.streams) == (streams if streams > 1 else 0)
+    for run in range(2):
+        for k, v in job.ranks.items():
+            np.testing.assert_array_equal(v, f[f"full_{k}"], err_msg=f"{k} run {run}")
+        for k, v in ref_metrics.items():
+            assert trace[k] == pytest.approx(v, rel=1e-6, abs=1e-9), k
+        trace = job.run()
+
+
+def test_batch_streams_score_sp_identical_to_one_stream():
+    """kge.engine.BatchStreams: score_sp batches launched on alternating streams give the
+    scores of the same batches on the caller's stream, bit for bit, and leaving the block
+    orders the caller's stream behind every batch."""
+    from kge import engine
+
+    f = np.load(os.path.join(GOLDEN, "eval_normal.npz"))
+    meta = json.loads(str(f["meta"]))
+    m = make_model("complex", meta["dim"], meta["E"], meta["R"], f["ent"], f["rel"])
+    g = torch.Generator().manual_seed(3)
+    s = torch.randint(0, meta["E"], (12, 257), generator=g).cuda()
+    p = torch.randint(0, meta["R"], (12, 257), generator=g).cuda()
+    with torch.no_grad():
+        ref = [m.score_sp(s[i], p[i]) for i in range(12)]
+        for count in (2, 3):
+            outs = []
+            with engine.BatchStreams("cuda", count) as lanes:
+                assert len(lanes.streams) == count
+                for i in range(12):
+                    with lanes.batch(i):
+                        outs.append(m.score_sp(s[i], p[i]))
+            total = torch.stack(outs).sum()  # on the caller's stream, after the block
+            assert torch.equal(torch.stack(outs), torch.stack(ref))
+            assert torch.isfinite(total)
+    with engine.BatchStreams("cuda", 1) as lanes:  # one stream: the caller's own
+        assert lanes.streams == []
+        with lanes.batch(0):
+            assert torch.cuda.current_stream() == torch.cuda.default_stream()
+
+
 def test_entity_ranking_bf16x3_normal_near_ties_only():
     """bf16x3 scoring on real-valued data: a rank may differ from the reference's only where
     unfiltered competitors lie within the score tolerance of the true score -- asserted per
