@@ -176,6 +176,17 @@ def shard_bounds(num_entities: int, world: int, rank: int):
     return lo, min(num_entities, lo + per)
 
 
+class _Ticket:
+    """An exchange in flight (submit_queries_local): the collective's work handle (None once
+    waited for, or when it completed synchronously), the gathered rows, this rank's rows (kept
+    alive until the gather has read them), the query direction and whether the rows are packed
+    bf16 planes."""
+    __slots__ = ("work", "q_all", "q_local", "direction", "planes")
+
+    def __init__(self, work, q_all, q_local, direction, planes):
+        self.work, self.q_all, self.q_local, self.direction, self.planes = work, q_all, q_local, direction, planes
+
+
 class RowShardedScorer:
     def __init__(self, ent_shard: torch.Tensor, lo: int, hi: int, num_entities: int, rel: torch.Tensor, ops,
                  group=None):
@@ -251,7 +262,12 @@ class RowShardedScorer:
         """Start the exchange of a shard-affine batch (queries_local) without waiting for it:
         the query rows are prepared on the current stream and their all_gather is issued
         asynchronously (RCCL runs it on its own stream), so the caller can score the previous
-        batch meanwhile.  Returns a ticket for ``score_submitted``."""
+        batch meanwhile.  Returns a ticket for ``score_submitted``.
+
+        e, p may hold SEVERAL batches back to back (k B queries): one preparation launch and
+        one collective then serve k scoring steps -- fewer, larger collectives: the per-call
+        host cost of the collective is paid once per k steps (``score_submitted(ticket, part)``
+        scores the gathered rows in k blocks)."""
         # shard-affine by contract: every query entity is one of this rank's rows
         planes = getattr(self.ops, "planes_ok", None) is not None and self.ops.planes_ok(self.ent, direction)
         if planes:  # bf16 hi / lo planes, packed per row: no split pass on the receiving side
@@ -260,16 +276,30 @@ class RowShardedScorer:
             q = self.ops.prep(direction, self.ent, e - self.lo, self.rel, p).contiguous()
         out = torch.empty((self.world * q.shape[0], q.shape[1]), dtype=q.dtype, device=q.device)
         work = all_gather_into_tensor(out, q, group=self.group, async_op=True)
-        return (work, out, q, direction, planes)  # q is kept alive until the gather has read it
+        return _Ticket(work, out, q, direction, planes)
 
-    def score_submitted(self, ticket) -> torch.Tensor:
-        """Local slice [W*B, hi - lo] of the scores of a batch started by submit_queries_local."""
-        work, q_all, _, direction, planes = ticket
-        if work is not None:
-            work.wait()  # the current stream waits for the gather; the host does not block
-        if planes:
-            return self.ops.score_planes(q_all, self._win(direction, self.ent))
-        return self.ops.score(q_all, self._win(direction, self.ent))
+    def score_submitted(self, ticket, part=None) -> torch.Tensor:
+        """Local slice [W*B, hi - lo] of the scores of a batch started by submit_queries_local.
+
+        part = (x, k): only the x-th of k equal blocks of the gathered rows, for a ticket of k
+        batches per rank.  The gathered rows are rank-major (rank 0's k B rows, then rank 1's,
+        ...), so block x holds W B consecutive rows: the queries of ranks and local batches
+        (w, j) with x W <= w k + j < (x + 1) W.  Over x = 0 .. k-1 every submitted query is
+        scored exactly once; which step scores it is the only difference to k single-batch
+        tickets."""
+        if ticket.work is not None:
+            ticket.work.wait()  # the current stream waits for the gather; the host does not block
+            ticket.work = None
+        q_all = ticket.q_all
+        if part is not None:
+            x, k = part
+            if q_all.shape[0] % k or not 0 <= x < k:
+                raise ValueError(f"part {part} of {q_all.shape[0]} gathered rows")
+            rows = q_all.shape[0] // k
+            q_all = q_all[x * rows:(x + 1) * rows]
+        if ticket.planes:
+            return self.ops.score_planes(q_all, self._win(ticket.direction, self.ent))
+        return self.ops.score(q_all, self._win(ticket.direction, self.ent))
 
     def topk(self, scores_local: torch.Tensor, k: int):
         """All-gather of per-shard top-k (score, global entity id), merged on every rank."""

@@ -177,5 +177,14 @@ def test_pipelined_exchange_world1_matches_direct_scoring(L, kind, prec, d):
             assert torch.equal(outs[i], direct)
             ref = engine.score_all(k, L.DIR_SP, L.PRECISIONS[prec], 1.0, ent, s[i], rel, p[i], shard, None)
             assert torch.equal(outs[i], ref)
+        # three batches in ONE exchange, scored block by block: the same scores
+        group = sh.submit_queries_local(s.reshape(-1), p.reshape(-1))
+        for i in range(3):
+            assert torch.equal(sh.score_submitted(group, (i, 3)), outs[i])
+        assert group.work is None  # waited for once
+        with pytest.raises(ValueError):
+            sh.score_submitted(group, (0, 5))  # 144 rows do not split into 5 blocks
+        with pytest.raises(ValueError):
+            sh.score_submitted(group, (3, 3))
     finally:
         dist.destroy_process_group()

@@ -180,3 +180,68 @@ def test_row_sharded_local_queries_world2():
     for rank, lo, hi, local, _, _ in res:
         np.testing.assert_allclose(local, full[:, lo:hi], rtol=1e-5, atol=1e-5)
     assert all(errs)
+
+
+def _worker_grouped(rank, world, port, out_q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from kge.sharded import RowShardedScorer, shard_bounds
+
+        g = torch.Generator().manual_seed(0)
+        E, R, d, B, k = 41, 4, 8, 5, 3
+        ent = torch.randn(E, d, generator=g)
+        rel = torch.randn(R, d, generator=g)
+        lo, hi = shard_bounds(E, world, rank)
+        sc = RowShardedScorer(ent[lo:hi].clone(), lo, hi, E, rel, OracleOps())
+        gq = torch.Generator().manual_seed(300 + rank)
+        s = torch.randint(lo, hi, (k, B), generator=gq)
+        p = torch.randint(0, R, (k, B), generator=gq)
+        # k single-batch exchanges, the next one in flight while a batch is scored
+        tickets = [sc.submit_queries_local(s[0], p[0])]
+        single = []
+        for i in range(k):
+            if i + 1 < k:
+                tickets.append(sc.submit_queries_local(s[i + 1], p[i + 1]))
+            single.append(sc.score_submitted(tickets.pop(0)).numpy())
+        # the same k batches in ONE exchange, scored in k blocks
+        group = sc.submit_queries_local(s.reshape(-1), p.reshape(-1))
+        blocks = [sc.score_submitted(group, (x, k)).numpy() for x in range(k)]
+        out_q.put((rank, lo, hi, single, blocks, s.numpy(), p.numpy()))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_row_sharded_grouped_exchange_world2():
+    """One all_gather for k batches per rank (submit_queries_local on k B queries) and
+    score_submitted(ticket, (x, k)): block x holds the gathered rows [x W B, (x + 1) W B) in
+    rank-major order, every query is scored exactly once, and the scores are those of the k
+    single-batch exchanges."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_grouped, args=(r, world, port, q)) for r in range(world)]
+    for pr in procs:
+        pr.start()
+    res = sorted([q.get(timeout=120) for _ in range(world)], key=lambda x: x[0])
+    for pr in procs:
+        pr.join(timeout=60)
+        assert pr.exitcode == 0
+    g = torch.Generator().manual_seed(0)
+    E, R, d, B, k = 41, 4, 8, 5, 3
+    ent = torch.randn(E, d, generator=g).double().numpy()
+    rel = torch.randn(R, d, generator=g).double().numpy()
+    # gathered order: rank 0's k B queries, then rank 1's
+    s_g = np.concatenate([r[5].reshape(-1) for r in res])
+    p_g = np.concatenate([r[6].reshape(-1) for r in res])
+    full = K.prep_sp("complex", ent[s_g], rel[p_g]) @ ent.T  # [W k B, E]
+    for rank, lo, hi, single, blocks, _, _ in res:
+        got = np.concatenate(blocks)
+        assert got.shape == (world * k * B, hi - lo)
+        np.testing.assert_allclose(got, full[:, lo:hi], rtol=1e-5, atol=1e-5)
+        # the same rows as the single-batch steps: step i holds (rank w, batch i) at rows w B ..
+        for i in range(k):
+            for w in range(world):
+                np.testing.assert_array_equal(single[i][w * B:(w + 1) * B],
+                                              got[(w * k + i) * B:(w * k + i + 1) * B])
