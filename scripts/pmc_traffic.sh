@@ -13,7 +13,7 @@ i=0
 for ctr in FETCH_SIZE WRITE_SIZE; do
   i=$((i+1))
   timeout -k 10 240 rocprofv3 --pmc $ctr --kernel-trace --output-format csv -d $OUT/p$i -o run -- \
-    python3 $GRAFT_REPO_ROOT/bench.py --no-cpu --no-extras --no-probe --steps 10 --warmup 3 > $OUT/bench$i.json 2> $OUT/err$i.txt \
+    python3 $GRAFT_REPO_ROOT/bench.py --no-cpu --no-extras --no-probe --streams 1 --steps 10 --warmup 3 > $OUT/bench$i.json 2> $OUT/err$i.txt \
     || { echo "pmc pass $ctr failed"; tail -5 $OUT/err$i.txt; exit 1; }
 done
 python3 - "$OUT" "$OUT/pmc_traffic.json" <<'EOF'
@@ -33,7 +33,7 @@ out = {"kernel": name, "dispatches": {k: len(v) for k, v in vals.items()},
        "read_bytes": 2 * fetch_kb * 1024, "write_bytes": write_kb * 1024,
        "traffic_bytes": 2 * fetch_kb * 1024 + write_kb * 1024,
        "method": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes, kernel-trace only) over "
-                 "bench.py --no-cpu --no-extras --no-probe; per-dispatch mean; FETCH_SIZE x2 (gfx950: 16-B/lane "
+                 "bench.py --no-cpu --no-extras --no-probe --streams 1; per-dispatch mean; FETCH_SIZE x2 (gfx950: 16-B/lane "
                  "streaming reads tallied at half, MI355X_MICROARCH.md §HBM); WRITE_SIZE as reported "
                  "(16-B/lane score stores)"}
 json.dump(out, open(dst, "w"), indent=1)
