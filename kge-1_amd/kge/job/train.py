@@ -166,37 +166,46 @@ class TrainingJob(Job):
         epoch_time = -time.time()
         fwd = bwd = prep = opt_t = 0.0
         n_batches = 0
-        pending = None  # (pinned host copy of a batch loss, its event, batch size, penalty)
+        pending = None  # (host copy of a batch loss, its event, batch size, host copy of the penalty)
 
         def settle(p):
-            nonlocal sum_loss
-            buf, ev, size, penalty = p
+            nonlocal sum_loss, sum_penalty
+            buf, ev, size, pen = p
             if ev is not None:
                 ev.synchronize()
             v = float(buf)
+            pen = float(pen)
             sum_loss += v * size
-            if self.abort_on_nan and math.isnan(v + penalty):
+            sum_penalty += pen
+            if self.abort_on_nan and math.isnan(v + pen):
                 raise FloatingPointError("Cost became nan, aborting training job")
+
+        def host_copy(x):
+            """A 0-dim device tensor on its way to pinned host memory (stream-ordered, not waited
+            for); anything else as it is."""
+            if torch.is_tensor(x) and x.is_cuda:
+                buf = torch.empty((), dtype=x.dtype, pin_memory=True)
+                buf.copy_(x.detach(), non_blocking=True)
+                return buf, True
+            return x, False
 
         for batch_index, example_ids in enumerate(self._batches()):
             for f in self.pre_batch_hooks:
                 f(self)
             batch = self._collate(example_ids)
             res, penalty, t_opt = self.train_step(batch_index, batch)
-            sum_penalty += penalty
             opt_t += t_opt
-            # The batch loss is read one batch late (an async copy + event): the host queues
-            # batch b + 1 while the device still runs batch b, instead of draining the queue
-            # every batch as loss.item() would (the reference's per-batch sync).  A NaN
-            # aborts one optimizer step later than in the reference.
-            if torch.is_tensor(res.loss) and res.loss.is_cuda:
-                buf = torch.empty((), dtype=res.loss.dtype, pin_memory=True)
-                buf.copy_(res.loss.detach(), non_blocking=True)
+            # The batch loss and penalty are read one batch late (async copies + an event): the
+            # host queues batch b + 1 while the device still runs batch b, instead of draining the
+            # queue every batch as loss.item() / penalty.item() would (the reference's per-batch
+            # syncs).  A NaN aborts one optimizer step later than in the reference.
+            loss_h, a = host_copy(res.loss)
+            pen_h, b = host_copy(penalty)
+            ev = None
+            if a or b:
                 ev = torch.cuda.Event()
                 ev.record()
-                cur = (buf, ev, res.size, penalty)
-            else:
-                cur = (float(res.loss), None, res.size, penalty)
+            cur = (loss_h, ev, res.size, pen_h)
             if pending is not None:
                 settle(pending)
             pending = cur
@@ -234,18 +243,36 @@ class TrainingJob(Job):
         if graph is not None:
             res = graph.run(batch_index, batch)
             if res is not None:
-                return res, 0.0, 0.0
+                return res, graph.penalty if graph.penalty is not None else 0.0, 0.0
         self.optimizer.zero_grad()
         res = self.process_batch(batch_index, batch)
-        penalty = 0.0
-        for _, pv in self.model.penalty(epoch=self.epoch, batch_index=batch_index, batch=batch):
-            pv.backward()
-            penalty += pv.item()
-            if graph is not None:
-                graph.disable()  # a penalty syncs on its value: not recordable
+        penalty = self._penalty_backward(batch_index, batch)
         t0 = time.time()
         self.optimizer.step()
         return res, penalty, time.time() - t0
+
+    def _penalty_backward(self, batch_index, batch):
+        """The penalty terms of the batch (train.py:320-337): backward on each, and their sum as a
+        0-dim tensor (0.0 when nothing regularises) -- not read on the host here."""
+        total = 0.0
+        for _, pv in self.model.penalty(epoch=self.epoch, batch_index=batch_index, batch=batch):
+            pv.backward()
+            total = pv.detach() + total
+        return total
+
+    def _penalties_recordable(self, weighted_ok: bool) -> bool:
+        """Whether the model's penalty terms can be part of a recorded step: none at all, or Lp
+        terms of lookup embedders (frequency-weighted ones only when the recorded batch carries
+        its triples)."""
+        from ..model.embedder.lookup_embedder import LookupEmbedder
+
+        m = self.model
+        for e in (m.get_s_embedder(), m.get_p_embedder(), m.get_o_embedder()):
+            if not getattr(e, "penalty_active", lambda: True)():
+                continue
+            if not isinstance(e, LookupEmbedder) or (e.penalty_weighted() and not weighted_ok):
+                return False
+        return True
 
 
 class _GraphStep:
@@ -277,6 +304,7 @@ class _GraphStep:
         self.pinned = []  # two pinned host staging buffers (+ their copy events) for the batch
         self.turn = 0
         self.loss = None  # recorded 0-dim loss
+        self.penalty = None  # recorded 0-dim sum of the penalty terms (None: nothing regularises)
         self.stepped = []
         self.warm = 0
         self.disabled = False
@@ -298,6 +326,12 @@ class _GraphStep:
 
     def _recorded_batch(self):
         return {"cols": self.static.view(len(TrainingJob1vsAll.INDEX_BLOCK), self.job.batch_size)}
+
+    def _penalty_batch(self):
+        """The batch the penalty terms are recorded with: the triples as columns of the block."""
+        cols = self._recorded_batch()["cols"]
+        s_row, o_row, p_row = (TrainingJob1vsAll.INDEX_BLOCK.index(c) for c in (S, O, P))
+        return {"triples": torch.stack((cols[s_row], cols[p_row], cols[o_row]), 1)}
 
     # ---- the step
     def run(self, batch_index, batch):
@@ -352,6 +386,7 @@ class _GraphStep:
         try:
             with torch.cuda.graph(g):
                 res = job.process_batch(batch_index, self._recorded_batch())
+                pen = job._penalty_backward(batch_index, self._penalty_batch())
                 opt.step()
         except Exception as e:  # not recordable: this and every later batch run eagerly
             for p, s in steps.items():
@@ -369,6 +404,7 @@ class _GraphStep:
             return False
         self.graph = g
         self.loss = res.loss
+        self.penalty = pen if torch.is_tensor(pen) else None
         self.stepped = [p for grp in opt.param_groups for p in grp["params"] if p.grad is not None]
         return True
 
@@ -404,6 +440,9 @@ class _KvsAllGraphStep(_GraphStep):
         B = self.job.batch_size
         st = self.static
         return {"stacked": (st[:B], st[B:2 * B], st[2 * B:3 * B + 1], st[3 * B + 1:3 * B + 2], st[3 * B + 2:])}
+
+    def _penalty_batch(self):
+        return {}  # unweighted terms only (TrainingJobKvsAll._prepare): no indexes needed
 
     def _loss_of(self, block):
         # the recording returns both query types' losses; the reference reports the last query
@@ -444,6 +483,7 @@ class TrainingJob1vsAll(TrainingJob):
                 and hasattr(opt, "graph_safe") and opt.graph_safe()
                 and self.kge_lr_scheduler._lr_scheduler is None
                 and not self.pre_batch_hooks  # e.g. the embedding normaliser re-creates the weights
+                and self._penalties_recordable(weighted_ok=True)
                 and self.model._lookup_tables() is not None):
             self._graph_step = _GraphStep(self)
 
@@ -625,6 +665,7 @@ class TrainingJobKvsAll(TrainingJob):
                 and self.kge_lr_scheduler._lr_scheduler is None
                 and not self.pre_batch_hooks
                 and not sharding_enabled(self.config)
+                and self._penalties_recordable(weighted_ok=False)  # its triples vary in number
                 and self._stacked_applicable()):
             self._graph_step = _KvsAllGraphStep(self)
 
@@ -690,7 +731,44 @@ class TrainingJobKvsAll(TrainingJob):
         return TrainingJob._ProcessBatchResult(per_type, bs, 0.0, fwd, bwd)
 
     def _collate(self, example_ids):
-        return {"examples": example_ids}
+        batch = {"examples": example_ids}
+        if self._weighted_penalty():
+            batch["triples"] = self._batch_triples(example_ids.numpy())
+        return batch
+
+    def _weighted_penalty(self) -> bool:
+        """Whether a penalty term weights embeddings by their frequency in the batch's triples."""
+        m = self.model
+        return any(getattr(e, "penalty_weighted", lambda: False)()
+                   for e in (m.get_s_embedder(), m.get_p_embedder(), m.get_o_embedder()))
+
+    def _batch_triples(self, ex: np.ndarray) -> torch.Tensor:
+        """All true triples of the batch, one per (query, label) in batch order (train.py:625-674):
+        what weighted penalties count index frequencies on."""
+        qt_of = np.searchsorted(np.asarray(self.query_last_example), ex, side="right")
+        starts = np.concatenate(([0], np.asarray(self.query_last_example[:-1], dtype=np.int64)))
+        lens = np.zeros(len(ex), dtype=np.int64)
+        for qi, ix in enumerate(self.query_indexes):
+            sel = np.nonzero(qt_of == qi)[0]
+            local = ex[sel] - starts[qi]
+            lens[sel] = ix.offsets[local + 1] - ix.offsets[local]
+        first = np.zeros(len(ex) + 1, dtype=np.int64)
+        np.cumsum(lens, out=first[1:])
+        triples = np.zeros((int(first[-1]), 3), dtype=np.int64)
+        for qi, (qt, ix) in enumerate(zip(self.query_types, self.query_indexes)):
+            sel = np.nonzero(qt_of == qi)[0]
+            if len(sel) == 0:
+                continue
+            local = ex[sel] - starts[qi]
+            n = lens[sel]
+            rows = np.repeat(first[sel], n) + np.arange(int(n.sum()), dtype=np.int64) - np.repeat(np.cumsum(n) - n, n)
+            pos = np.repeat(ix.offsets[local], n) + np.arange(int(n.sum()), dtype=np.int64) - np.repeat(
+                np.cumsum(n) - n, n)
+            k1_col, k2_col, target_col = (S, P, O) if qt == "sp_" else (P, O, S)
+            triples[rows, k1_col] = np.repeat(ix.keys[local, 0], n)
+            triples[rows, k2_col] = np.repeat(ix.keys[local, 1], n)
+            triples[rows, target_col] = ix.values[pos]
+        return torch.from_numpy(triples)
 
     def _queries(self, qi, sel):
         """(query pairs [n, 2], label CSR pointer [n + 1], label columns) of the selected

@@ -73,8 +73,17 @@ class LookupEmbedder(KgeEmbedder):
         """Whether penalty() returns a term (lp regularisation with a non-zero weight)."""
         return self.regularize != "" and self.get_option("regularize_weight") != 0.0
 
+    def penalty_weighted(self) -> bool:
+        """Whether the penalty weights each row by its frequency among the batch's indexes."""
+        return self.penalty_active() and bool(self.get_option("regularize_args.weighted"))
+
     def penalty(self, **kwargs) -> List:
-        """Lp regularisation (lookup_embedder.py:112-158)."""
+        """Lp regularisation (lookup_embedder.py:112-158).
+
+        While a HIP graph is being recorded the weighted form sums over the OCCURRENCES of the
+        indexes instead of over unique indexes times their counts: the same sum (a row that
+        occurs c times contributes c equal terms) without torch.unique, whose output shape
+        depends on the data and cannot be recorded."""
         result = super().penalty(**kwargs)
         if self.regularize == "" or self.get_option("regularize_weight") == 0.0:
             return result
@@ -83,6 +92,12 @@ class LookupEmbedder(KgeEmbedder):
         if not self.get_option("regularize_args.weighted"):
             params = self._embeddings_all()
             result += [(f"{self.configuration_key}.L{p}_penalty", (w / p * params.norm(p=p) ** p).sum())]
+        elif kwargs["indexes"].is_cuda and torch.cuda.is_current_stream_capturing():
+            indexes = kwargs["indexes"]
+            params = self._embeddings.weight.index_select(0, indexes)
+            if p % 2 == 1:
+                params = torch.abs(params)
+            result += [(f"{self.configuration_key}.L{p}_penalty", (w / p * params ** p).sum() / len(indexes))]
         else:
             unique_indexes, counts = torch.unique(kwargs["indexes"], return_counts=True)
             params = self._embeddings(unique_indexes)

@@ -708,6 +708,77 @@ def gen_eval_metrics_per():
     return fn
 
 
+def gen_penalty_fixture():
+    """Three batch steps of the reference's batch loop (train.py:309-429) WITH embedding
+    penalties: weighted L3 on the entities and weighted L2 on the relations (lookup_embedder.py:
+    112-158 -- the weights come from the batch's triples, which KvsAll builds per label,
+    train.py:625-674), for 1vsAll (ComplEx) and KvsAll (DistMult); plus an unweighted L2 run of
+    1vsAll.  Per batch: the loss, every penalty term, and the tables after the steps."""
+    from kge.job import TrainingJob
+
+    E, R, splits = make_dataset_splits()
+    out = dict(tri_train=splits["train"].astype(np.int32))
+    cases = [("1vsall_w", "complex", "1vsAll", True, 128), ("kvsall_w", "distmult", "KvsAll", True, 64),
+             ("1vsall_u", "complex", "1vsAll", False, 128)]
+    dim, nb = 32, 3
+    meta = dict(E=E, R=R, dim=dim, num_batches=nb, lr=0.2, cases={}, torch=torch.__version__)
+    for tag, model, ttype, weighted, bs in cases:
+        folder = os.path.join(TMP, "ds_pen_" + tag)
+        write_dataset(folder, E, R, splits)
+        extra = {"train.type": ttype, "train.optimizer": "Adagrad", "train.optimizer_args": {"lr": 0.2},
+                 "train.loss": "kl", "train.batch_size": bs,
+                 "lookup_embedder.regularize": "lp", "lookup_embedder.regularize_args.weighted": weighted,
+                 f"{model}.entity_embedder.regularize_weight": 0.05,
+                 f"{model}.relation_embedder.regularize_weight": 0.02,
+                 f"{model}.entity_embedder.regularize_args.p": 3,
+                 f"{model}.relation_embedder.regularize_args.p": 2}
+        config = ds_config(model, dim, folder, E, R, extra)
+        ds = Dataset.create(config, folder=folder)
+        gen = torch.Generator().manual_seed(21)
+        ent = torch.randn(E, dim, generator=gen) * 0.1
+        rel = torch.randn(R, dim, generator=gen) * 0.1
+        job = TrainingJob.create(config, ds)
+        set_tables(job.model, ent, rel)
+        job._prepare()
+        out[f"{tag}_ent0"], out[f"{tag}_rel0"] = ent.numpy(), rel.numpy()
+        losses, pens = [], []
+        if ttype == "1vsAll":
+            perm = torch.randperm(len(splits["train"]), generator=gen)[:nb * bs]
+            train = torch.from_numpy(splits["train"])
+            batches = [{"triples": train[perm[b * bs:(b + 1) * bs]].long()} for b in range(nb)]
+            out[f"{tag}_batches"] = np.stack([b["triples"].numpy() for b in batches])
+        else:
+            collate = job._get_collate_fun()
+            perm = torch.randperm(job.num_examples, generator=gen)[:nb * bs].tolist()
+            batches = [collate(perm[b * bs:(b + 1) * bs]) for b in range(nb)]
+            out[f"{tag}_examples"] = np.array(perm, dtype=np.int64).reshape(nb, bs)
+            for b, batch in enumerate(batches):
+                out[f"{tag}_triples_{b}"] = batch["triples"].numpy()
+        keys = None
+        for b, batch in enumerate(batches):
+            job.optimizer.zero_grad()
+            res = job._process_batch(b, batch)
+            terms = job.model.penalty(epoch=1, batch_index=b, num_batches=nb, batch=batch)
+            for _, t in terms:
+                t.backward()
+            keys = [k for k, _ in terms]
+            pens.append([t.item() for _, t in terms])
+            out[f"{tag}_g_ent_{b}"] = job.model._entity_embedder._embeddings.weight.grad.detach().clone().numpy()
+            out[f"{tag}_g_rel_{b}"] = job.model._relation_embedder._embeddings.weight.grad.detach().clone().numpy()
+            job.optimizer.step()
+            losses.append(res.avg_loss)
+        out[f"{tag}_losses"] = np.array(losses, dtype=np.float64)
+        out[f"{tag}_penalties"] = np.array(pens, dtype=np.float64)
+        out[f"{tag}_ent1"] = job.model._entity_embedder._embeddings.weight.detach().numpy()
+        out[f"{tag}_rel1"] = job.model._relation_embedder._embeddings.weight.detach().numpy()
+        meta["cases"][tag] = dict(model=model, train_type=ttype, weighted=weighted, batch_size=bs,
+                                  penalty_keys=keys, extra={k: v for k, v in extra.items() if "regular" in k})
+    out["meta"] = np.array(json.dumps(meta))
+    fn = os.path.join(OUT, "train_penalties.npz")
+    np.savez_compressed(fn, **out)
+    return fn
+
+
 def gen_shapes():
     rows = []
     for model, d in [("rotate", 64), ("rotate", 1024), ("rescal", 16), ("rescal", 32),
@@ -738,7 +809,8 @@ def main():
         written.append(gen_shapes())
     extra = {"eval_fullsize": gen_eval_fullsize, "kvsall": gen_kvsall_fixture,
              "ns_rotate": lambda: gen_ns_fixture("rotate"), "ns_complex": lambda: gen_ns_fixture("complex"),
-             "toy": gen_toy_fixture, "score_so": gen_score_so_fixture, "eval_metrics_per": gen_eval_metrics_per}
+             "toy": gen_toy_fixture, "score_so": gen_score_so_fixture, "eval_metrics_per": gen_eval_metrics_per,
+             "penalties": gen_penalty_fixture}
     for name, fn in extra.items():
         if only is None or name in only:
             written.append(fn())

@@ -195,6 +195,61 @@ def test_kvsall_batch_queries_host_csr():
             assert got == sorted(answers[qi][key]), (qi, key)
 
 
+def test_kvsall_batch_triples_and_weighted_penalty_vs_reference():
+    """TrainingJobKvsAll._collate under a frequency-weighted penalty: the batch's true triples
+    (one per query and label, train.py:625-674) equal the reference collate's, and the penalty
+    terms of the first batch (lookup_embedder.py:112-158; plain torch, no engine) equal the
+    reference's values -- in the unique-index form and in the per-occurrence form a recorded
+    step uses."""
+    import json
+    import os
+
+    from kge import Config, Dataset
+    from kge.job import TrainingJob
+
+    f = np.load(os.path.join(os.path.dirname(__file__), "golden", "train_penalties.npz"))
+    meta = json.loads(str(f["meta"]))
+    case = meta["cases"]["kvsall_w"]
+    c = Config()
+    c.set("model", case["model"])
+    c._import(case["model"])
+    c.set("job.device", "cpu")
+    c.set("lookup_embedder.dim", meta["dim"])
+    c.set("train.type", "KvsAll")
+    c.set("train.batch_size", case["batch_size"])
+    c.set("dataset.num_entities", meta["E"])
+    c.set("dataset.num_relations", meta["R"])
+    c.set("verbose", False)
+    for k, v in case["extra"].items():
+        c.set(k, v)
+    ds = Dataset(c, None)
+    ds._triples = {"train": torch.from_numpy(f["tri_train"].astype(np.int32))}
+    job = TrainingJob.create(c, ds)
+    job._prepare()
+    assert job._weighted_penalty()
+    with torch.no_grad():
+        job.model._entity_embedder._embeddings.weight.copy_(torch.from_numpy(f["kvsall_w_ent0"]))
+        job.model._relation_embedder._embeddings.weight.copy_(torch.from_numpy(f["kvsall_w_rel0"]))
+    for b in range(meta["num_batches"]):
+        batch = job._collate(torch.from_numpy(f["kvsall_w_examples"][b]))
+        np.testing.assert_array_equal(batch["triples"].numpy(), f[f"kvsall_w_triples_{b}"])
+    batch = job._collate(torch.from_numpy(f["kvsall_w_examples"][0]))
+    terms = job.model.penalty(epoch=1, batch_index=0, batch=batch)
+    assert [k for k, _ in terms] == case["penalty_keys"]
+    np.testing.assert_allclose([t.item() for _, t in terms], f["kvsall_w_penalties"][0], rtol=1e-6)
+    # the per-occurrence form of the weighted term: the same sum without torch.unique
+    emb = job.model._entity_embedder
+    idx = batch["triples"][:, 0]
+    occ = (0.05 / 3 * emb._embeddings.weight.index_select(0, idx).abs() ** 3).sum() / len(idx)
+    assert occ.item() == pytest.approx(f["kvsall_w_penalties"][0][0], rel=1e-6)
+    # no weighted penalty: the batch carries no triples (nothing reads them)
+    c2 = c.clone()
+    c2.set("lookup_embedder.regularize_args.weighted", False)
+    job2 = TrainingJob.create(c2, ds)
+    job2._prepare()
+    assert "triples" not in job2._collate(torch.arange(5))
+
+
 def test_dataset_relation_types_and_frequency_percentiles():
     """Dataset.index("relation_types" / "relations_per_type" / "frequency_percentiles") against the
     reference's own indexes (captured in eval_metrics_per.npz) and against the oracle's loops on a
