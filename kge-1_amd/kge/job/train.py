@@ -309,10 +309,14 @@ class _GraphStep:
         self.warm = 0
         self.disabled = False
         self.error = None  # why recording was abandoned, if it was
+        self.hyper = None  # the optimizer's (lr, weight decay, eps) per group at recording time
 
     def disable(self):
         self.disabled = True
         self.graph = None
+
+    def _hyper(self):
+        return [(g["lr"], g.get("weight_decay"), g.get("eps")) for g in self.job.optimizer.param_groups]
 
     # ---- what a batch looks like (1vsAll: the [5, B] index block of TrainingJob1vsAll.INDEX_BLOCK)
     def _capacity(self) -> int:
@@ -341,6 +345,10 @@ class _GraphStep:
         if self.graph is None and self.warm < self.WARMUP:
             self.warm += 1
             return None  # the caller runs this batch eagerly
+        if self.graph is not None and self._hyper() != self.hyper:
+            # the learning rate is an argument of the recorded optimizer kernel: after an lr
+            # scheduler (or anyone else) changed it, this batch is recorded anew
+            self.graph = None
         t = -time.time()
         block = self._block(batch)
         if block is None or block.numel() > self._capacity():
@@ -403,6 +411,7 @@ class _GraphStep:
             self.disable()
             return False
         self.graph = g
+        self.hyper = self._hyper()
         self.loss = res.loss
         self.penalty = pen if torch.is_tensor(pen) else None
         self.stepped = [p for grp in opt.param_groups for p in grp["params"] if p.grad is not None]
@@ -481,7 +490,6 @@ class TrainingJob1vsAll(TrainingJob):
                 and isinstance(self.loss, KLDivWithSoftmaxKgeLoss)
                 and torch.device(self.device).type == "cuda"
                 and hasattr(opt, "graph_safe") and opt.graph_safe()
-                and self.kge_lr_scheduler._lr_scheduler is None
                 and not self.pre_batch_hooks  # e.g. the embedding normaliser re-creates the weights
                 and self._penalties_recordable(weighted_ok=True)
                 and self.model._lookup_tables() is not None):
@@ -662,7 +670,6 @@ class TrainingJobKvsAll(TrainingJob):
                 and 1 <= len(self.query_types) <= 2
                 and torch.device(self.device).type == "cuda"
                 and hasattr(opt, "graph_safe") and opt.graph_safe()
-                and self.kge_lr_scheduler._lr_scheduler is None
                 and not self.pre_batch_hooks
                 and not sharding_enabled(self.config)
                 and self._penalties_recordable(weighted_ok=False)  # its triples vary in number

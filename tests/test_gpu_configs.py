@@ -332,7 +332,9 @@ def test_c1_toy_complex_options_trajectory_vs_reference(precision):
     ref_epochs = json.loads(str(f["epochs"]))
     ref_valids = json.loads(str(f["valids"]))
     assert len(traces) == len(ref_epochs) and len(job.valid_trace) == len(ref_valids)
-    assert job._graph_step is None  # an lr scheduler and a penalty keep the step off the graph path
+    # the penalty is part of the recorded step, and the step is recorded anew after each lr change
+    assert job._graph_step is not None and job._graph_step.graph is not None, job._graph_step.error
+    assert job._graph_step.hyper[0][0] == ref_epochs[-1]["lr"][0] < meta["lr"]  # the last epoch's rate
     for t, r in zip(traces, ref_epochs):
         assert t["epoch"] == r["epoch"] and t["batches"] == r["batches"] and t["size"] == r["size"]
         assert t["lr"] == pytest.approx(r["lr"], rel=1e-12), f"lr schedule at epoch {r['epoch']}"

@@ -352,3 +352,30 @@ def test_penalty_trajectories_vs_reference(tag, graph):
     for got, ref in ((e1, f[tag + "_ent1"]), (r1, f[tag + "_rel1"])):
         off = np.abs(got - ref) > 1e-4
         assert off.mean() < 1e-3 and np.abs(got - ref).max() < 2e-3, (off.sum(), np.abs(got - ref).max())
+
+
+def test_graph_step_recorded_anew_when_the_learning_rate_changes():
+    """The learning rate is an argument of the recorded optimizer kernel: after a scheduler
+    changes it the next batch is recorded anew, and the run follows the eager one."""
+    runs = {}
+    for graph in (False, True):
+        job, tr = _job(graph, "fp32")
+        losses, recordings = [], []
+        for b in range(9):
+            if b == 5:
+                for group in job.optimizer.param_groups:
+                    group["lr"] = 0.02
+            res, _, _ = job.train_step(b, {"triples": tr[b * 64:(b + 1) * 64].long()})
+            losses.append(float(res.loss))
+            if graph:
+                recordings.append(job._graph_step.graph)
+        if graph:
+            assert recordings[1] is None and recordings[2] is not None
+            assert recordings[4] is recordings[2] and recordings[5] is not recordings[4]
+            assert recordings[8] is recordings[5]
+            assert job._graph_step.hyper[0][0] == 0.02
+        ent = job.model._entity_embedder._embeddings.weight
+        runs[graph] = (np.array(losses), ent.detach().cpu().numpy())
+    np.testing.assert_allclose(runs[True][0], runs[False][0], rtol=1e-5)
+    off = np.abs(runs[True][1] - runs[False][1]) > 1e-5
+    assert off.mean() < 0.05 and np.abs(runs[True][1] - runs[False][1]).max() < 2e-2
