@@ -1,6 +1,7 @@
 """Optimizer / LR-scheduler factories (kge/util/optimizer.py:6-71): torch.optim classes
 selected by name with ``train.optimizer_args``; "Adagrad" runs on the engine's fused step
-(engine.fused_optimizer, default on) with torch.optim.Adagrad's semantics and state."""
+(engine.fused_optimizer, default on) with torch.optim.Adagrad's semantics and state, "Adam"
+with device-side step counters so that the recorded training step can end in it."""
 from __future__ import annotations
 
 import torch
@@ -76,6 +77,28 @@ class FusedAdagrad(torch.optim.Adagrad):
             self.state[p]["step"] += 1
 
 
+class CapturableAdam(torch.optim.Adam):
+    """torch.optim.Adam with its step counters on the device (capturable=True): every step
+    issues the same device work with the same arguments, so a training step that ends in it can
+    be recorded as a HIP graph and replayed (TrainingJob graph_step).  Same arithmetic and
+    state_dict layout as torch.optim.Adam."""
+
+    def __init__(self, params, **args):
+        args.setdefault("capturable", True)
+        super().__init__(params, **args)
+
+    def graph_safe(self) -> bool:
+        for group in self.param_groups:
+            if not group["capturable"] or group["differentiable"]:
+                return False
+            if not all(p.is_cuda for p in group["params"]):
+                return False
+        return True
+
+    def advance_steps(self, params):
+        """Nothing to do on the host: the replayed step advances the device-side counters."""
+
+
 class KgeOptimizer:
     @staticmethod
     def create(config, model=None, params=None):
@@ -87,6 +110,9 @@ class KgeOptimizer:
         args = config.get("train.optimizer_args")
         if name == "Adagrad" and config.get("engine.fused_optimizer"):
             return FusedAdagrad(params, **args)
+        if (name == "Adam" and config.get("engine.graph_step") and params
+                and all(p.is_cuda for p in params)):
+            return CapturableAdam(params, **args)
         try:
             cls = getattr(torch.optim, name)
         except AttributeError as e:
