@@ -12,6 +12,7 @@ c.set("job.device", "cuda")
 c.set("lookup_embedder.dim", 512)
 c.set("lookup_embedder.initialize_args", {"mean": 0.0, "std": 0.1})
 c.set("eval.split", "test"); c.set("eval.batch_size", 1024)
+c.set("engine.eval_streams", 1)  # per-kernel durations: launches overlapping on two streams stretch each other
 ds = Dataset.synthetic(c, "fb15k-237", seed=0)
 model = KgeModel.create(c, ds)
 model.eval()
