@@ -241,14 +241,19 @@ class _ScoreXentPlanes(torch.autograd.Function):
     (kge_score_dot_bwd_q_planes / _t_planes): no fp32 copy of Q, no split per tile, dT written
     (not accumulated).  Returns (total, parts): total = scale * sum of all rows' losses carries
     the gradient; parts = scale * (sum of the first batch's rows, sum of the second's) is
-    detached (for reporting)."""
+    detached (for reporting).
+
+    tab: the candidate rows when they are not the table the queries are gathered from (e.g.
+    a dropout copy of the entity table, queries built from dropped rows); None: ent itself,
+    whose gradient then collects both the candidates' and the queries' contributions."""
 
     @staticmethod
-    def forward(ctx, kind, ent, rel, sq, labels, l_ptr, smoothing, scale):
+    def forward(ctx, kind, ent, rel, sq, labels, l_ptr, smoothing, scale, tab=None):
         ent, rel = _rows(ent), _rows(rel)
-        n, m = sq.eidx.numel(), ent.shape[0]
+        cand = ent if tab is None else _rows(tab)
+        n, m = sq.eidx.numel(), cand.shape[0]
         d_e, d_r = ent.shape[1], rel.shape[1]
-        qw, tab_w = L.query_width(kind, d_e), window(kind, sq.dir_a, ent)
+        qw, tab_w = L.query_width(kind, d_e), window(kind, sq.dir_a, cand)
         n_pad, ld = L.planes_layout(n, m)
         buf = torch.empty(n_pad, ld, device=ent.device, dtype=torch.float32)
         ldp = (qw + 31) // 32 * 32
@@ -261,9 +266,9 @@ class _ScoreXentPlanes(torch.autograd.Function):
                             out=(None, hi[:n], lo[:n]))
         _timed(L.score_dot_split, hi[:n], lo[:n], tab_w, None, qw, out=buf[:n, :m])
         loss_rows, _ = L.softmax_planes(buf, n, m, labels, l_ptr, smoothing, scale)
-        ctx.meta = (kind, n, m, d_e, d_r, sq.dir_a, sq.dir_b, sq.n_a, sq.n_a_dev is not None)
+        ctx.meta = (kind, n, m, d_e, d_r, sq.dir_a, sq.dir_b, sq.n_a, sq.n_a_dev is not None, tab is None)
         ctx.save_for_backward(ent, rel, hi, lo, buf, sq.eidx, sq.ridx,
-                              sq.n_a_dev if sq.n_a_dev is not None else sq.eidx.new_empty(0))
+                              sq.n_a_dev if sq.n_a_dev is not None else sq.eidx.new_empty(0), cand)
         total, per_part = L.loss_sums(loss_rows, sq.n_a, scale, sq.n_a_dev)  # one launch, fixed order
         ctx.mark_non_differentiable(per_part)
         ctx.set_materialize_grads(False)  # no zero tensor for the detached parts' gradient
@@ -272,24 +277,38 @@ class _ScoreXentPlanes(torch.autograd.Function):
     @staticmethod
     def backward(ctx, g_total, _g_parts):
         if g_total is None:
-            return (None,) * 8
-        kind, n, m, d_e, d_r, dir_a, dir_b, n_a, has_dev = ctx.meta
-        ent, rel, hi, lo, buf, eidx, ridx, n_a_dev = ctx.saved_tensors
+            return (None,) * 9
+        kind, n, m, d_e, d_r, dir_a, dir_b, n_a, has_dev, same = ctx.meta
+        ent, rel, hi, lo, buf, eidx, ridx, n_a_dev, cand = ctx.saved_tensors
         gl = g_total.reshape(1).float().contiguous()  # read by the kernels from device memory
         gp = L.GradPlanes(buf, n, m)
-        tab_w = window(kind, dir_a, ent)
+        tab_w = window(kind, dir_a, cand)
         dq = L.score_dot_bwd_q_planes(gp, tab_w, gscale=gl)
         if tab_w.shape[1] == d_e:  # the GEMM covers every column: write, do not accumulate
-            d_ent = torch.empty_like(ent)
-            L.score_dot_bwd_t_planes(gp, hi, lo, d_ent, gscale=gl, accumulate=False)
+            d_cand = torch.empty_like(cand)
+            L.score_dot_bwd_t_planes(gp, hi, lo, d_cand, gscale=gl, accumulate=False)
         else:  # CP: the contraction sees one half of the entity rows
-            d_ent = torch.zeros_like(ent)
-            L.score_dot_bwd_t_planes(gp, hi, lo, window(kind, dir_a, d_ent), gscale=gl, accumulate=False)
+            d_cand = torch.zeros_like(cand)
+            L.score_dot_bwd_t_planes(gp, hi, lo, window(kind, dir_a, d_cand), gscale=gl, accumulate=False)
+        d_ent = d_cand if same else torch.zeros_like(ent)
         d_rel = torch.zeros_like(rel)
         L.prep_query_bwd2(kind, dir_a, dir_b, n_a, n_a_dev if has_dev else None, ent, eidx, rel, ridx, d_e, d_r, dq,
                           d_ent, d_rel)
         return (None, d_ent if ctx.needs_input_grad[1] else None, d_rel if ctx.needs_input_grad[2] else None,
-                None, None, None, None, None)
+                None, None, None, None, None, None if same or not ctx.needs_input_grad[8] else d_cand)
+
+
+_ARANGE = {}
+
+
+def _arange(n: int, device) -> torch.Tensor:
+    """0 .. n-1 as int64 on the device, kept (a recorded step must not re-create it per replay)."""
+    key = (n, str(device))
+    if key not in _ARANGE:
+        if torch.cuda.is_current_stream_capturing():
+            return torch.arange(n, device=device, dtype=torch.int64)  # recorded with the step
+        _ARANGE[key] = torch.arange(n, device=device, dtype=torch.int64)
+    return _ARANGE[key]
 
 
 def _planes_applicable(kind, precision, ent, direction) -> bool:
@@ -317,6 +336,16 @@ def score_all_xent(kind: int, direction: int, precision: int, l_norm: float, ent
     if tab is ent and tidx is None and eidx is not None and _planes_applicable(kind, precision, ent, direction):
         total, _ = _ScoreXentPlanes.apply(kind, ent, rel, StackedQueries.of([(direction, eidx, ridx)]),
                                           L.idx64(labels), L.idx64(l_ptr), float(smoothing), float(scale))
+        return total
+    if (tab is not ent and tidx is None and eidx is None and ridx is None and ent.dim() == 2 and rel.dim() == 2
+            and ent.shape[0] == rel.shape[0] and ent.shape[1] == tab.shape[1]
+            and ent.dtype == rel.dtype == torch.float32
+            and _planes_applicable(kind, precision, tab, direction)):
+        # query rows given as tensors (one entity row and one relation row per query, e.g. after
+        # dropout) against their own candidate table: the same plane-fed pass, rows taken in order
+        rows = _arange(ent.shape[0], ent.device)
+        total, _ = _ScoreXentPlanes.apply(kind, ent, rel, StackedQueries.of([(direction, rows, rows)]),
+                                          L.idx64(labels), L.idx64(l_ptr), float(smoothing), float(scale), tab)
         return total
     return _ScoreXent.apply(kind, direction, precision, float(l_norm), ent, L.idx64(eidx), rel, L.idx64(ridx),
                             tab, L.idx64(tidx), L.idx64(labels), L.idx64(l_ptr), float(smoothing), float(scale))

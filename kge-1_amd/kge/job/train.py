@@ -492,7 +492,9 @@ class TrainingJob1vsAll(TrainingJob):
                 and hasattr(opt, "graph_safe") and opt.graph_safe()
                 and not self.pre_batch_hooks  # e.g. the embedding normaliser re-creates the weights
                 and self._penalties_recordable(weighted_ok=True)
-                and self.model._lookup_tables() is not None):
+                # plain lookups, or lookups with dropout (torch's dropout is recorded with the
+                # step: every replay draws new masks)
+                and (self.model._lookup_tables() is not None or self.model._lookup_embedders_with_dropout())):
             self._graph_step = _GraphStep(self)
 
     def _collate(self, example_ids):

@@ -167,6 +167,17 @@ class RelationalScorer(KgeBase):
         return engine.score_all_xent(self.engine_kind, d, self.precision(), self.l_norm(), ent, e_idx, rel, p_idx,
                                      ent, None, labels, scale, l_ptr, smoothing)
 
+    def score_emb_xent(self, e_emb: Tensor, p_emb: Tensor, cand: Tensor, direction: str, labels: Tensor,
+                       scale: float, l_ptr: Optional[Tensor] = None, smoothing: float = 0.0) -> Tensor:
+        """score_lookup_xent for queries given as embedding rows (one entity row and one
+        relation row per query) against the candidate rows cand: what a lookup embedder with
+        dropout hands over -- dropped query rows and a dropped copy of the table."""
+        from .. import engine, _lib
+
+        d = _lib.DIR_SP if direction == "sp_" else _lib.DIR_PO
+        return engine.score_all_xent(self.engine_kind, d, self.precision(), self.l_norm(), e_emb, None, p_emb, None,
+                                     cand, None, labels, scale, l_ptr, smoothing)
+
     def score_lookup_xent2(self, ent: Tensor, rel: Tensor, part_a, part_b, scale: float,
                            smoothing: float = 0.0) -> Optional[Tensor]:
         """Both halves of a training step in one engine pass: part = (direction "sp_" / "_po",
@@ -366,6 +377,29 @@ class KgeModel(KgeBase):
             return e.weight_for_scoring(), r.weight_for_scoring()
         return None
 
+    def _lookup_embedders_with_dropout(self) -> bool:
+        """Whether the fused losses apply in their embedding-row form: lookup embedders (one
+        shared by subjects and objects) that only add dropout, and an engine-backed scorer."""
+        from .embedder.lookup_embedder import LookupEmbedder
+
+        e, r = self.get_s_embedder(), self.get_p_embedder()
+        return (self._scorer.engine_kind is not None and isinstance(e, LookupEmbedder)
+                and isinstance(r, LookupEmbedder) and e is self.get_o_embedder())
+
+    def _xent_dropout(self, e_idx, p_idx, direction, labels, scale, l_ptr=None, smoothing=0.0):
+        """The fused loss with dropout in the embedders: dropped query rows and a dropped copy of
+        the entity table (torch's dropout, drawn in the order score_sp / score_po draw them),
+        scored and differentiated in one engine pass; autograd carries the gradients through
+        the dropout masks and the lookups."""
+        ent_e, rel_e = self.get_s_embedder(), self.get_p_embedder()
+        if direction == "sp_":  # kge_model.py:639-659: s, p, then all objects
+            e, p = ent_e.embed(e_idx), rel_e.embed(p_idx)
+            cand = ent_e.embed_all()
+        else:  # kge_model.py:661-682: all subjects, o, then p
+            cand = ent_e.embed_all()
+            e, p = ent_e.embed(e_idx), rel_e.embed(p_idx)
+        return self._scorer.score_emb_xent(e, p, cand, direction, labels, scale, l_ptr, smoothing)
+
     # ----------------------------------------------------------------- scoring API
     def score_spo(self, s: Tensor, p: Tensor, o: Tensor, direction=None) -> Tensor:
         """Scores of triples (s_i, p_i, o_i) -> [n] (kge_model.py:620-637)."""
@@ -403,14 +437,14 @@ class KgeModel(KgeBase):
         without an engine kernel): the caller then scores and applies its loss itself."""
         tabs = self._lookup_tables()
         if tabs is None:
-            return None
+            return self._xent_dropout(s, p, "sp_", o, scale) if self._lookup_embedders_with_dropout() else None
         return self._scorer.score_lookup_xent(tabs[0], tabs[1], s, p, "sp_", o, scale)
 
     def score_po_xent(self, p: Tensor, o: Tensor, s: Tensor, scale: float) -> Optional[Tensor]:
         """scale * sum_i CrossEntropy(score_po(p, o)[i, :], s[i]) (see score_sp_xent)."""
         tabs = self._lookup_tables()
         if tabs is None:
-            return None
+            return self._xent_dropout(o, p, "_po", s, scale) if self._lookup_embedders_with_dropout() else None
         return self._scorer.score_lookup_xent(tabs[0], tabs[1], o, p, "_po", s, scale)
 
     # --- both directions of a training step in one engine pass
@@ -472,6 +506,8 @@ class KgeModel(KgeBase):
         engine; row i's positives are l_col[l_ptr[i]:l_ptr[i+1]].  None when not fusable."""
         tabs = self._lookup_tables()
         if tabs is None:
+            if self._lookup_embedders_with_dropout():
+                return self._xent_dropout(s, p, "sp_", l_col, scale, l_ptr, smoothing)
             return None
         return self._scorer.score_lookup_xent(tabs[0], tabs[1], s, p, "sp_", l_col, scale, l_ptr, smoothing)
 
@@ -480,6 +516,8 @@ class KgeModel(KgeBase):
         """KvsAll (?, p, o) queries; see score_sp_kl."""
         tabs = self._lookup_tables()
         if tabs is None:
+            if self._lookup_embedders_with_dropout():
+                return self._xent_dropout(o, p, "_po", l_col, scale, l_ptr, smoothing)
             return None
         return self._scorer.score_lookup_xent(tabs[0], tabs[1], o, p, "_po", l_col, scale, l_ptr, smoothing)
 

@@ -431,3 +431,68 @@ def test_graph_step_with_adam_matches_eager():
     # elements may step the other way (as with Adagrad above)
     off = np.abs(runs[True][1] - runs[False][1]) > 1e-5
     assert off.mean() < 0.05 and np.abs(runs[True][1] - runs[False][1]).max() < 0.2
+
+
+@pytest.mark.parametrize("precision", ["bf16x3", "fp32"])
+@pytest.mark.parametrize("direction", ["sp_", "_po"])
+def test_fused_loss_with_embedder_dropout_matches_unfused(direction, precision):
+    """lookup_embedder.dropout > 0 in training mode: score_sp_xent / score_po_xent score dropped
+    query rows against a dropped copy of the table in one engine pass.  Under the same seed the
+    unfused path (score_sp / score_po, torch cross entropy) draws the same masks: same loss, same
+    gradients."""
+    job, tr = _job(False, precision)
+    m = job.model
+    for e in (m._entity_embedder, m._relation_embedder):
+        e.dropout.p = 0.3
+    m.train()
+    assert m._lookup_tables() is None and m._lookup_embedders_with_dropout()
+    t = tr[:64].long().cuda()
+    s, p, o = t[:, 0], t[:, 1], t[:, 2]
+    ent, rel = m._entity_embedder._embeddings.weight, m._relation_embedder._embeddings.weight
+    out = {}
+    for fused in (True, False):
+        ent.grad = rel.grad = None
+        torch.manual_seed(5)
+        if fused:
+            loss = m.score_sp_xent(s, p, o, 1.0 / 64) if direction == "sp_" else m.score_po_xent(p, o, s, 1.0 / 64)
+        else:
+            scores = m.score_sp(s, p) if direction == "sp_" else m.score_po(p, o)
+            loss = torch.nn.functional.cross_entropy(scores, o if direction == "sp_" else s, reduction="sum") / 64
+        loss.backward()
+        out[fused] = (float(loss.detach()), ent.grad.detach().clone(), rel.grad.detach().clone())
+    tol = 2e-5 if precision == "fp32" else 2e-4
+    assert out[True][0] == pytest.approx(out[False][0], rel=1e-5)
+    for a, b in zip(out[True][1:], out[False][1:]):
+        assert (a - b).abs().max().item() <= tol * b.abs().max().item()
+    # the masks are redrawn per call
+    torch.manual_seed(5)
+    first = float(m.score_sp_xent(s, p, o, 1.0 / 64).detach())
+    assert float(m.score_sp_xent(s, p, o, 1.0 / 64).detach()) != first
+
+
+def test_graph_step_with_embedder_dropout_records_and_redraws_masks():
+    """Dropout in the lookup embedders keeps the step on the recorded path: torch's dropout is
+    part of the recording and every replay draws new masks (replaying one batch twice gives two
+    different losses); the loss falls over the run like the eager job's."""
+    runs = {}
+    for graph in (True, False):
+        job, tr = _job(graph, "bf16x3")
+        for e in (job.model._entity_embedder, job.model._relation_embedder):
+            e.dropout.p = 0.2
+        job._prepare()  # decides on the graph step with the dropout in place
+        torch.manual_seed(1)
+        losses = []
+        for rep in range(5):
+            for b in range(8):
+                res, _, _ = job.train_step(b, {"triples": tr[b * 64:(b + 1) * 64].long()})
+                losses.append(float(res.loss))
+        recorded = job._graph_step is not None and job._graph_step.graph is not None
+        assert recorded == graph, getattr(job._graph_step, "error", None)
+        runs[graph] = np.array(losses)
+        if graph:
+            a = float(job.train_step(0, {"triples": tr[:64].long()})[0].loss)
+            b = float(job.train_step(0, {"triples": tr[:64].long()})[0].loss)
+            assert a != b
+    for losses in runs.values():
+        assert np.isfinite(losses).all() and losses[-8:].mean() < 0.8 * losses[:8].mean()
+    assert runs[True][-8:].mean() == pytest.approx(runs[False][-8:].mean(), rel=0.25)
