@@ -766,6 +766,14 @@ def other_configs(device):
     sec, _ = _job_step_time(c, "fb15k-237", 512)
     res["c4_ns_rotate1024_fb15k237_b512_n1024_step_ms"] = round(sec * 1e3, 3)
     res["c4_scored_triples_per_s"] = 2 * 512 * 1025 / sec  # s and o slots, positive + 1024 negatives
+    # the same step scoring every query against the chunk's unique candidates and picking
+    # (implementation "batch", what the reference's "auto" takes for more than 30 negatives,
+    # train.py:762-771, 931-968): the all-entities distance kernel and its backward instead of
+    # per-query candidate gathers.  (This package's "auto" takes "triple" here.)
+    torch.manual_seed(0)
+    c.set("negative_sampling.implementation", "batch")
+    sec, _ = _job_step_time(c, "fb15k-237", 512)
+    res["c4_ns_rotate1024_implementation_batch_step_ms"] = round(sec * 1e3, 3)
     return res
 
 

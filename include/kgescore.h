@@ -220,6 +220,17 @@ int kge_score_dist_bwd(int kind, float sign, const float* g, int64_t ldg,
                        const int64_t* tidx, int64_t n, int64_t m, int d, float* dq,
                        int64_t lddq, float* dt, int64_t lddt, void* stream);
 
+/* The same gradients from READY pair weights W [n, m]: dQ[i,:] += sum_j W[i,j] phi(Q[i] - T[j]),
+ * dT[row(j),:] += sum_i W[i,j] phi(T[j] - Q[i]); W = sign * G for the L1 kinds (phi = sign(x), or
+ * z / |z| per complex component for RotatE), W = sign * G / dist for the L2 kinds (phi = identity)
+ * -- the autograd of torch.cdist / of the norm over rotate.py:41-60's pairwise tensor with the
+ * per-pair factor left to the caller, who holds the [n, m] block anyway.  Requires
+ * (d or d/2 for RotatE) % 4 == 0 and 16-B aligned rows of q and t (else KGE_ERR_ALIGN). */
+int kge_score_dist_bwd_weighted(int kind, const float* w, int64_t ldw, const float* q, int64_t ldq,
+                                const float* t, int64_t ldt, const int64_t* tidx, int64_t n,
+                                int64_t m, int d, float* dq, int64_t lddq, float* dt,
+                                int64_t lddt, void* stream);
+
 /* ---- row-wise triple scores ------------------------------------------------------
  * out[i] = score(ent[sidx[i]], rel[pidx[i]], ent[oidx[i]])      (combine="spo")
  * Replaces KgeModel.score_spo (kge_model.py:620-637) for the five scorers.  TransE uses

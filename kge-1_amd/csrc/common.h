@@ -139,6 +139,12 @@ int kge_zero_rows(float* x, int64_t ldx, int64_t n, int d, hipStream_t st);
 int kge_score_dist2(int kind, float sign, const float* q, int64_t ldq, const float* t, int64_t ldt,
                     const int64_t* tidx, int64_t n, int64_t m, int d, float* s, int64_t lds, hipStream_t st);
 
+// owner-computes distance backward from ready pair weights (score_dist_bwd2.hip); -1 when the
+// layout does not fit
+int kge_score_dist_bwd_own(int kind, float scale, const float* w, int64_t ldw, const float* q, int64_t ldq,
+                           const float* t, int64_t ldt, const int64_t* tidx, int64_t n, int64_t m, int d, float* dq,
+                           int64_t lddq, float* dt, int64_t lddt, hipStream_t st);
+
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);

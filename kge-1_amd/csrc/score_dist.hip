@@ -118,9 +118,11 @@ __global__ void __launch_bounds__(NT) score_dist_kernel(float sign, const float*
   }
 }
 
-// Backward: per 64 x 64 tile, pass 1 recomputes the distances (needed by L2 kinds),
-// pass 2 forms per-pair gradient weights and accumulates per-(row, k) partial sums in
-// LDS, flushed to global with one atomic add per (row, k) per tile.
+// Generic backward (any layout; the L2 kinds without ready weights): per 64 x 64 tile, pass 1
+// recomputes the distances (needed by L2 kinds), pass 2 forms per-pair gradient weights and
+// accumulates per-(row, k) partial sums in LDS, flushed to global with one atomic add per
+// (row, k) per tile.  Slow (LDS atomics per pair row); float4-readable layouts take
+// score_dist_bwd2.hip instead.
 template <int KIND>
 __global__ void __launch_bounds__(NT) score_dist_bwd_kernel(float sign, const float* __restrict__ g, int64_t ldg,
                                                             const float* __restrict__ q, int64_t ldq,
@@ -306,8 +308,19 @@ extern "C" int kge_score_dist_bwd(int kind, float sign, const float* g, int64_t 
   KGE_REQUIRE(kind >= KGE_DIST_L1 && kind <= KGE_DIST_ROT_L2);
   KGE_REQUIRE(!is_rot(kind) || d % 2 == 0);
   if (n == 0 || m == 0 || (!dq && !dt)) return 0;
-  KGE_REQUIRE((n + TM - 1) / TM < 65536);
   hipStream_t st = as_stream(stream);
+  // L1 kinds: the pair weights are sign * G as they stand -> the owner-computes kernels
+  // (score_dist_bwd2.hip).  The L2 kinds need G / dist: callers that can hold that [n, m]
+  // block use kge_score_dist_bwd_weighted; here they take the generic kernel below, which
+  // recomputes the distances per tile.
+  if (kind == KGE_DIST_L1 || kind == KGE_DIST_ROT_L1) {
+    const int r = kge_score_dist_bwd_own(kind, sign, g, ldg, q, ldq, t, ldt, tidx, n, m, d, dq, lddq, dt, lddt, st);
+    if (r >= 0) {
+      if (r == 0) KGE_CHECK_LAUNCH();
+      return r;
+    }
+  }
+  KGE_REQUIRE((n + TM - 1) / TM < 65536);
   dim3 grid((unsigned)((m + TN - 1) / TN), (unsigned)((n + TM - 1) / TM));
 #define KGE_DB(K) \
   score_dist_bwd_kernel<K><<<grid, NT, 0, st>>>(sign, g, ldg, q, ldq, t, ldt, tidx, (int)n, (int)m, d, dq, lddq, dt, lddt)

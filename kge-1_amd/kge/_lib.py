@@ -56,6 +56,7 @@ SIGNATURES = {
     "kge_score_dist": ([_I, _F, _P, _I64, _P, _I64, _P, _I64, _I64, _I, _P, _I64, _P], _I),
     "kge_score_dist_bwd": ([_I, _F, _P, _I64, _P, _I64, _P, _I64, _P, _I64, _I64, _I, _P, _I64, _P,
                             _I64, _P], _I),
+    "kge_score_dist_bwd_weighted": ([_I, _P, _I64, _P, _I64, _P, _I64, _P, _I64, _I64, _I, _P, _I64, _P, _I64, _P], _I),
     "kge_score_spo": ([_I, _F, _P, _I64, _P, _P, _I64, _P, _P, _I64, _I, _I, _P, _P], _I),
     "kge_score_spo_bwd": ([_I, _F, _P, _I64, _P, _P, _I64, _P, _P, _I64, _I, _I, _P, _P, _I64, _P,
                            _I64, _P], _I),
@@ -394,9 +395,23 @@ def score_dist(kind, sign, q, t, tidx, out=None):
 
 
 def score_dist_bwd(kind, sign, g, q, t, tidx, dq, dt):
+    """dq += , dt += the gradients of sign * dist(q, t rows) for dL/dS = g.  The L2 kinds need
+    g / dist per pair: where the layout allows, the distances are recomputed by the forward
+    kernel into an [n, m] block, the pair weights formed there, and the owner-computes kernels
+    take them (kge_score_dist_bwd_weighted); otherwise the generic kernel recomputes them per
+    tile."""
     tidx = idx64(tidx)
     n, m = g.shape
     d = q.shape[1]
+    if (kind in (DIST_L2, DIST_ROT_L2) and n > 0 and m > 0 and (d // 2 if kind == DIST_ROT_L2 else d) % 4 == 0
+            and rows(q) % 4 == 0 and rows(t) % 4 == 0 and ptr(q) % 16 == 0 and ptr(t) % 16 == 0):
+        dist = score_dist(kind, 1.0, q, t, tidx)
+        w = torch.where(dist > 0, g * sign / dist, torch.zeros((), device=g.device, dtype=g.dtype))
+        _check(lib().kge_score_dist_bwd_weighted(kind, ptr(w), rows(w), ptr(q), rows(q), ptr(t), rows(t), ptr(tidx),
+                                                 n, m, d, ptr(dq), rows(dq) if dq is not None else 0, ptr(dt),
+                                                 rows(dt) if dt is not None else 0, stream()),
+               "kge_score_dist_bwd_weighted")
+        return
     _check(lib().kge_score_dist_bwd(kind, sign, ptr(g), rows(g), ptr(q), rows(q), ptr(t), rows(t), ptr(tidx),
                                     n, m, d, ptr(dq), rows(dq) if dq is not None else 0, ptr(dt),
                                     rows(dt) if dt is not None else 0, stream()), "kge_score_dist_bwd")

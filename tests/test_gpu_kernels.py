@@ -331,6 +331,61 @@ def test_score_dist_tiled_and_generic_kernels(L, kind, d):
     assert rel_err(outs[2][0].cpu().numpy(), outs[1][0].cpu().double().numpy()) < 1e-5
 
 
+@pytest.mark.parametrize("kind", [0, 1, 2, 3])
+@pytest.mark.parametrize("d", [72, 512, 30])
+def test_score_dist_bwd_owner_and_generic_kernels(L, kind, d):
+    """Backward of the all-entities distance scores against float64 autograd, for dL/dS = G:
+    the owner-computes kernels (score_dist_bwd2.hip: L1 kinds directly, L2 kinds through pair
+    weights G / dist) on float4-readable rows -- d = 72 leaves a partial block of components,
+    the candidate subset repeats rows (their gradients add up), n and m are ragged -- and the
+    generic kernel on rows with an odd leading dimension and on d = 30; both accumulate into
+    dq / dt."""
+    g = torch.Generator().manual_seed(kind * 100 + d)
+    n, m, extra = 131, 300, 9
+    # values on a grid so that exact zeros of q - t occur (sign(0) = 0, |0| has gradient 0)
+    q = (torch.randint(-8, 9, (n, d), generator=g) / 16.0).cuda()
+    t = (torch.randint(-8, 9, (m + extra, d), generator=g) / 16.0).cuda()
+    sub = torch.randint(0, m + extra, (m,), generator=g).cuda()
+    sign = -1.0 if kind < 2 else 1.0
+
+    def reference(rows, G):
+        qq = q.double().cpu().requires_grad_(True)
+        tt = t.double().cpu().requires_grad_(True)
+        tr = tt if rows is None else tt[rows.cpu()]
+        if kind < 2:
+            diff = qq[:, None, :] - tr[None, :, :]
+            dist = diff.abs().sum(-1) if kind == 0 else diff.pow(2).sum(-1).sqrt()
+        else:
+            h = d // 2
+            dr = qq[:, None, :h] - tr[None, :, :h]
+            di = qq[:, None, h:] - tr[None, :, h:]
+            sq = dr * dr + di * di
+            mod = torch.where(sq > 0, sq.clamp_min(1e-300).sqrt(), torch.zeros_like(sq))
+            dist = mod.sum(-1) if kind == 2 else sq.sum(-1).sqrt()
+        (sign * dist * G.double().cpu()).sum().backward()
+        return qq.grad.numpy(), tt.grad.numpy()
+
+    for rows in (None, sub):
+        cols = m + extra if rows is None else m
+        G = torch.randn(n, cols, generator=g).cuda()
+        ref_q, ref_t = reference(rows, G)
+        tol = 2e-5 * max(1.0, float(np.abs(ref_q).max()), float(np.abs(ref_t).max()))
+        for odd in (False, True):
+            if odd:  # rows that are only 4-B aligned: the generic kernel
+                q_in = torch.zeros(n, d + 1, device="cuda")[:, :d]
+                q_in.copy_(q)
+                t_in = torch.zeros(m + extra, d + 1, device="cuda")[:, :d]
+                t_in.copy_(t)
+            else:
+                q_in, t_in = q, t
+            dq = torch.full((n, d), 0.5, device="cuda")
+            dt = torch.full((m + extra, d), -0.25, device="cuda")
+            L.score_dist_bwd(kind, sign, G, q_in, t_in, rows, dq, dt)
+            got_q, got_t = (dq - 0.5).cpu().numpy(), (dt + 0.25).cpu().numpy()
+            assert np.abs(got_q - ref_q).max() < tol, (kind, d, rows is None, odd, "dq")
+            assert np.abs(got_t - ref_t).max() < tol, (kind, d, rows is None, odd, "dt")
+
+
 def test_contract_dispatch_and_errors(L):
     q = torch.randn(8, 6).cuda()
     t = torch.randn(20, 6).cuda()
