@@ -305,6 +305,14 @@ int kge_softmax_grad(const float* s, int64_t lds, int64_t n, int64_t m, int64_t 
                      const int64_t* labels, const float* lse, float scale, float* g, int64_t ldg,
                      void* stream);
 
+/* kge_softmax_grad with G left as bf16 hi / lo planes in `planes` (n_pad rows of ld floats: ld bf16
+ * of the hi plane, then ld bf16 of the lo plane; columns [m, ld) and rows [n, n_pad) zeroed) -- what
+ * kge_score_dot_bwd_q_planes / _t_planes read.  Out of place and elementwise, so a row may be a
+ * whole shard of a large entity table.  ld % 32 == 0, 16-B aligned planes (else KGE_ERR_ALIGN). */
+int kge_softmax_grad_planes(const float* s, int64_t lds, int64_t n, int64_t n_pad, int64_t m,
+                            int64_t c0, const int64_t* labels, const float* lse, float scale,
+                            float* planes, int64_t ld, void* stream);
+
 /* ---- per-row candidate lists (negative sampling) -------------------------------------
  * out[i, c] = score(Q[i, :], ent[cand[i, c], :])  i in [0, n), c in [0, k), with the
  * semantics of KgeModel.score_spo on the triple the candidate completes (kge_model.py:620-637):

@@ -570,6 +570,81 @@ extern "C" int kge_softmax_row_stats(const float* s, int64_t lds, int64_t n, int
   return 0;
 }
 
+// kge_softmax_grad with G left as bf16 hi / lo planes in a buffer of its own (rows of ld floats:
+// ld bf16 of the hi plane, then ld bf16 of the lo plane -- the layout of the in-place kernels
+// above, which the plane-fed GEMMs read).  Out of place because a row need not fit a workgroup's
+// registers here (a shard of a large entity table): elementwise, any row length.  Columns
+// [m, ld) and rows [n, n_pad) are zeroed (K padding of the GEMMs).
+constexpr int GP_CH = 4096;  // columns per workgroup
+
+template <bool VEC>
+__global__ void __launch_bounds__(NT) grad_planes_kernel(const float* __restrict__ s, int64_t lds, int n, int m,
+                                                         int64_t c0, const int64_t* __restrict__ labels,
+                                                         const float* __restrict__ lse, float scale,
+                                                         float* __restrict__ planes, int64_t ld) {
+  const int64_t row = blockIdx.y;
+  const int tid = threadIdx.x;
+  const int64_t j0 = (int64_t)blockIdx.x * GP_CH, j1 = min(j0 + GP_CH, ld);
+  kge_bf16_t* hi = reinterpret_cast<kge_bf16_t*>(planes + row * ld);
+  kge_bf16_t* lo = hi + ld;
+  if (row >= n) {  // K-padding rows
+    for (int64_t j = j0 + (int64_t)tid * 4; j < j1; j += (int64_t)NT * 4) {  // ld % 4 == 0
+      *reinterpret_cast<uint2*>(hi + j) = make_uint2(0u, 0u);
+      *reinterpret_cast<uint2*>(lo + j) = make_uint2(0u, 0u);
+    }
+    return;
+  }
+  const float* sr = s + row * lds;
+  const float l = lse[row];
+  const int64_t lab = labels ? labels[row] - c0 : -1;
+  for (int64_t j = j0 + (int64_t)tid * 4; j < j1; j += (int64_t)NT * 4) {
+    float v[4];
+    if (VEC && j + 3 < m) {
+      const float4 x = *reinterpret_cast<const float4*>(sr + j);
+      v[0] = x.x, v[1] = x.y, v[2] = x.z, v[3] = x.w;
+    } else {
+#pragma unroll
+      for (int c = 0; c < 4; ++c) v[c] = j + c < m ? sr[j + c] : 0.f;
+    }
+    float g[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      g[c] = j + c < m ? scale * __expf(v[c] - l) : 0.f;  // K padding columns: 0
+      if (j + c == lab) g[c] -= scale;
+    }
+    bf16x4 h, lw;
+    split_bf16x4_pk(make_float4(g[0], g[1], g[2], g[3]), h, lw);
+    *reinterpret_cast<bf16x4*>(hi + j) = h;
+    *reinterpret_cast<bf16x4*>(lo + j) = lw;
+  }
+}
+
+extern "C" int kge_softmax_grad_planes(const float* s, int64_t lds, int64_t n, int64_t n_pad, int64_t m, int64_t c0,
+                                       const int64_t* labels, const float* lse, float scale, float* planes,
+                                       int64_t ld, void* stream) {
+  KGE_REQUIRE(n >= 0 && n_pad >= n && n_pad < (1LL << 31) && m > 0 && m < (1LL << 31) && lds >= m);
+  KGE_REQUIRE(s && lse && planes && ld >= m && planes != s);
+  if (ld % 32 != 0 || !aligned16(planes)) return KGE_ERR_ALIGN;
+  if (n_pad == 0) return 0;
+  hipStream_t st = as_stream(stream);
+  // grid.y carries the rows (<= 65,535 per launch: larger batches go in slices)
+  for (int64_t r0 = 0; r0 < n_pad; r0 += 65535) {
+    const int64_t rows = std::min<int64_t>(65535, n_pad - r0);
+    const int64_t n_here = std::max<int64_t>(0, std::min<int64_t>(n - r0, rows));
+    const dim3 grid((unsigned)((ld + GP_CH - 1) / GP_CH), (unsigned)rows);
+    const float* sp = s + r0 * lds;
+    const int64_t* lp = labels ? labels + r0 : nullptr;
+    if (lds % 4 == 0 && aligned16(s))
+      grad_planes_kernel<true><<<grid, dim3(NT), 0, st>>>(sp, lds, (int)n_here, (int)m, c0, lp, lse + r0, scale,
+                                                          planes + r0 * ld, ld);
+    else
+      grad_planes_kernel<false><<<grid, dim3(NT), 0, st>>>(sp, lds, (int)n_here, (int)m, c0, lp, lse + r0, scale,
+                                                           planes + r0 * ld, ld);
+    KGE_CHECK_LAUNCH();
+  }
+  return 0;
+}
+
 extern "C" int kge_softmax_grad(const float* s, int64_t lds, int64_t n, int64_t m, int64_t c0, const int64_t* labels,
                                 const float* lse, float scale, float* g, int64_t ldg, void* stream) {
   KGE_REQUIRE(n >= 0 && m > 0 && m < (1LL << 31) && n < (1LL << 31) && lds >= m);

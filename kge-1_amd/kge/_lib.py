@@ -88,6 +88,7 @@ SIGNATURES = {
                              _I64, _P], _I),
     "kge_softmax_row_stats": ([_P, _I64, _I64, _I64, _I64, _P, _P, _P, _P, _P], _I),
     "kge_softmax_grad": ([_P, _I64, _I64, _I64, _I64, _P, _P, _F, _P, _I64, _P], _I),
+    "kge_softmax_grad_planes": ([_P, _I64, _I64, _I64, _I64, _I64, _P, _P, _F, _P, _I64, _P], _I),
 }
 
 _lib: Optional[ctypes.CDLL] = None
@@ -319,6 +320,16 @@ def split_rows(x):
     hi = torch.empty(n, ldo, device=x.device, dtype=torch.bfloat16)
     lo = torch.empty_like(hi)
     _check(lib().kge_split_rows(ptr(x), rows(x), n, d, ptr(hi), ptr(lo), ldo, stream()), "kge_split_rows")
+    return hi, lo
+
+
+def split_rows_into(x, hi, lo):
+    """split_rows into given bf16 planes (same shape and row stride, ld >= d, zeroed past d by the
+    caller or by the kernel's own padding up to its ld argument)."""
+    n, d = x.shape
+    if hi.shape != lo.shape or hi.stride(0) != lo.stride(0) or hi.shape[0] != n or hi.shape[1] < d:
+        raise ValueError("split_rows_into: planes must be [n, ld >= d] with equal row strides")
+    _check(lib().kge_split_rows(ptr(x), rows(x), n, d, ptr(hi), ptr(lo), hi.stride(0), stream()), "kge_split_rows")
     return hi, lo
 
 
@@ -616,6 +627,19 @@ def softmax_grad(s, c0, labels, lse, scale, g):
     _check(lib().kge_softmax_grad(ptr(s), rows(s), n, m, int(c0), ptr(labels), ptr(lse), float(scale), ptr(g),
                                   rows(g), stream()), "kge_softmax_grad")
     return g
+
+
+def softmax_grad_planes(s, c0, labels, lse, scale):
+    """softmax_grad with the gradient as bf16 hi / lo planes in a buffer of its own (any row
+    length): GradPlanes for score_dot_bwd_q_planes / _t_planes."""
+    labels = idx64(labels)
+    lse = lse.contiguous()
+    n, m = s.shape
+    n_pad, ld = planes_layout(n, m)
+    buf = torch.empty(n_pad, ld, device=s.device, dtype=torch.float32)
+    _check(lib().kge_softmax_grad_planes(ptr(s), rows(s), n, n_pad, m, int(c0), ptr(labels), ptr(lse), float(scale),
+                                         ptr(buf), ld, stream()), "kge_softmax_grad_planes")
+    return GradPlanes(buf, n, m)
 
 
 def softmax_kl(s, l_ptr, l_col, smoothing, scale, g=None, loss=None):

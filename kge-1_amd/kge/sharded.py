@@ -108,7 +108,43 @@ class EngineOps:
     def score_planes(self, packed, tab, out=None):
         return self.L.score_dot_packed(packed, tab, tab.shape[1], out=out)
 
-    # ---- vocab-parallel 1vsAll training
+    # ---- vocab-parallel 1vsAll training on gradient planes: the shard's slice of G leaves the
+    # loss kernel as bf16 hi / lo planes and the backward GEMMs read G and the query rows by
+    # LDS-DMA (no per-tile split of fp32 operands)
+    def train_planes_ok(self, ent, direction) -> bool:
+        from .engine import BILINEAR, window
+
+        if self.kind not in BILINEAR or self.precision != self.L.PREC_BF16X3 or ent.dim() != 2 or ent.stride(1) != 1:
+            return False
+        qw, tab_w = self.L.query_width(self.kind, ent.shape[1]), window(self.kind, direction, ent)
+        return (self.L.split_ok(qw, tab_w, self.precision) and ent.shape[1] % 4 == 0 and qw % 8 == 0
+                and ent.data_ptr() % 16 == 0 and tab_w.shape[1] == qw)
+
+    def split_padded(self, q):
+        """bf16 hi / lo planes of the query rows, padded with zero rows to the GEMMs' K stage."""
+        n, d = q.shape
+        n_pad = (n + 31) // 32 * 32
+        ld = (d + 31) // 32 * 32
+        hi = torch.empty(n_pad, ld, device=q.device, dtype=torch.bfloat16)
+        lo = torch.empty_like(hi)
+        if n_pad > n:
+            hi[n:].zero_()
+            lo[n:].zero_()
+        self.L.split_rows_into(q, hi[:n], lo[:n])
+        return hi, lo
+
+    def score_split(self, hi, lo, n, tab, out=None):
+        return self.L.score_dot_split(hi[:n], lo[:n], tab, None, tab.shape[1], out=out)
+
+    def softmax_grad_planes(self, s, c0, labels, lse, scale):
+        return self.L.softmax_grad_planes(s, c0, labels, lse, scale)
+
+    def score_bwd_planes(self, gp, hi, lo, tab, d_tab):
+        """Returns dq = G . tab (written); d_tab += G^T . Q."""
+        dq = self.L.score_dot_bwd_q_planes(gp, tab)
+        self.L.score_dot_bwd_t_planes(gp, hi, lo, d_tab, accumulate=True)
+        return dq
+
     def row_stats(self, s, c0, labels):
         return self.L.softmax_row_stats(s, c0, labels)
 
@@ -188,6 +224,9 @@ class _Ticket:
 
 
 class RowShardedScorer:
+    #: smallest [n, E_k] score block whose training gradient is kept as bf16 planes
+    PLANES_MIN_ELEMS = 1 << 25
+
     def __init__(self, ent_shard: torch.Tensor, lo: int, hi: int, num_entities: int, rel: torch.Tensor, ops,
                  group=None):
         self.ent = ent_shard
@@ -353,7 +392,17 @@ class RowShardedScorer:
             q = torch.where(owned[:, None], q, torch.zeros_like(q))
             all_reduce(q, group=self.group)
             buf = torch.empty(n, (E_k + 3) // 4 * 4, device=q.device, dtype=torch.float32)
-            logits = self.ops.score(q, self._win(direction, self.ent), out=buf[:, :E_k])
+            tab_w = self._win(direction, self.ent)
+            # gradient planes pay off once the GEMMs dominate the step (a few more launches and
+            # one more [n, E_k] buffer: at 1,024 x 14,541 the fp32 path is 10 % faster, at
+            # 1,024 x 574,311 the planes are 16 % faster)
+            planes = (n * E_k >= self.PLANES_MIN_ELEMS and getattr(self.ops, "train_planes_ok", None) is not None
+                      and self.ops.train_planes_ok(self.ent, direction))
+            if planes:
+                q_hi, q_lo = self.ops.split_padded(q)
+                logits = self.ops.score_split(q_hi, q_lo, n, tab_w, out=buf[:, :E_k])
+            else:
+                logits = self.ops.score(q, tab_w, out=buf[:, :E_k])
             mx, sm, tg = self.ops.row_stats(logits, self.lo, labels)
             M = mx.clone()
             all_reduce(M, op=dist.ReduceOp.MAX, group=self.group)
@@ -362,9 +411,15 @@ class RowShardedScorer:
             all_reduce(tg, group=self.group)
             lse = M + torch.log(z)
             loss += ((lse - tg).double().sum() * scale)
-            g = self.ops.softmax_grad(logits, self.lo, labels, lse, scale, logits)
-            dq = torch.empty_like(q)
-            self.ops.score_bwd(g, q, self._win(direction, self.ent), dq, self._win(direction, d_ent))
+            if planes:
+                gp = self.ops.softmax_grad_planes(logits, self.lo, labels, lse, scale)
+                del logits, buf
+                dq = self.ops.score_bwd_planes(gp, q_hi, q_lo, tab_w, self._win(direction, d_ent))
+                del gp
+            else:
+                g = self.ops.softmax_grad(logits, self.lo, labels, lse, scale, logits)
+                dq = torch.empty_like(q)
+                self.ops.score_bwd(g, q, tab_w, dq, self._win(direction, d_ent))
             all_reduce(dq, group=self.group)
             dq = torch.where(owned[:, None], dq, torch.zeros_like(dq))
             self.ops.prep_bwd(direction, self.ent, local, self.rel, p_all, dq, d_ent, d_rel)

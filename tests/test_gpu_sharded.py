@@ -52,8 +52,11 @@ def _free_port():
         return s_.getsockname()[1]
 
 
-@pytest.mark.parametrize("prec", ["bf16x3", "fp32"])
-def test_train_1vsall_grads_world1_matches_fused(L, prec):
+@pytest.mark.parametrize("prec,planes", [("bf16x3", False), ("bf16x3", True), ("fp32", False)])
+def test_train_1vsall_grads_world1_matches_fused(L, prec, planes):
+    """planes: the shard's gradient slice leaves the loss kernel as bf16 hi / lo planes
+    (kge_softmax_grad_planes) for the plane-fed backward GEMMs -- what large shards use; forced
+    here on a small one whose 300 rows need K padding."""
     from kge import Config, Dataset, KgeModel
     from kge.sharded import EngineOps, RowShardedScorer
 
@@ -79,7 +82,13 @@ def test_train_1vsall_grads_world1_matches_fused(L, prec):
         loss = m.score_sp_xent(s, p, o, 1.0 / B) + m.score_po_xent(p, o, s, 1.0 / B)
         loss.backward()
         sc = RowShardedScorer(ent.detach(), 0, 3001, 3001, rel.detach(), EngineOps(0, L.PRECISIONS[prec]))
+        used = []
+        if planes:
+            sc.PLANES_MIN_ELEMS = 0
+            inner = sc.ops.softmax_grad_planes
+            sc.ops.softmax_grad_planes = lambda *a: (used.append(1), inner(*a))[1]
         l2, d_ent, d_rel = sc.train_1vsall_grads(s, p, o)
+        assert len(used) == (2 if planes else 0)  # one per direction
         assert abs(l2 - loss.item()) <= 1e-5 * abs(loss.item())
         tol = 1e-4 if prec == "bf16x3" else 1e-5
         assert (d_ent - ent.grad).abs().max() <= tol * ent.grad.abs().max()
