@@ -27,6 +27,7 @@ for rank against reference-captured fixtures) timed on this host's cores: score_
 beside the GPU job's MRR on the same tables and triples.
 """
 import argparse
+import gc
 import json
 import os
 import platform
@@ -715,6 +716,10 @@ def _job_step_time(cfg, dataset, batch, steps=10, warmup=3):
     from kge import Dataset
     from kge.job import TrainingJob
 
+    # drop what earlier jobs left behind now (their recorded graphs and multi-GB buffers sit in
+    # reference cycles): a cyclic collection in the middle of the timed steps would free them
+    # there, and freeing device memory waits for the device
+    gc.collect()
     ds = Dataset.synthetic(cfg, dataset, seed=0)
     job = TrainingJob.create(cfg, ds)
     job._prepare()
@@ -774,6 +779,34 @@ def other_configs(device):
     c.set("negative_sampling.implementation", "batch")
     sec, _ = _job_step_time(c, "fb15k-237", 512)
     res["c4_ns_rotate1024_implementation_batch_step_ms"] = round(sec * 1e3, 3)
+
+    # C2's training step with the options tuned LibKGE configurations carry (embedder dropout,
+    # frequency-weighted Lp penalties): still fused and replayed from a recorded graph; and the
+    # distance models' 1vsAll step at the same shape (VALU kernels, forward and backward)
+    def c2(model, extra):
+        c = Config()
+        c.set("model", model)
+        c._import(model)
+        c.set("job.device", str(device))
+        c.set("lookup_embedder.dim", 512)
+        c.set("lookup_embedder.initialize_args", {"mean": 0.0, "std": 0.1})
+        c.set("train.type", "1vsAll")
+        c.set("train.optimizer", "Adagrad")
+        c.set("train.optimizer_args", {"lr": 0.2})
+        c.set("train.batch_size", 1024)
+        c.set("engine.row_sharded", "off")
+        c.set("verbose", False)
+        for k, v in extra.items():
+            c.set(k, v)
+        torch.manual_seed(0)
+        return _job_step_time(c, "fb15k-237", 1024)[0]
+
+    res["c2_step_with_dropout_and_weighted_penalties_ms"] = round(c2("complex", {
+        "lookup_embedder.dropout": 0.2, "lookup_embedder.regularize_args.weighted": True,
+        "complex.entity_embedder.regularize_weight": 1e-6, "complex.relation_embedder.regularize_weight": 1e-6,
+    }) * 1e3, 3)
+    res["transe512_1vsall_fb15k237_b1024_step_ms"] = round(c2("transe", {}) * 1e3, 3)
+    res["rotate512_1vsall_fb15k237_b1024_step_ms"] = round(c2("rotate", {}) * 1e3, 3)
     return res
 
 
