@@ -197,3 +197,96 @@ def test_pipelined_exchange_world1_matches_direct_scoring(L, kind, prec, d):
             sh.score_submitted(group, (3, 3))
     finally:
         dist.destroy_process_group()
+
+
+def complex_q(e, r, direction):
+    """float64 query rows of ComplEx: (s o r) for sp_, (o o conj r) for _po (complex.py:19-44)."""
+    h = e.shape[1] // 2
+    er, ei, rr, ri = e[:, :h], e[:, h:], r[:, :h], r[:, h:]
+    if direction == 0:
+        return torch.cat((er * rr - ei * ri, er * ri + ei * rr), 1)
+    return torch.cat((rr * er + ri * ei, rr * ei - ri * er), 1)
+
+
+def test_c5_rank_shapes_at_n8_past_2_32_elements(L):
+    """What ONE rank sees at N = 8 on the Wikidata5M configuration: 8,192 global queries against a
+    574,311-row shard -- a [8192, 574311] score block of 4.7e9 elements, past 2^32 -- through the
+    row-sharded scoring and training paths (gradient planes) at world size 1 over RCCL, with the
+    loss and sampled scores / dE rows checked in float64."""
+    from kge.sharded import EngineOps, RowShardedScorer
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()))
+    dist.init_process_group("nccl", rank=0, world_size=1)
+    try:
+        _c5_rank_shapes(L, EngineOps, RowShardedScorer)
+    finally:
+        dist.destroy_process_group()
+        torch.cuda.empty_cache()
+
+
+def _c5_rank_shapes(L, EngineOps, RowShardedScorer):
+    E, R, B, d = 574311, 237, 8192, 512
+    torch.manual_seed(0)
+    ent = torch.randn(E, d, device="cuda") * 0.1
+    rel = torch.randn(R, d, device="cuda") * 0.1
+    sh = RowShardedScorer(ent, 0, E, E, rel, EngineOps(L.COMPLEX, L.PREC_BF16X3))
+    g = torch.Generator().manual_seed(1)
+    s = torch.randint(0, E, (B,), generator=g).cuda()
+    p = torch.randint(0, R, (B,), generator=g).cuda()
+    o = torch.randint(0, E, (B,), generator=g).cuda()
+    rows = torch.tensor([0, 1, 4095, 4096, 7000, 8191]).cuda()      # rows on both sides of 2^32 / E
+    cols = torch.tensor([0, 5, 300000, 523775, 574310]).cuda()
+
+    # ---- scoring (what bench.py's row_sharded_c5 runs per rank at N = 8)
+    scores = sh.score_submitted(sh.submit_queries_local(s, p))
+    q64 = complex_q(ent[s[rows]].double(), rel[p[rows]].double(), 0)
+    ref = q64 @ ent[cols].double().T
+    got = scores[rows][:, cols].double()
+    err = (got - ref).abs().max().item() / ref.abs().max().item()
+    assert err < 2e-5
+    del scores
+    torch.cuda.empty_cache()
+
+    # ---- training gradients (vocab-parallel 1vsAll; gradient planes at this size)
+    tr = torch.stack([s, p, o], 1)
+    loss, d_ent, d_rel = sh.train_1vsall_global(tr)
+    # the loss in float64, every row, in column chunks
+    total = 0.0
+    for direction, e_idx, lab in ((0, s, o), (1, o, s)):
+        for b0 in range(0, B, 512):
+            sl = slice(b0, b0 + 512)
+            q64 = complex_q(ent[e_idx[sl]].double(), rel[p[sl]].double(), direction)
+            acc_max = torch.full((512,), -float("inf"), device="cuda", dtype=torch.float64)
+            acc_sum = torch.zeros(512, device="cuda", dtype=torch.float64)
+            for c0 in range(0, E, 65536):
+                lg = q64 @ ent[c0:c0 + 65536].double().T
+                m = torch.maximum(acc_max, lg.max(1).values)
+                acc_sum = acc_sum * torch.exp(acc_max - m) + torch.exp(lg - m[:, None]).sum(1)
+                acc_max = m
+            tgt = (q64 * ent[lab[sl]].double()).sum(1)
+            total += float((acc_max + torch.log(acc_sum) - tgt).sum())
+    ref_loss = total / B
+    assert abs(float(loss) - ref_loss) < 1e-5 * abs(ref_loss)
+    # dE rows: sum over both directions of G^T Q restricted to sampled entity rows
+    ref_de = torch.zeros(len(cols), d, device="cuda", dtype=torch.float64)
+    for direction, e_idx, lab in ((0, s, o), (1, o, s)):
+        for b0 in range(0, B, 512):
+            sl = slice(b0, b0 + 512)
+            q64 = complex_q(ent[e_idx[sl]].double(), rel[p[sl]].double(), direction)
+            acc_max = torch.full((512,), -float("inf"), device="cuda", dtype=torch.float64)
+            acc_sum = torch.zeros(512, device="cuda", dtype=torch.float64)
+            for c0 in range(0, E, 65536):
+                lg = q64 @ ent[c0:c0 + 65536].double().T
+                m = torch.maximum(acc_max, lg.max(1).values)
+                acc_sum = acc_sum * torch.exp(acc_max - m) + torch.exp(lg - m[:, None]).sum(1)
+                acc_max = m
+            lse = acc_max + torch.log(acc_sum)
+            gcols = torch.exp(q64 @ ent[cols].double().T - lse[:, None])          # [512, 5]
+            gcols -= (lab[sl][:, None] == cols[None, :]).double()
+            ref_de += (gcols / B).T @ q64
+    # the query rows' own contribution (prep backward) lands on rows s / o, not on the sampled cols
+    # unless they coincide: mask those out of the comparison
+    touched = torch.isin(cols, torch.cat((s, o)))
+    got = d_ent[cols].double()
+    err = ((got - ref_de)[~touched]).abs().max().item() / ref_de.abs().max().item()
+    assert err < 1e-4
