@@ -7,16 +7,20 @@ KgeModel.score_sp(s, p) -> fused LookupEmbedder gather + ComplEx query prep + th
 all-entities contraction against the entity table (libkgescore, gfx950).
 value = scored triples / s = (queries x entities) / step time, all ranks.
 
-N = 1: the whole 14,541-row table on the one GPU.
+N = 1: the whole 14,541-row table on the one GPU.  The batches are independent, so consecutive
+steps take turns on two HIP streams (kge.engine.BatchStreams; --streams 1 turns that off, and
+the one-stream time of the same run is reported as ms_per_step_one_stream).
 
 N > 1 (torchrun, one process per GPU): the entity table is ROW-SHARDED over the ranks
 (kge.sharded.RowShardedScorer, RCCL over xGMI): every rank contributes its own 1024 queries
 (subjects it owns), prepares their query rows, the rows are all-gathered (W x 1024 x 512 fp32),
 and every rank scores the global batch against its E / W rows -- per-GPU work is constant
-(weak scaling), W x 1024 x 14,541 triples are scored per step.  The exchange of batch i + 1 is
-issued asynchronously while batch i is scored (a loader knows the next batch), the figure
-without that overlap and the replicated-table data-parallel figure (no collective at all)
-are reported next to it, and so is the same step at the Wikidata5M shape (configs[4]).
+(weak scaling), W x 1024 x 14,541 triples are scored per step.  Three schedules of the same
+work are timed -- the exchange of batch i + 1 issued asynchronously while batch i is scored (a
+loader knows the next batch), everything back to back, and one exchange per group of four
+batches per rank -- and the fastest is the headline; the replicated-table data-parallel figure
+(no collective at all) is reported next to it, and so are the same step and the vocab-parallel
+training gradients at the Wikidata5M shape (configs[4]).
 
 Also reported (rank 0, N = 1): the contraction kernel's roofline from HIP events on the launch
 stream (bf16x3 production kernel and the exact-fp32 kernel), score_po, a full 1vsAll training
