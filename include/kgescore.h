@@ -373,6 +373,18 @@ int kge_adagrad_step_multi(int count, float* const* params, const float* const* 
                            float* const* state_sums, const int64_t* ns, const float* minus_clrs,
                            float eps, float weight_decay, int maximize, void* stream);
 
+/* ---- frequency-weighted Lp penalty of a lookup embedder ------------------------------------------
+ * The weighted branch of LookupEmbedder.penalty (lookup_embedder.py:138-158) summed over the
+ * OCCURRENCES of the batch's indexes instead of over unique indexes times their counts (the same
+ * number, without torch.unique's data-dependent shape):
+ *   row_sums[i] = sum_k |w[idx[i], k]|^p;        the caller sums them and scales by weight / (p n)
+ *   dw[idx[i], k] += gscale[0] * coeff * d/dx |x|^p at x = w[idx[i], k]        (gscale may be NULL: 1)
+ * p = 1 .. 4. */
+int kge_lp_rows(const float* w, int64_t ldw, const int64_t* idx, int64_t n, int d, int p,
+                float* row_sums, void* stream);
+int kge_lp_rows_bwd(const float* w, int64_t ldw, const int64_t* idx, int64_t n, int d, int p,
+                    const float* gscale, float coeff, float* dw, int64_t lddw, void* stream);
+
 /* Copy n int64 from host-pinned, device-visible memory (hipHostMalloc) into device memory
  * with a kernel on `stream`: the per-batch index upload of the replayed 1vsAll training
  * step (engine.graph_step).  Internal plumbing; no reference counterpart (the reference

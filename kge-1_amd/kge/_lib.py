@@ -52,6 +52,8 @@ SIGNATURES = {
     "kge_score_dot_bwd_t": ([_P, _I64, _P, _I64, _P, _I64, _I64, _I, _P, _I64, _I, _P], _I),
     "kge_adagrad_step": ([_P, _P, _P, _I64, ctypes.c_float, ctypes.c_float, ctypes.c_float, _I, _P], _I),
     "kge_adagrad_step_multi": ([_I, _P, _P, _P, _P, _P, ctypes.c_float, ctypes.c_float, _I, _P], _I),
+    "kge_lp_rows": ([_P, _I64, _P, _I64, _I, _I, _P, _P], _I),
+    "kge_lp_rows_bwd": ([_P, _I64, _P, _I64, _I, _I, _P, _F, _P, _I64, _P], _I),
     "kge_score_dot_bwd_t_ex": ([_P, _I64, _P, _I64, _P, _I64, _I64, _I, _P, _I64, _I, _I, _P], _I),
     "kge_score_dist": ([_I, _F, _P, _I64, _P, _I64, _P, _I64, _I64, _I, _P, _I64, _P], _I),
     "kge_score_dist_bwd": ([_I, _F, _P, _I64, _P, _I64, _P, _I64, _P, _I64, _I64, _I, _P, _I64, _P,
@@ -757,6 +759,26 @@ def stage_i64(src_pinned, dst):
             and src_pinned.is_contiguous() and dst.is_contiguous() and src_pinned.numel() == dst.numel()):
         raise ValueError("stage_i64: needs a contiguous pinned int64 source and a same-size CUDA int64 target")
     _check(lib().kge_stage_i64(ptr(src_pinned), ptr(dst), dst.numel(), stream()), "kge_stage_i64")
+
+
+def lp_rows(w, idx, p):
+    """row_sums[i] = sum_k |w[idx[i], k]|^p for p in 1 .. 4 (kge_lp_rows)."""
+    require_device(w)
+    idx = idx64(idx).reshape(-1)
+    check_index(idx, w.shape[0], "penalty index")
+    out = torch.empty(idx.numel(), device=w.device, dtype=torch.float32)
+    _check(lib().kge_lp_rows(ptr(w), rows(w), ptr(idx), idx.numel(), w.shape[1], int(p), ptr(out), stream()),
+           "kge_lp_rows")
+    return out
+
+
+def lp_rows_bwd(w, idx, p, gscale, coeff, dw):
+    """dw[idx[i], :] += gscale * coeff * d|x|^p/dx at w[idx[i], :] (kge_lp_rows_bwd); gscale: a 0-dim /
+    1-element fp32 device tensor or None."""
+    idx = idx64(idx).reshape(-1)
+    _check(lib().kge_lp_rows_bwd(ptr(w), rows(w), ptr(idx), idx.numel(), w.shape[1], int(p), ptr(gscale),
+                                 float(coeff), ptr(dw), rows(dw), stream()), "kge_lp_rows_bwd")
+    return dw
 
 
 ADAGRAD_MULTI_MAX = 8

@@ -37,6 +37,37 @@ class _Rows(torch.autograd.Function):
         return d_weight, None
 
 
+class _LpOccurrences(torch.autograd.Function):
+    """coeff * sum over the occurrences i of sum_k |weight[indexes[i], k]|^p on the engine
+    (kge_lp_rows / kge_lp_rows_bwd): a launch and a row-sum forward, one launch backward,
+    instead of a dozen elementwise kernels each way."""
+
+    @staticmethod
+    def forward(ctx, weight, indexes, p, coeff):
+        from ... import _lib
+
+        ctx.save_for_backward(weight, indexes)
+        ctx.p, ctx.coeff = p, coeff
+        return _lib.lp_rows(weight, indexes, p).sum() * coeff
+
+    @staticmethod
+    def backward(ctx, g):
+        from ... import _lib
+
+        weight, indexes = ctx.saved_tensors
+        gs = g.reshape(1).float().contiguous()
+        held = weight.grad
+        if (held is not None and not held.is_sparse and held.dtype == torch.float32 and held.shape == weight.shape
+                and held.stride(1) == 1 and not torch.is_grad_enabled()):
+            # the loss backward has left the table's dense gradient: the touched rows are added
+            # into it where it stands (no table-sized zero tensor, no table-sized add)
+            _lib.lp_rows_bwd(weight, indexes, ctx.p, gs, ctx.coeff, held)
+            return None, None, None, None
+        d_weight = torch.zeros_like(weight)
+        _lib.lp_rows_bwd(weight, indexes, ctx.p, gs, ctx.coeff, d_weight)
+        return d_weight, None, None, None
+
+
 class LookupEmbedder(KgeEmbedder):
     def __init__(self, config, dataset, configuration_key: str, vocab_size: int, init_for_load_only=False):
         super().__init__(config, dataset, configuration_key, init_for_load_only=init_for_load_only)
@@ -118,10 +149,15 @@ class LookupEmbedder(KgeEmbedder):
             result += [(f"{self.configuration_key}.L{p}_penalty", (w / p * params.norm(p=p) ** p).sum())]
         elif kwargs["indexes"].is_cuda and torch.cuda.is_current_stream_capturing():
             indexes = kwargs["indexes"]
-            params = self._embeddings.weight.index_select(0, indexes)
-            if p % 2 == 1:
-                params = torch.abs(params)
-            result += [(f"{self.configuration_key}.L{p}_penalty", (w / p * params ** p).sum() / len(indexes))]
+            weight = self._embeddings.weight
+            if p in (1, 2, 3, 4) and weight.dtype == torch.float32 and weight.stride(1) == 1:
+                value = _LpOccurrences.apply(weight, indexes, int(p), w / p / len(indexes))
+            else:
+                params = weight.index_select(0, indexes)
+                if p % 2 == 1:
+                    params = torch.abs(params)
+                value = (w / p * params ** p).sum() / len(indexes)
+            result += [(f"{self.configuration_key}.L{p}_penalty", value)]
         else:
             unique_indexes, counts = torch.unique(kwargs["indexes"], return_counts=True)
             params = self._embeddings(unique_indexes)
