@@ -143,3 +143,33 @@ def test_fused_adagrad_matches_torch(kw):
     sd = o_mine.state_dict()  # torch's layout: loads into a stock Adagrad
     o2 = torch.optim.Adagrad(ref, lr=0.1, **kw)
     o2.load_state_dict(sd)
+
+
+@pytest.mark.parametrize("p", [1, 2, 3, 4])
+def test_lp_rows_kernels_vs_torch(p):
+    """kge_lp_rows / kge_lp_rows_bwd (the frequency-weighted Lp penalty over the occurrences of a
+    batch's indexes, lookup_embedder.py:138-158) against torch: row sums of |x|^p, the gradient
+    scattered into an existing buffer with repeated rows adding up, values on a grid so that
+    exact zeros occur (p = 1: sign(0) = 0), an odd row width, a leading dimension wider than the
+    rows."""
+    from kge import _lib as L
+
+    g = torch.Generator().manual_seed(p)
+    wide = (torch.randint(-6, 7, (300, 70), generator=g) / 8.0).cuda()
+    w = wide[:, :67]  # ld 70, d 67
+    idx = torch.randint(0, 300, (513,), generator=g).cuda()
+    idx[:7] = 11  # one row many times
+    sums = L.lp_rows(w, idx, p)
+    ref = w[idx].double().abs().pow(p).sum(1)
+    assert torch.allclose(sums.double(), ref, rtol=1e-6, atol=1e-7)
+    gs = torch.tensor([0.75], device="cuda")
+    dw = torch.full((300, 67), 0.5, device="cuda")
+    L.lp_rows_bwd(w, idx, p, gs, 0.3, dw)
+    wr = w.double().clone().requires_grad_(True)
+    (0.3 * 0.75 * wr[idx].abs().pow(p).sum()).backward()
+    assert torch.allclose((dw - 0.5).double(), wr.grad, rtol=1e-5, atol=1e-6)
+    # no scale pointer: factor 1; nothing to do for an empty index vector
+    dw2 = torch.zeros(300, 67, device="cuda")
+    L.lp_rows_bwd(w, idx, p, None, 0.3, dw2)
+    assert torch.allclose(dw2.double() * 0.75, wr.grad, rtol=1e-5, atol=1e-6)
+    assert L.lp_rows(w, idx[:0], p).numel() == 0
