@@ -17,23 +17,30 @@ from ..kge_model import KgeEmbedder
 
 
 class _Rows(torch.autograd.Function):
-    """weight[indexes] whose backward is a zero fill plus one scatter-add (index_add_) -- a
-    few microseconds on the device, against the sort-based embedding_dense_backward of
-    nn.Embedding (~60 us per call whatever the table's size).  Same values; rows that occur
+    """weight[indexes] whose backward is one scatter-add (index_add_) -- a few microseconds on
+    the device, against the sort-based embedding_dense_backward of nn.Embedding (~60 us per call
+    whatever the table's size).  When the table already holds a dense gradient (an earlier
+    backward of the step left it), the rows are added into it where it stands; otherwise into
+    a zero tensor that autograd then takes as the gradient.  Same values; rows that occur
     several times sum their gradients by atomic adds."""
 
     @staticmethod
     def forward(ctx, weight, indexes):
-        ctx.save_for_backward(indexes)
-        ctx.rows = weight.shape[0]
+        ctx.save_for_backward(weight, indexes)
         return weight.index_select(0, indexes.reshape(-1)).view(*indexes.shape, weight.shape[1])
 
     @staticmethod
     def backward(ctx, g):
-        (indexes,) = ctx.saved_tensors
+        weight, indexes = ctx.saved_tensors
         g = g.reshape(-1, g.shape[-1])
-        d_weight = torch.zeros(ctx.rows, g.shape[1], device=g.device, dtype=g.dtype)
-        d_weight.index_add_(0, indexes.reshape(-1), g)
+        idx = indexes.reshape(-1)
+        held = weight.grad
+        if (held is not None and not held.is_sparse and held.dtype == g.dtype and held.shape == weight.shape
+                and not torch.is_grad_enabled()):
+            held.index_add_(0, idx, g)
+            return None, None
+        d_weight = torch.zeros(weight.shape[0], g.shape[1], device=g.device, dtype=g.dtype)
+        d_weight.index_add_(0, idx, g)
         return d_weight, None
 
 
