@@ -2,7 +2,7 @@
 synthetic FB15K-237 shape with embedder dropout, frequency-weighted Lp penalties,
 ReduceLROnPlateau on the validation MRR and validation after every epoch.
 
-    python scripts/dev/e2e_train.py [epochs]
+    python scripts/dev/e2e_train.py [epochs] [eager]
 """
 import os
 import sys
@@ -38,6 +38,8 @@ c.set("train.max_epochs", epochs)
 c.set("valid.every", 1)
 c.set("eval.batch_size", 1024)
 c.set("engine.row_sharded", "off")
+if len(sys.argv) > 2 and sys.argv[2] == "eager":
+    c.set("engine.graph_step", False)
 c.set("verbose", False)
 ds = Dataset.synthetic(c, "fb15k-237", seed=0)
 torch.manual_seed(0)

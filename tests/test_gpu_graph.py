@@ -496,3 +496,33 @@ def test_graph_step_with_embedder_dropout_records_and_redraws_masks():
     for losses in runs.values():
         assert np.isfinite(losses).all() and losses[-8:].mean() < 0.8 * losses[:8].mean()
     assert runs[True][-8:].mean() == pytest.approx(runs[False][-8:].mean(), rel=0.25)
+
+
+def test_graph_step_penalties_follow_eager_over_many_steps():
+    """Frequency-weighted Lp penalties inside the recorded step (engine kernels over the
+    occurrences of the batch's indexes, added into the held gradient) against the eager step's
+    unique-index form: the same penalty and loss at every one of 12 steps, i.e. also on the
+    replays after the recording, and after an lr change records the step anew."""
+    runs = {}
+    for graph in (True, False):
+        job, tr = _job(graph, "fp32")
+        for e, w, p in ((job.model._entity_embedder, 1e-2, 3), (job.model._relation_embedder, 5e-3, 2)):
+            e.config.set(e.configuration_key + ".regularize_weight", w)
+            e.config.set("lookup_embedder.regularize_args.weighted", True)
+            e.config.set(e.configuration_key + ".regularize_args.p", p)
+        job._prepare()
+        assert job.model._entity_embedder.penalty_weighted()
+        pens, losses = [], []
+        for b in range(12):
+            if b == 8:
+                for group in job.optimizer.param_groups:
+                    group["lr"] = 0.05
+            res, pen, _ = job.train_step(b % 9, {"triples": tr[(b % 9) * 64:(b % 9 + 1) * 64].long()})
+            pens.append(float(pen))
+            losses.append(float(res.loss))
+        recorded = job._graph_step is not None and job._graph_step.graph is not None
+        assert recorded == graph, getattr(job._graph_step, "error", None)
+        runs[graph] = (np.array(pens), np.array(losses))
+    assert (runs[False][0] > 0).all()
+    np.testing.assert_allclose(runs[True][0], runs[False][0], rtol=2e-5)
+    np.testing.assert_allclose(runs[True][1], runs[False][1], rtol=2e-5)
