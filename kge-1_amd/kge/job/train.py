@@ -486,6 +486,7 @@ class TrainingJob1vsAll(TrainingJob):
             self._sharded = ShardedTraining1vsAll(self)
             return
         opt = self.optimizer
+        self._graph_step = None  # decided anew by every _prepare
         if (self.config.get("engine.graph_step") and self.config.get("engine.fused_loss")
                 and isinstance(self.loss, KLDivWithSoftmaxKgeLoss)
                 and torch.device(self.device).type == "cuda"
@@ -667,6 +668,7 @@ class TrainingJobKvsAll(TrainingJob):
         from ..sharded import sharding_enabled
 
         opt = self.optimizer
+        self._graph_step = None  # decided anew by every _prepare
         if (self.config.get("engine.graph_step") and self.config.get("engine.fused_loss")
                 and isinstance(self.loss, KLDivWithSoftmaxKgeLoss)
                 and 1 <= len(self.query_types) <= 2

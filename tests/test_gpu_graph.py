@@ -526,3 +526,37 @@ def test_graph_step_penalties_follow_eager_over_many_steps():
     assert (runs[False][0] > 0).all()
     np.testing.assert_allclose(runs[True][0], runs[False][0], rtol=2e-5)
     np.testing.assert_allclose(runs[True][1], runs[False][1], rtol=2e-5)
+
+
+def test_kvsall_graph_step_with_unweighted_penalty_matches_eager():
+    """KvsAll records its step with UNWEIGHTED Lp penalties (whole-table norms: nothing
+    batch-dependent) and follows the eager step; with frequency-weighted terms it steps eagerly
+    (their triples vary in number) and its batches carry those triples."""
+    runs = {}
+    for graph in (True, False):
+        job = _kvsall_job(graph, "distmult")
+        for e, w in ((job.model._entity_embedder, 1e-3), (job.model._relation_embedder, 5e-4)):
+            e.config.set(e.configuration_key + ".regularize_weight", w)
+        job._prepare()
+        assert (job._graph_step is not None) == graph
+        perm = torch.randperm(job.num_examples, generator=torch.Generator().manual_seed(3))
+        pens, losses = [], []
+        for b in range(8):
+            res, pen, _ = job.train_step(b, job._collate(perm[b * 64:(b + 1) * 64]))
+            pens.append(float(pen))
+            losses.append(float(res.loss))
+        if graph:
+            assert job._graph_step.graph is not None, job._graph_step.error
+        runs[graph] = (np.array(pens), np.array(losses))
+    assert (runs[False][0] > 0).all()
+    np.testing.assert_allclose(runs[True][0], runs[False][0], rtol=2e-5)
+    np.testing.assert_allclose(runs[True][1], runs[False][1], rtol=2e-5)
+    job = _kvsall_job(True, "distmult")
+    job.config.set("lookup_embedder.regularize_args.weighted", True)
+    job.config.set("distmult.entity_embedder.regularize_weight", 1e-3)
+    job._prepare()
+    assert job._graph_step is None and job._weighted_penalty()
+    batch = job._collate(torch.arange(64))
+    assert batch["triples"].shape[1] == 3
+    res, pen, _ = job.train_step(0, batch)
+    assert float(pen) > 0
