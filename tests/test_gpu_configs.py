@@ -688,3 +688,53 @@ def test_score_so_and_generic_s_o_combine_vs_reference():
         with pytest.raises(ValueError):
             m.get_scorer().score_emb(torch.zeros(2, ent.shape[1]).cuda(), torch.zeros(2, rel.shape[1]).cuda(),
                                      torch.zeros(2, ent.shape[1]).cuda(), "sp*")
+
+
+# ------------------------------------------------------------------------------ the reference's examples
+
+
+@pytest.mark.parametrize("name,opts", [
+    ("toy-complex-train", {
+        "model": "complex", "train.optimizer": "Adagrad", "train.optimizer_args": {"lr": 0.2},
+        "train.lr_scheduler": "ReduceLROnPlateau", "train.lr_scheduler_args": {"mode": "max", "patience": 4},
+        "lookup_embedder.dim": 100, "lookup_embedder.regularize_weight": 0.8e-7,
+        "lookup_embedder.initialize": "normal_",
+        "lookup_embedder.initialize_args": {"normal_": {"mean": 0.0, "std": 0.1}}}),
+    ("toy-complex-train-sampling", {
+        "model": "complex", "train.type": "negative_sampling", "train.optimizer": "Adagrad",
+        "train.optimizer_args": {"lr": 0.6, "weight_decay": 0.4e-7}, "train.loss": "margin_ranking",
+        "train.loss_arg": 2.0, "train.batch_size": 512, "lookup_embedder.dim": 100,
+        "negative_sampling.num_samples.s": 30, "negative_sampling.num_samples.p": 30,
+        "negative_sampling.num_samples.o": -1, "negative_sampling.filtering.s": True,
+        "negative_sampling.filtering.o": True}),
+    ("toy-transe-train", {
+        "model": "transe", "train.batch_size": 256, "train.loss": "margin_ranking", "train.loss_arg": 4.0,
+        "train.optimizer": "Adagrad", "train.optimizer_args": {"lr": 0.1}, "train.type": "negative_sampling"}),
+], ids=lambda x: x if isinstance(x, str) else "")
+def test_reference_training_examples_run(name, opts):
+    """The options of the reference's runnable training examples (examples/toy-complex-train.yaml,
+    toy-complex-train-sampling.yaml without its relation-slot filtering, toy-transe-train.yaml)
+    through TrainingJob.run with validation every epoch, on the small dataset the reference's own
+    tests ship: every key is accepted, the jobs train and evaluate, costs and metrics are finite."""
+    from kge import Config, Dataset
+    from kge.job import TrainingJob
+
+    c = Config()
+    c.set("model", opts["model"])
+    c._import(opts["model"])
+    c.set("job.device", "cuda")
+    c.set("verbose", False)
+    c.set("train.max_epochs", 3)
+    c.set("valid.every", 1)
+    for k, v in opts.items():
+        if k != "model":
+            c.set(k, v)
+    ds = Dataset.create(c, folder=os.path.join(GOLDEN, "dataset_test"))
+    torch.manual_seed(0)
+    job = TrainingJob.create(c, ds)
+    traces = job.run()
+    assert len(traces) == 3 and len(job.valid_trace) == 3
+    for t in traces:
+        assert np.isfinite(t["avg_cost"]) and np.isfinite(t["avg_loss"]) and t["batches"] >= 1
+    for v in job.valid_trace:
+        assert 0.0 < v["mean_reciprocal_rank_filtered"] <= 1.0 and v["mean_rank"] >= 1.0
