@@ -225,7 +225,7 @@ class Dataset(Configurable):
         return self._triples[split]
 
     def index(self, key: str):
-        """"<split>_sp_to_o" / "<split>_po_to_s" (indexing.py:287-301), "relation_types",
+        """"<split>_sp_to_o" / "<split>_po_to_s" / "<split>_so_to_p" (indexing.py:287-301), "relation_types",
         "relations_per_type" and "frequency_percentiles" (indexing.py:142-263)."""
         if key not in self._indexes:
             if key == "relation_types":
@@ -244,6 +244,9 @@ class Dataset(Configurable):
             elif key.endswith("_po_to_s"):
                 t = self.split(key[: -len("_po_to_s")]).numpy()
                 self._indexes[key] = KvsAllIndex(t, (1, 2), 0)
+            elif key.endswith("_so_to_p"):
+                t = self.split(key[: -len("_so_to_p")]).numpy()
+                self._indexes[key] = KvsAllIndex(t, (0, 2), 1)
             else:
                 raise KeyError(key)
         return self._indexes[key]

@@ -9,7 +9,7 @@ leaves the GPU:
   (sampler.py:318-345);
 * ``shared``    -- one draw per batch shared by all rows, with each row's own positive
   dropped (sampler.py:199-255);
-* filtering    -- sampled positives (the training triples completing (p, o) / (s, p)) are
+* filtering    -- sampled positives (the training triples completing (p, o) / (s, o) / (s, p)) are
   re-drawn until none is left (sampler.py:140-171): membership is one searchsorted into a
   device copy of the slot's CSR index, globally sorted by (key, value).
 
@@ -52,12 +52,9 @@ class KgeSampler:
                 else:
                     self.num_samples[slot] = 0
         self._filter = [None, None, None]
-        for slot in (S, O):
+        for slot, name in ((S, "po_to_s"), (P, "so_to_p"), (O, "sp_to_o")):
             if self.filter_positives[slot]:
-                idx = dataset.index(f"{split}_{'po_to_s' if slot == S else 'sp_to_o'}")
-                self._filter[slot] = self._device_index(idx)
-        if self.filter_positives[P]:
-            raise NotImplementedError("filtering of relation (p) negatives is outside the scoring path")
+                self._filter[slot] = self._device_index(dataset.index(f"{split}_{name}"))
 
     def _device_index(self, idx):
         """(key codes, (key rank * V + value) codes) -- both sorted -- of a KvsAllIndex."""
@@ -99,8 +96,8 @@ class KgeSampler:
 
     def _is_positive(self, neg: torch.Tensor, slot: int, positive_triples: torch.Tensor) -> torch.Tensor:
         kcode, vcode, k1max, V = self._filter[slot]
-        a, b = (positive_triples[:, P], positive_triples[:, O]) if slot == S else (positive_triples[:, S],
-                                                                                 positive_triples[:, P])
+        ka, kb = {S: (P, O), P: (S, O), O: (S, P)}[slot]  # the slot's key columns, in index order
+        a, b = positive_triples[:, ka], positive_triples[:, kb]
         q = a * k1max + b
         pos = torch.searchsorted(kcode, q).clamp_(max=max(len(kcode) - 1, 0))
         has = kcode[pos] == q if len(kcode) else torch.zeros_like(q, dtype=torch.bool)

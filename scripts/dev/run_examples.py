@@ -29,7 +29,7 @@ EXAMPLES = {
         "train.loss_arg": 2.0, "train.batch_size": 512, "lookup_embedder.dim": 100,
         "negative_sampling.num_samples.s": 30, "negative_sampling.num_samples.p": 30,
         "negative_sampling.num_samples.o": -1, "negative_sampling.filtering.s": True,
-        "negative_sampling.filtering.o": True,  # the example also filters p: outside the scoring path here
+        "negative_sampling.filtering.o": True, "negative_sampling.filtering.p": True,
     },
     "toy-transe-train": {
         "model": "transe", "train.batch_size": 256, "train.loss": "margin_ranking", "train.loss_arg": 4.0,

@@ -706,14 +706,14 @@ def test_score_so_and_generic_s_o_combine_vs_reference():
         "train.loss_arg": 2.0, "train.batch_size": 512, "lookup_embedder.dim": 100,
         "negative_sampling.num_samples.s": 30, "negative_sampling.num_samples.p": 30,
         "negative_sampling.num_samples.o": -1, "negative_sampling.filtering.s": True,
-        "negative_sampling.filtering.o": True}),
+        "negative_sampling.filtering.o": True, "negative_sampling.filtering.p": True}),
     ("toy-transe-train", {
         "model": "transe", "train.batch_size": 256, "train.loss": "margin_ranking", "train.loss_arg": 4.0,
         "train.optimizer": "Adagrad", "train.optimizer_args": {"lr": 0.1}, "train.type": "negative_sampling"}),
 ], ids=lambda x: x if isinstance(x, str) else "")
 def test_reference_training_examples_run(name, opts):
     """The options of the reference's runnable training examples (examples/toy-complex-train.yaml,
-    toy-complex-train-sampling.yaml without its relation-slot filtering, toy-transe-train.yaml)
+    toy-complex-train-sampling.yaml, toy-transe-train.yaml)
     through TrainingJob.run with validation every epoch, on the small dataset the reference's own
     tests ship: every key is accepted, the jobs train and evaluate, costs and metrics are finite."""
     from kge import Config, Dataset

@@ -27,6 +27,28 @@ def test_filtering_removes_training_positives():
         assert bool(smp._is_positive(tr[:, [slot]], slot, tr).all())
 
 
+def test_filtering_of_relation_negatives():
+    """filtering.p: sampled relations r with (s, r, o) in the training split are redrawn
+    (sampler.py:140-171 with the so_to_p index); with 24 relations over 641 entity pairs (up to 15 positives each) many rows
+    have a positive among their first draws."""
+    c = Config()
+    c.set("negative_sampling.filtering.p", True)
+    c.set("negative_sampling.num_samples.p", 3)
+    ds = _ds(c, E=30, R=24)
+    smp = KgeSampler.create(c, "negative_sampling", ds, "cpu")
+    assert smp.num_samples[1] == 3
+    tr = ds.split("train")[:300].long()
+    first = smp._sample(300, 1, 3)
+    assert bool(smp._is_positive(first, 1, tr).any())  # unfiltered draws do hit positives
+    neg = smp.sample(tr, 1)
+    assert neg.shape == (300, 3) and int(neg.min()) >= 0 and int(neg.max()) < 24
+    assert not bool(smp._is_positive(neg, 1, tr).any())
+    assert bool(smp._is_positive(tr[:, [1]], 1, tr).all())
+    train = {tuple(t) for t in ds.split("train").tolist()}
+    for (s, p, o), row in zip(tr.tolist(), neg.tolist()):
+        assert all((s, r, o) not in train for r in row)
+
+
 def test_shared_sampling_drops_own_positive():
     c = Config()
     c.set("negative_sampling.shared", True)
