@@ -610,7 +610,7 @@ __global__ void __launch_bounds__(NT) grad_planes_kernel(const float* __restrict
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
       g[c] = j + c < m ? scale * __expf(v[c] - l) : 0.f;  // K padding columns: 0
-      if (j + c == lab) g[c] -= scale;
+      if (j + c == lab && j + c < m) g[c] -= scale;  // a label of another shard may fall into the padding
     }
     bf16x4 h, lw;
     split_bf16x4_pk(make_float4(g[0], g[1], g[2], g[3]), h, lw);

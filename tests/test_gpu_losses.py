@@ -173,3 +173,32 @@ def test_lp_rows_kernels_vs_torch(p):
     L.lp_rows_bwd(w, idx, p, None, 0.3, dw2)
     assert torch.allclose(dw2.double() * 0.75, wr.grad, rtol=1e-5, atol=1e-6)
     assert L.lp_rows(w, idx[:0], p).numel() == 0
+
+
+@pytest.mark.parametrize("n,m", [(37, 130), (64, 257), (5, 31)])
+def test_softmax_grad_planes_slice_vs_float64(n, m):
+    """kge_softmax_grad_planes on a column slice [c0, c0 + m) of rows whose labels are GLOBAL ids:
+    hi + lo reproduces scale * (exp(s - lse) - onehot) to the split's 2^-16; labels that belong to
+    another shard -- below c0, past the slice, and in particular inside the slice's K padding
+    [m, ld) -- leave no trace; padding columns and rows are zero."""
+    from kge import _lib as L
+
+    g = torch.Generator().manual_seed(n * 1000 + m)
+    c0 = 11
+    s = torch.randn(n, m, generator=g).cuda()
+    lse = (torch.logsumexp(s.double(), 1) + 0.3).float()
+    labels = torch.randint(0, c0 + m + 40, (n,), generator=g)
+    labels[0] = c0 + m          # first padding column
+    labels[1 % n] = c0 - 1      # just below the slice
+    labels[2 % n] = c0 + m - 1  # last column of the slice
+    labels = labels.cuda()
+    gp = L.softmax_grad_planes(s, c0, labels, lse, 0.5)
+    ref = 0.5 * torch.exp(s.double() - lse.double()[:, None])
+    lab = labels - c0
+    own = (lab >= 0) & (lab < m)
+    ref[torch.arange(n, device="cuda")[own], lab[own]] -= 0.5
+    got = gp.hi[:n, :m].double() + gp.lo[:n, :m].double()
+    assert (got - ref).abs().max().item() <= 3e-5 * ref.abs().max().item()
+    for plane in (gp.hi, gp.lo):
+        assert float(plane[:, m:].float().abs().sum()) == 0.0
+        assert float(plane[n:].float().abs().sum()) == 0.0
