@@ -290,3 +290,85 @@ def _c5_rank_shapes(L, EngineOps, RowShardedScorer):
     got = d_ent[cols].double()
     err = ((got - ref_de)[~touched]).abs().max().item() / ref_de.abs().max().item()
     assert err < 1e-4
+
+
+def _world2_batch():
+    """Tables and one global batch for the two-rank test; some targets sit right past the end of
+    shard 0 (rows 502 .. 511 of 1,003: inside the K padding of shard 0's gradient planes) and
+    right before shard 1."""
+    from kge.sharded import shard_bounds
+
+    E, R, d, B = 1003, 11, 64, 96
+    g = torch.Generator().manual_seed(5)
+    ent = torch.randn(E, d, generator=g) * 0.2
+    rel = torch.randn(R, d, generator=g) * 0.2
+    tr = torch.stack([torch.randint(0, E, (B,), generator=g), torch.randint(0, R, (B,), generator=g),
+                      torch.randint(0, E, (B,), generator=g)], 1)
+    hi0 = shard_bounds(E, 2, 0)[1]
+    tr[0, 2], tr[1, 2], tr[2, 0], tr[3, 0], tr[4, 2] = hi0, hi0 + 3, hi0, hi0 - 1, hi0 - 1
+    return E, R, d, B, ent, rel, tr
+
+
+def _world2_worker(rank, world, port, planes, out_q):
+    """One of two ranks sharing the GPU; collectives over gloo (device tensors staged through host
+    memory by kge.sharded), compute on the engine."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from kge import _lib
+        from kge.sharded import EngineOps, RowShardedScorer, shard_bounds
+
+        E, R, d, B, ent, rel, tr = _world2_batch()
+        lo, hi = shard_bounds(E, world, rank)
+        sc = RowShardedScorer(ent[lo:hi].cuda().contiguous(), lo, hi, E, rel.cuda(),
+                              EngineOps(_lib.COMPLEX, _lib.PREC_BF16X3))
+        if planes:
+            sc.PLANES_MIN_ELEMS = 0
+        loss, d_ent, d_rel = sc.train_1vsall_global(tr.cuda())
+        out_q.put((rank, lo, hi, float(loss), d_ent.cpu().numpy(), d_rel.cpu().numpy()))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("planes", [True, False], ids=["planes", "fp32_block"])
+def test_train_1vsall_world2_on_the_engine_matches_fused(L, planes):
+    """Vocab-parallel 1vsAll gradients with TWO ranks on the engine's kernels (both on this GPU,
+    collectives over gloo through host memory): every rank's shard of dE, the relation gradient
+    and the loss equal the single-GPU fused step's -- with targets that live in the other shard,
+    including the columns right past a shard's end (the K padding of its gradient planes)."""
+    import torch.multiprocessing as mp
+
+    from kge import Config, Dataset, KgeModel
+
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_world2_worker, args=(r, world, port, planes, q)) for r in range(world)]
+    for pr in procs:
+        pr.start()
+    res = sorted([q.get(timeout=240) for _ in range(world)], key=lambda x: x[0])
+    for pr in procs:
+        pr.join(timeout=60)
+        assert pr.exitcode == 0
+    E, R, d, B, ent, rel, tr = _world2_batch()
+    c = Config()
+    c.set("model", "complex")
+    c._import("complex")
+    c.set("job.device", "cuda")
+    c.set("lookup_embedder.dim", d)
+    c.set("dataset.num_entities", E)
+    c.set("dataset.num_relations", R)
+    m = KgeModel.create(c, Dataset(c, None))
+    we, wr = m._entity_embedder._embeddings.weight, m._relation_embedder._embeddings.weight
+    with torch.no_grad():
+        we.copy_(ent)
+        wr.copy_(rel)
+    t = tr.cuda()
+    loss = m.score_sp_xent(t[:, 0], t[:, 1], t[:, 2], 1.0 / B) + m.score_po_xent(t[:, 1], t[:, 2], t[:, 0], 1.0 / B)
+    loss.backward()
+    ref_e, ref_r = we.grad.cpu().numpy(), wr.grad.cpu().numpy()
+    for rank, lo, hi, l2, d_ent, d_rel in res:
+        assert l2 == pytest.approx(loss.item(), rel=1e-5)
+        assert np.abs(d_ent - ref_e[lo:hi]).max() <= 1e-4 * np.abs(ref_e).max(), rank
+        assert np.abs(d_rel - ref_r).max() <= 1e-4 * np.abs(ref_r).max(), rank
