@@ -372,3 +372,101 @@ def test_train_1vsall_world2_on_the_engine_matches_fused(L, planes):
         assert l2 == pytest.approx(loss.item(), rel=1e-5)
         assert np.abs(d_ent - ref_e[lo:hi]).max() <= 1e-4 * np.abs(ref_e).max(), rank
         assert np.abs(d_rel - ref_r).max() <= 1e-4 * np.abs(ref_r).max(), rank
+
+
+def _world2_score_worker(rank, world, port, out_q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from kge import _lib
+        from kge.sharded import EngineOps, RowShardedScorer, shard_bounds
+
+        E, R, d, B, ent, rel, tr = _world2_batch()
+        lo, hi = shard_bounds(E, world, rank)
+        sc = RowShardedScorer(ent[lo:hi].cuda().contiguous(), lo, hi, E, rel.cuda(),
+                              EngineOps(_lib.COMPLEX, _lib.PREC_BF16X3))
+        g = torch.Generator().manual_seed(40 + rank)
+        k = 2
+        s = torch.randint(lo, hi, (k, 48), generator=g).cuda()   # shard-affine queries: own subjects
+        p = torch.randint(0, R, (k, 48), generator=g).cuda()
+        single = [sc.score_submitted(sc.submit_queries_local(s[i], p[i])).cpu().numpy() for i in range(k)]
+        group = sc.submit_queries_local(s.reshape(-1), p.reshape(-1))
+        blocks = [sc.score_submitted(group, (x, k)).cpu().numpy() for x in range(k)]
+        # the generic path: any subjects, owner-computed query rows + all_reduce
+        s_any = torch.randint(0, E, (48,), generator=g).cuda()
+        generic = sc.score_sp(s_any, p[0])
+        tv, ti = sc.topk(generic, 5)
+        # evaluation counts of a batch every rank holds
+        t = tr[:32].cuda()
+        f_ptr = torch.arange(0, 65, 2).cuda()
+        f_col = torch.randint(0, E, (64,), generator=torch.Generator().manual_seed(9)).cuda()
+        counts = sc.rank_counts(t[:, 0], t[:, 1], t[:, 2], (f_ptr, f_col), (f_ptr, f_col))
+        out_q.put((rank, lo, hi, s.cpu().numpy(), p.cpu().numpy(), single, blocks, s_any.cpu().numpy(),
+                   generic.cpu().numpy(), tv.cpu().numpy(), ti.cpu().numpy(), counts.cpu().numpy()))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_scoring_and_ranking_world2_on_the_engine(L):
+    """Two ranks on the engine's kernels: shard-affine scoring through the packed-plane exchange
+    (single batches and one grouped exchange of two batches), the generic owner-computes path,
+    the top-k merge and the evaluation counts -- against the unsharded engine on the whole table."""
+    import torch.multiprocessing as mp
+
+    from kge import engine
+
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_world2_score_worker, args=(r, world, port, q)) for r in range(world)]
+    for pr in procs:
+        pr.start()
+    res = sorted([q.get(timeout=240) for _ in range(world)], key=lambda x: x[0])
+    for pr in procs:
+        pr.join(timeout=60)
+        assert pr.exitcode == 0
+    E, R, d, B, ent, rel, tr = _world2_batch()
+    ent, rel = ent.cuda(), rel.cuda()
+
+    def full(s, p):
+        return engine.score_all(L.COMPLEX, L.DIR_SP, L.PREC_BF16X3, 1.0, ent, torch.as_tensor(s).cuda(), rel,
+                                torch.as_tensor(p).cuda(), ent, None).cpu().numpy()
+
+    k = 2
+    s_ranks, p_ranks = [r[3] for r in res], [r[4] for r in res]
+    for rank, lo, hi, _, _, single, blocks, s_any, generic, tv, ti, counts in res:
+        for i in range(k):  # step i: rank 0's batch i, then rank 1's
+            ref = full(np.concatenate([s_ranks[0][i], s_ranks[1][i]]), np.concatenate([p_ranks[0][i], p_ranks[1][i]]))
+            np.testing.assert_allclose(single[i], ref[:, lo:hi], rtol=0, atol=2e-5 * np.abs(ref).max())
+        # grouped: rank-major rows (rank 0's two batches, then rank 1's), scored in two blocks
+        s_g = np.concatenate([s_ranks[0].reshape(-1), s_ranks[1].reshape(-1)])
+        p_g = np.concatenate([p_ranks[0].reshape(-1), p_ranks[1].reshape(-1)])
+        ref = full(s_g, p_g)
+        np.testing.assert_allclose(np.concatenate(blocks), ref[:, lo:hi], rtol=0, atol=2e-5 * np.abs(ref).max())
+    # generic path: the global batch is rank 0's queries then rank 1's
+    s_all = np.concatenate([r[7] for r in res])
+    p_all = np.concatenate([p_ranks[0][0], p_ranks[1][0]])
+    ref = full(s_all, p_all)
+    for rank, lo, hi, *_rest in res:
+        generic, tv, ti = _rest[5], _rest[6], _rest[7]
+        np.testing.assert_allclose(generic, ref[:, lo:hi], rtol=0, atol=2e-5 * np.abs(ref).max())
+        np.testing.assert_allclose(tv, np.sort(ref, 1)[:, ::-1][:, :5], rtol=0, atol=2e-5 * np.abs(ref).max())
+        np.testing.assert_allclose(np.take_along_axis(ref, ti, 1), tv, rtol=0, atol=2e-5 * np.abs(ref).max())
+    np.testing.assert_array_equal(res[0][11], res[1][11])  # the reduced counts are global
+    # the same counts from one rank holding the whole table
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()))
+    dist.init_process_group("gloo", rank=0, world_size=1)
+    try:
+        from kge.sharded import EngineOps, RowShardedScorer
+
+        one = RowShardedScorer(ent, 0, E, E, rel, EngineOps(L.COMPLEX, L.PREC_BF16X3))
+        t = tr[:32].cuda()
+        f_ptr = torch.arange(0, 65, 2).cuda()
+        f_col = torch.randint(0, E, (64,), generator=torch.Generator().manual_seed(9)).cuda()
+        ref_counts = one.rank_counts(t[:, 0], t[:, 1], t[:, 2], (f_ptr, f_col), (f_ptr, f_col)).cpu().numpy()
+    finally:
+        dist.destroy_process_group()
+    # bf16x3 scores of a shard and of the whole table agree to rounding: counts may differ only
+    # where a competitor ties the true score within that rounding -- none on these random tables
+    np.testing.assert_array_equal(res[0][11], ref_counts)
