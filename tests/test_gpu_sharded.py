@@ -470,3 +470,83 @@ def test_scoring_and_ranking_world2_on_the_engine(L):
     # bf16x3 scores of a shard and of the whole table agree to rounding: counts may differ only
     # where a competitor ties the true score within that rounding -- none on these random tables
     np.testing.assert_array_equal(res[0][11], ref_counts)
+
+
+def _jobs_config(mode, precision="fp32"):
+    from kge import Config
+
+    c = Config()
+    c.set("model", "complex")
+    c._import("complex")
+    c.set("job.device", "cuda")
+    c.set("verbose", False)
+    c.set("lookup_embedder.dim", 64)
+    c.set("lookup_embedder.initialize_args", {"mean": 0.0, "std": 0.1})
+    c.set("train.type", "1vsAll")
+    c.set("train.batch_size", 256)
+    c.set("train.max_epochs", 2)
+    c.set("train.optimizer_args", {"lr": 0.1})
+    c.set("valid.every", 0)
+    c.set("eval.batch_size", 100)
+    c.set("random_seed.torch", 3)
+    c.set("engine.precision", precision)
+    c.set("engine.graph_step", False)
+    c.set("engine.row_sharded", mode)
+    return c
+
+
+def _run_jobs(c):
+    from kge import Dataset
+    from kge.job import EntityRankingJob, TrainingJob
+
+    ds = Dataset.synthetic(c, "toy", seed=1, num_entities=700, num_relations=9, sizes=(2000, 150, 150))
+    torch.manual_seed(11)
+    job = TrainingJob.create(c, ds)
+    traces = job.run()
+    ev = EntityRankingJob(c, ds, model=job.model)
+    ev.capture_ranks = True
+    et = ev.run()
+    return ([t["avg_loss"] for t in traces], job.model._entity_embedder._embeddings.weight.detach().cpu().numpy(),
+            job.model._relation_embedder._embeddings.weight.detach().cpu().numpy(), ev.ranks,
+            et["mean_reciprocal_rank_filtered_with_test"], job._sharded is not None)
+
+
+def _world2_jobs_worker(rank, world, port, out_q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        out_q.put((rank,) + _run_jobs(_jobs_config("on")))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_sharded_jobs_world2_on_the_engine_match_unsharded_jobs(L):
+    """TrainingJob1vsAll and EntityRankingJob row-sharded over TWO ranks with the engine's kernels
+    (both on this GPU, gloo through host memory): after sync_model both ranks hold the tables the
+    unsharded job trains, the loss trajectory and the evaluation ranks are the same."""
+    import torch.multiprocessing as mp
+
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_world2_jobs_worker, args=(r, world, port, q)) for r in range(world)]
+    for pr in procs:
+        pr.start()
+    res = sorted([q.get(timeout=300) for _ in range(world)], key=lambda x: x[0])
+    for pr in procs:
+        pr.join(timeout=60)
+        assert pr.exitcode == 0
+    off = _run_jobs(_jobs_config("off"))
+    assert not off[5]
+    for r in res:
+        on = r[1:]
+        assert on[5]
+        np.testing.assert_allclose(on[0], off[0], rtol=1e-5)
+        for i in (1, 2):
+            diff = np.abs(on[i] - off[i])
+            assert int((diff > 1e-4).sum()) <= max(4, 1e-3 * diff.size) and float(diff.mean()) < 1e-5
+        same = sum(int((on[3][k] == off[3][k]).sum()) for k in on[3])
+        total = sum(len(v) for v in on[3].values())
+        assert same >= 0.99 * total
+        assert on[4] == pytest.approx(off[4], rel=1e-2)
