@@ -46,10 +46,22 @@ class ReciprocalRelationsModel(KgeModel):
         o = self.get_o_embedder().embed(o)
         return self._scorer.score_emb(o, p, s, combine="sp_")
 
+    def _xent_dropout_po(self, p, o, labels, scale, l_ptr=None, smoothing=0.0):
+        """The fused loss of (?, p, o) queries with dropout in the embedders: dropped rows drawn
+        in score_po's order (reciprocal_relations_model.py:67-74: all subjects, p + R, then o),
+        scored as (o, p + R, ?) and differentiated in one engine pass."""
+        if not self._lookup_embedders_with_dropout():
+            return None
+        ent_e, rel_e = self.get_s_embedder(), self.get_p_embedder()
+        cand = ent_e.embed_all()
+        p_inv = rel_e.embed(p + self.dataset.num_relations())
+        o = self.get_o_embedder().embed(o)
+        return self._scorer.score_emb_xent(o, p_inv, cand, "sp_", labels, scale, l_ptr, smoothing)
+
     def score_po_xent(self, p: Tensor, o: Tensor, s: Tensor, scale: float):
         tabs = self._lookup_tables()
         if tabs is None:
-            return None
+            return self._xent_dropout_po(p, o, s, scale)
         return self._scorer.score_lookup_xent(tabs[0], tabs[1], o, p + self.dataset.num_relations(), "sp_", s,
                                               scale)
 
@@ -68,7 +80,7 @@ class ReciprocalRelationsModel(KgeModel):
     def score_po_kl(self, p: Tensor, o: Tensor, l_ptr: Tensor, l_col: Tensor, smoothing: float, scale: float):
         tabs = self._lookup_tables()
         if tabs is None:
-            return None
+            return self._xent_dropout_po(p, o, l_col, scale, l_ptr, smoothing)
         return self._scorer.score_lookup_xent(tabs[0], tabs[1], o, p + self.dataset.num_relations(), "sp_", l_col,
                                               scale, l_ptr, smoothing)
 

@@ -14,12 +14,17 @@ pytestmark = pytest.mark.gpu
 GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
 
 
-def _job(graph, precision="fp32", E=700, R=9, dim=64, seed=0):
+def _job(graph, precision="fp32", E=700, R=9, dim=64, seed=0, reciprocal=False):
     from kge import Config, Dataset
     from kge.job import TrainingJob
 
     c = Config()
-    c.set("model", "complex")
+    if reciprocal:
+        c.set("model", "reciprocal_relations_model")
+        c._import("reciprocal_relations_model")
+        c.set("reciprocal_relations_model.base_model.type", "complex")
+    else:
+        c.set("model", "complex")
     c._import("complex")
     c.set("job.device", "cuda")
     c.set("lookup_embedder.dim", dim)
@@ -433,14 +438,16 @@ def test_graph_step_with_adam_matches_eager():
     assert off.mean() < 0.05 and np.abs(runs[True][1] - runs[False][1]).max() < 0.2
 
 
+@pytest.mark.parametrize("reciprocal", [False, True])
 @pytest.mark.parametrize("precision", ["bf16x3", "fp32"])
 @pytest.mark.parametrize("direction", ["sp_", "_po"])
-def test_fused_loss_with_embedder_dropout_matches_unfused(direction, precision):
+def test_fused_loss_with_embedder_dropout_matches_unfused(direction, precision, reciprocal):
     """lookup_embedder.dropout > 0 in training mode: score_sp_xent / score_po_xent score dropped
     query rows against a dropped copy of the table in one engine pass.  Under the same seed the
     unfused path (score_sp / score_po, torch cross entropy) draws the same masks: same loss, same
-    gradients."""
-    job, tr = _job(False, precision)
+    gradients.  The reciprocal-relations model draws its (?, p, o) rows in its own order
+    (reciprocal_relations_model.py:67-74)."""
+    job, tr = _job(False, precision, reciprocal=reciprocal)
     m = job.model
     for e in (m._entity_embedder, m._relation_embedder):
         e.dropout.p = 0.3
@@ -470,13 +477,14 @@ def test_fused_loss_with_embedder_dropout_matches_unfused(direction, precision):
     assert float(m.score_sp_xent(s, p, o, 1.0 / 64).detach()) != first
 
 
-def test_graph_step_with_embedder_dropout_records_and_redraws_masks():
+@pytest.mark.parametrize("reciprocal", [False, True])
+def test_graph_step_with_embedder_dropout_records_and_redraws_masks(reciprocal):
     """Dropout in the lookup embedders keeps the step on the recorded path: torch's dropout is
     part of the recording and every replay draws new masks (replaying one batch twice gives two
     different losses); the loss falls over the run like the eager job's."""
     runs = {}
     for graph in (True, False):
-        job, tr = _job(graph, "bf16x3")
+        job, tr = _job(graph, "bf16x3", reciprocal=reciprocal)
         for e in (job.model._entity_embedder, job.model._relation_embedder):
             e.dropout.p = 0.2
         job._prepare()  # decides on the graph step with the dropout in place
