@@ -643,22 +643,27 @@ class TrainingJobKvsAll(TrainingJob):
     def _prepare(self):
         super()._prepare()
         self.query_types = [k for k, v in self.config.get("KvsAll.query_types").items() if v]
-        if "s_o" in self.query_types:
-            raise NotImplementedError("KvsAll query type s_o is outside the scoring path")
         self.query_indexes = []
         self.query_last_example = []
         self.num_examples = 0
+        index_of = {"sp_": "sp_to_o", "s_o": "so_to_p", "_po": "po_to_s"}  # train.py:568-577
         for qt in self.query_types:
-            idx = self.dataset.index(f"{self.train_split}_{'sp_to_o' if qt == 'sp_' else 'po_to_s'}")
+            idx = self.dataset.index(f"{self.train_split}_{index_of[qt]}")
             self.query_indexes.append(idx)
             self.num_examples += len(idx)
             self.query_last_example.append(self.num_examples)
         # How the model scores each query type, as (engine direction, key column of the entity
         # index, key column of the relation index, offset added to the relation index): asked of
         # the model itself (a reciprocal-relations model answers (?, p, o) as (o, p + R, ?)).
+        # (s, ?, o) queries score relations (KgeModel.score_so): outside the engine's all-entities
+        # passes, they run per query type through the scorer's generic path.
+        entity_targets = "s_o" not in self.query_types
         self._part_spec = []
         for qt in self.query_types:
             k0, k1 = torch.tensor([0]), torch.tensor([1])
+            if qt == "s_o":
+                self._part_spec.append(None)
+                continue
             if qt == "sp_":  # keys (s, p)
                 d, e, r, _, _ = self.model.xent_part_sp(k0, k1, None)
             else:  # keys (p, o)
@@ -671,7 +676,7 @@ class TrainingJobKvsAll(TrainingJob):
         self._graph_step = None  # decided anew by every _prepare
         if (self.config.get("engine.graph_step") and self.config.get("engine.fused_loss")
                 and isinstance(self.loss, KLDivWithSoftmaxKgeLoss)
-                and 1 <= len(self.query_types) <= 2
+                and 1 <= len(self.query_types) <= 2 and entity_targets
                 and torch.device(self.device).type == "cuda"
                 and hasattr(opt, "graph_safe") and opt.graph_safe()
                 and not self.pre_batch_hooks
@@ -775,7 +780,7 @@ class TrainingJobKvsAll(TrainingJob):
             rows = np.repeat(first[sel], n) + np.arange(int(n.sum()), dtype=np.int64) - np.repeat(np.cumsum(n) - n, n)
             pos = np.repeat(ix.offsets[local], n) + np.arange(int(n.sum()), dtype=np.int64) - np.repeat(
                 np.cumsum(n) - n, n)
-            k1_col, k2_col, target_col = (S, P, O) if qt == "sp_" else (P, O, S)
+            k1_col, k2_col, target_col = {"sp_": (S, P, O), "s_o": (S, O, P), "_po": (P, O, S)}[qt]
             triples[rows, k1_col] = np.repeat(ix.keys[local, 0], n)
             triples[rows, k2_col] = np.repeat(ix.keys[local, 1], n)
             triples[rows, target_col] = ix.values[pos]
@@ -812,7 +817,7 @@ class TrainingJobKvsAll(TrainingJob):
         fwd = bwd = 0.0
         total = None
         fused = self.config.get("engine.fused_loss") and isinstance(self.loss, KLDivWithSoftmaxKgeLoss)
-        if fused and len(self.query_types) == 2:
+        if fused and len(self.query_types) == 2 and "s_o" not in self.query_types:
             res = self._process_batch_fused2(ex, bs)
             if res is not None:
                 return res
@@ -826,7 +831,7 @@ class TrainingJobKvsAll(TrainingJob):
             t -= time.time()
             q, l_ptr, l_col = self._queries(qi, sel)
             loss = None
-            if self.config.get("engine.fused_loss") and isinstance(self.loss, KLDivWithSoftmaxKgeLoss):
+            if fused and qt != "s_o":
                 # positives as a CSR (no dense label matrix); KL + gradient in the engine
                 t += time.time()
                 fwd -= time.time()
@@ -835,15 +840,18 @@ class TrainingJobKvsAll(TrainingJob):
                 fwd += time.time()
                 t -= time.time()
             if loss is None:
-                labels = torch.zeros(len(sel), E, device=self.device)
+                width = self.dataset.num_relations() if qt == "s_o" else E
+                labels = torch.zeros(len(sel), width, device=self.device)
                 rows = torch.repeat_interleave(torch.arange(len(sel), device=self.device), l_ptr[1:] - l_ptr[:-1])
                 labels[rows, l_col] = 1.0
-                if self.label_smoothing > 0.0:
+                if self.label_smoothing > 0.0 and qt != "s_o":  # entity targets only (train.py:715-721)
                     labels = (1.0 - self.label_smoothing) * labels + 1.0 / E
                 t += time.time()
                 fwd -= time.time()
                 if qt == "sp_":
                     scores = self.model.score_sp(q[:, 0], q[:, 1])
+                elif qt == "s_o":
+                    scores = self.model.score_so(q[:, 0], q[:, 1])
                 else:
                     scores = self.model.score_po(q[:, 0], q[:, 1])
                 loss = self.loss(scores, labels) / bs

@@ -33,6 +33,8 @@ Fixtures written:
   count (E = 14,541, R = 237, ComplEx-512, N(0, 0.1) tables regenerated from a recorded numpy
   seed -- the 30 MB tables themselves are not stored, a checksum is), 512 evaluation triples
   filtered against 30,000 training triples, with test filtering;
+* ``train_kvsall_so_distmult.npz`` -- the same with (s, ?, o) relation queries enabled as well
+  (three query types; label smoothing on entity targets only).
 * ``train_kvsall_distmult.npz`` -- F7: three KvsAll batches (DistMult, sp_ and _po queries,
   label smoothing, KL, Adagrad) with the queries / labels of each batch, the per-batch loss
   the reference reports and the final tables;
@@ -442,7 +444,7 @@ def gen_eval_fullsize():
     return fn
 
 
-def gen_kvsall_fixture():
+def gen_kvsall_fixture(with_so=False):
     from kge.job import TrainingJob
 
     E, R, splits = make_dataset_splits()
@@ -452,6 +454,7 @@ def gen_kvsall_fixture():
     config = ds_config("distmult", dim, folder, E, R, {
         "train.type": "KvsAll", "train.optimizer": "Adagrad", "train.optimizer_args": {"lr": 0.2},
         "train.loss": "kl", "train.batch_size": bs, "KvsAll.label_smoothing": 0.1,
+        "KvsAll.query_types.s_o": with_so,
     })
     ds = Dataset.create(config, folder=folder)
     gen = torch.Generator().manual_seed(12)
@@ -469,6 +472,7 @@ def gen_kvsall_fixture():
         out[f"queries_{b}"] = batch["queries"].numpy()
         out[f"qtype_{b}"] = batch["query_type_indexes"].numpy()
         out[f"label_coords_{b}"] = batch["label_coords"].numpy()
+        out[f"triples_{b}"] = batch["triples"].numpy()  # what weighted penalties count on
         # tables before the batch and the gradients its backward leaves (before the step)
         out[f"ent_before_{b}"] = job.model._entity_embedder._embeddings.weight.detach().clone().numpy()
         out[f"rel_before_{b}"] = job.model._relation_embedder._embeddings.weight.detach().clone().numpy()
@@ -484,7 +488,7 @@ def gen_kvsall_fixture():
     out["meta"] = np.array(json.dumps(dict(
         E=E, R=R, dim=dim, model="distmult", lr=0.2, optimizer="Adagrad", loss="kl", batch_size=bs,
         label_smoothing=0.1, query_types=job.query_types, num_batches=nb, torch=torch.__version__)))
-    fn = os.path.join(OUT, "train_kvsall_distmult.npz")
+    fn = os.path.join(OUT, "train_kvsall_so_distmult.npz" if with_so else "train_kvsall_distmult.npz")
     np.savez_compressed(fn, **out)
     return fn
 
@@ -808,6 +812,7 @@ def main():
         written.append(gen_train_fixture())
         written.append(gen_shapes())
     extra = {"eval_fullsize": gen_eval_fullsize, "kvsall": gen_kvsall_fixture,
+             "kvsall_so": lambda: gen_kvsall_fixture(with_so=True),
              "ns_rotate": lambda: gen_ns_fixture("rotate"), "ns_complex": lambda: gen_ns_fixture("complex"),
              "toy": gen_toy_fixture, "score_so": gen_score_so_fixture, "eval_metrics_per": gen_eval_metrics_per,
              "penalties": gen_penalty_fixture}

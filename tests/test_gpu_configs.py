@@ -370,20 +370,24 @@ def _example_ids(job, queries, qtype):
     return torch.tensor(ids, dtype=torch.int64)
 
 
+@pytest.mark.parametrize("query_types", [["sp_", "_po"], ["sp_", "s_o", "_po"]], ids=["sp_po", "sp_so_po"])
 @pytest.mark.parametrize("fused", [True, False], ids=["fused_kl", "torch_kl"])
 @pytest.mark.parametrize("precision,atol", [("fp32", 1e-4), ("bf16x3", 2e-4)])
-def test_c3_kvsall_trajectory_vs_reference(precision, atol, fused):
+def test_c3_kvsall_trajectory_vs_reference(precision, atol, fused, query_types):
     """Three reference KvsAll batches (DistMult, sp_ + _po queries, label smoothing 0.1, KL,
     Adagrad): the same queries with the same label sets, the loss the reference reports per
-    batch (its last query type's, train.py:747) and the tables after the three steps."""
+    batch (its last query type's, train.py:747) and the tables after the three steps.  With
+    (s, ?, o) queries as well: relation targets through score_so, not smoothed (train.py:715-751)."""
     from kge.job import TrainingJob
 
-    f = np.load(os.path.join(GOLDEN, "train_kvsall_distmult.npz"))
+    name = "train_kvsall_so_distmult.npz" if "s_o" in query_types else "train_kvsall_distmult.npz"
+    f = np.load(os.path.join(GOLDEN, name))
     meta = json.loads(str(f["meta"]))
-    assert meta["query_types"] == ["sp_", "_po"]
+    assert meta["query_types"] == query_types
     c = base_config("distmult", meta["dim"], meta["E"], meta["R"], {
         "train.type": "KvsAll", "train.optimizer": "Adagrad", "train.optimizer_args": {"lr": meta["lr"]},
         "train.batch_size": meta["batch_size"], "KvsAll.label_smoothing": meta["label_smoothing"],
+        "KvsAll.query_types.s_o": "s_o" in query_types,
         "engine.precision": precision, "engine.fused_loss": fused})
     ds = dataset_from(c, f)
     job = TrainingJob.create(c, ds)
@@ -404,6 +408,8 @@ def test_c3_kvsall_trajectory_vs_reference(precision, atol, fused):
             mine = ix.values[ix.offsets[e]:ix.offsets[e + 1]]
             assert sorted(mine.tolist()) == sorted(coords[coords[:, 0] == row, 1].tolist())
         batches.append(ids)
+        # the batch's true triples, one per (query, label) in batch order (train.py:625-674)
+        assert np.array_equal(job._batch_triples(ids.numpy()).numpy(), f[f"triples_{b}"])
         # (1) from the reference's tables before this batch: its loss and its gradients
         set_tables(job.model, f[f"ent_before_{b}"], f[f"rel_before_{b}"])
         job.optimizer.zero_grad()
