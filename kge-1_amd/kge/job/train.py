@@ -501,6 +501,11 @@ class TrainingJob1vsAll(TrainingJob):
     def _collate(self, example_ids):
         return {"triples": self.dataset.split(self.train_split)[example_ids, :].long()}
 
+    def _penalty_backward(self, batch_index, batch):
+        if self._sharded is not None:
+            return self._sharded.penalty_backward(batch)
+        return super()._penalty_backward(batch_index, batch)
+
     def _process_batch(self, batch_index, batch) -> TrainingJob._ProcessBatchResult:
         """train.py:1032-1062: sp then po, each loss / B followed by backward.  With
         engine.fused_loss and the kl loss, scoring + cross entropy + its gradient of both
@@ -575,9 +580,6 @@ class ShardedTraining1vsAll:
 
         if not isinstance(job.loss, KLDivWithSoftmaxKgeLoss):
             raise NotImplementedError("row-sharded 1vsAll training supports train.loss kl only")
-        emb = (job.model.get_s_embedder(), job.model.get_p_embedder())
-        if any(getattr(e, "penalty_active", lambda: False)() for e in emb):
-            raise NotImplementedError("row-sharded training does not support embedding penalties")
         if job.model._lookup_tables() is None and job.sharded_ops is None:
             raise NotImplementedError("row-sharded training needs plain lookup embedders and an engine scorer")
         self.job = job
@@ -617,6 +619,38 @@ class ShardedTraining1vsAll:
         self.ent_param.grad = d_ent
         self.rel_param.grad = d_rel
         return TrainingJob._ProcessBatchResult(loss, len(triples), t, fwd, 0.0)
+
+    def penalty_backward(self, batch):
+        """The embedders' Lp penalty terms of the batch (kge_model.py:588-605,
+        lookup_embedder.py:112-158) on the row-sharded table: each rank differentiates the
+        entity terms over ITS rows -- its share of the whole-table norm, or the subjects and
+        objects of the global batch that fall into its shard, divided by the batch's full
+        index count -- and every rank the replicated relation term.  Returns the value the
+        unsharded job reports: the ranks' entity parts summed, plus the relation term."""
+        from ..sharded import all_reduce
+
+        model = self.job.model
+        ent_e, rel_e = model.get_s_embedder(), model.get_p_embedder()
+        if not (ent_e.penalty_active() or rel_e.penalty_active()):
+            return 0.0
+        triples = batch["triples"].to(self.job.device).long()
+        local = torch.zeros((), device=triples.device)
+        replicated = torch.zeros((), device=triples.device)
+        with torch.enable_grad():
+            for emb, param, cols in ((ent_e, self.ent_param, (S, O)), (rel_e, self.rel_param, (P,))):
+                if not emb.penalty_active():
+                    continue
+                for col in cols:
+                    idx = triples[:, col]
+                    if param is self.ent_param:
+                        idx = idx[(idx >= self.lo) & (idx < self.hi)] - self.lo
+                    value = emb.lp_term(param, idx, len(triples))
+                    value.backward()  # adds to the gradient process_batch left on the parameter
+                    if param is self.ent_param:
+                        local += value.detach()
+                    else:
+                        replicated += value.detach()
+        return all_reduce(local) + replicated
 
     def sync_model(self):
         """All-gather the shards into every rank's full entity table (before unsharded

@@ -139,6 +139,22 @@ class LookupEmbedder(KgeEmbedder):
         """Whether the penalty weights each row by its frequency among the batch's indexes."""
         return self.penalty_active() and bool(self.get_option("regularize_args.weighted"))
 
+    def lp_term(self, weight: Tensor, indexes: Tensor, count: int) -> Tensor:
+        """The Lp term of penalty() (lookup_embedder.py:112-158) over ``weight`` in place of the
+        embedder's whole table: w / p * sum |weight|^p, or, frequency-weighted, over the rows
+        ``indexes`` of ``weight`` (each as often as it occurs) divided by ``count``.  A
+        row-sharded table sums this over its shards: rank k passes its rows, the batch's
+        indexes that fall into them, and the batch's full index count."""
+        p = self.get_option("regularize_args.p") if self.has_option("regularize_args.p") else 2
+        w = self.get_option("regularize_weight")
+        if not self.get_option("regularize_args.weighted"):
+            return (w / p * weight.norm(p=p) ** p).sum()
+        unique_indexes, counts = torch.unique(indexes, return_counts=True)
+        rows = weight[unique_indexes]
+        if p % 2 == 1:
+            rows = torch.abs(rows)
+        return (w / p * (rows ** p * counts.float().view(-1, 1))).sum() / count
+
     def penalty(self, **kwargs) -> List:
         """Lp regularisation (lookup_embedder.py:112-158).
 

@@ -495,49 +495,59 @@ def _jobs_config(mode, precision="fp32"):
     return c
 
 
-def _run_jobs(c):
+def _run_jobs(c, penalties=False):
     from kge import Dataset
     from kge.job import EntityRankingJob, TrainingJob
 
     ds = Dataset.synthetic(c, "toy", seed=1, num_entities=700, num_relations=9, sizes=(2000, 150, 150))
     torch.manual_seed(11)
     job = TrainingJob.create(c, ds)
+    if penalties:  # frequency-weighted L3 on the (sharded) entity table, plain L2 on the relations
+        for e, w, p, weighted in ((job.model._entity_embedder, 1e-2, 3, True),
+                                  (job.model._relation_embedder, 5e-3, 2, False)):
+            e.config.set(e.configuration_key + ".regularize_weight", w)
+            e.config.set(e.configuration_key + ".regularize_args.p", p)
+            e.config.set(e.configuration_key + ".regularize_args.weighted", weighted)
     traces = job.run()
+    if penalties:
+        assert min(t["avg_penalty"] for t in traces) > 0
     ev = EntityRankingJob(c, ds, model=job.model)
     ev.capture_ranks = True
     et = ev.run()
-    return ([t["avg_loss"] for t in traces], job.model._entity_embedder._embeddings.weight.detach().cpu().numpy(),
+    return ([t["avg_loss"] + t["avg_penalty"] for t in traces], job.model._entity_embedder._embeddings.weight.detach().cpu().numpy(),
             job.model._relation_embedder._embeddings.weight.detach().cpu().numpy(), ev.ranks,
             et["mean_reciprocal_rank_filtered_with_test"], job._sharded is not None)
 
 
-def _world2_jobs_worker(rank, world, port, out_q):
+def _world2_jobs_worker(rank, world, port, out_q, penalties):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        out_q.put((rank,) + _run_jobs(_jobs_config("on")))
+        out_q.put((rank,) + _run_jobs(_jobs_config("on"), penalties))
     finally:
         dist.destroy_process_group()
 
 
-def test_sharded_jobs_world2_on_the_engine_match_unsharded_jobs(L):
+@pytest.mark.parametrize("penalties", [False, True], ids=["plain", "lp_penalties"])
+def test_sharded_jobs_world2_on_the_engine_match_unsharded_jobs(L, penalties):
     """TrainingJob1vsAll and EntityRankingJob row-sharded over TWO ranks with the engine's kernels
     (both on this GPU, gloo through host memory): after sync_model both ranks hold the tables the
-    unsharded job trains, the loss trajectory and the evaluation ranks are the same."""
+    unsharded job trains, the loss (plus penalty) trajectory and the evaluation ranks are the same;
+    also with Lp penalties, whose entity terms every rank differentiates over its own rows."""
     import torch.multiprocessing as mp
 
     world = 2
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_world2_jobs_worker, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=_world2_jobs_worker, args=(r, world, port, q, penalties)) for r in range(world)]
     for pr in procs:
         pr.start()
     res = sorted([q.get(timeout=300) for _ in range(world)], key=lambda x: x[0])
     for pr in procs:
         pr.join(timeout=60)
         assert pr.exitcode == 0
-    off = _run_jobs(_jobs_config("off"))
+    off = _run_jobs(_jobs_config("off"), penalties)
     assert not off[5]
     for r in res:
         on = r[1:]

@@ -92,7 +92,30 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _worker(rank, world, port, out_q):
+#: penalty cases: (weight, p, weighted) of the entity and of the relation embedder
+PENALTIES = {"ent_weighted_l3": ((2e-2, 3, True), (1e-2, 2, False)),
+             "ent_unweighted_l2": ((5e-3, 2, False), (2e-2, 3, True))}
+
+
+def _set_penalties(job, case):
+    m = job.model
+    for e, (w, p, weighted) in zip((m._entity_embedder, m._relation_embedder), PENALTIES[case]):
+        e.config.set(e.configuration_key + ".regularize_weight", w)
+        e.config.set(e.configuration_key + ".regularize_args.p", p)
+        e.config.set(e.configuration_key + ".regularize_args.weighted", weighted)
+        assert e.penalty_active() and e.penalty_weighted() == weighted
+
+
+def _lp(table, idx, w, p, weighted):
+    """lookup_embedder.py:112-158 on the whole table."""
+    if not weighted:
+        return w / p * table.norm(p=p) ** p
+    u, cnt = torch.unique(idx, return_counts=True)
+    rows = table[u].abs() if p % 2 == 1 else table[u]
+    return (w / p * (rows ** p * cnt.float().view(-1, 1))).sum() / len(idx)
+
+
+def _worker(rank, world, port, out_q, penalties=None):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
@@ -103,6 +126,8 @@ def _worker(rank, world, port, out_q):
         ds = Dataset(c, None)
         ds._triples = {k: torch.from_numpy(v.astype(np.int32)) for k, v in _splits().items()}
         job = TrainingJob.create(c, ds)
+        if penalties:
+            _set_penalties(job, penalties)
         ent0, rel0 = _tables()
         with torch.no_grad():
             job.model._entity_embedder._embeddings.weight.copy_(ent0)
@@ -111,6 +136,12 @@ def _worker(rank, world, port, out_q):
         traces = job.run()
         assert job._sharded is not None and job._sharded.world == world
         lo, hi = job._sharded.lo, job._sharded.hi
+        if penalties:
+            job._sharded.sync_model()
+            out_q.put((rank, [t["avg_loss"] for t in traces], [t["avg_penalty"] for t in traces],
+                       job.model._entity_embedder._embeddings.weight.detach().numpy().copy(),
+                       job.model._relation_embedder._embeddings.weight.detach().numpy().copy()))
+            return
         state_rows = [tuple(st["sum"].shape) for st in job.optimizer.state.values()]
         job._sharded.sync_model()
         for k in ("head_and_tail", "relation_type", "argument_frequency"):
@@ -129,7 +160,7 @@ def _worker(rank, world, port, out_q):
         dist.destroy_process_group()
 
 
-def _unsharded_reference():
+def _unsharded_reference(penalties=None):
     """The same training run without any sharding, by torch autograd."""
     splits = _splits()
     ent0, rel0 = _tables()
@@ -138,10 +169,11 @@ def _unsharded_reference():
     opt = torch.optim.Adagrad([ent, rel], lr=0.1)
     gen = torch.Generator().manual_seed(SEED)
     train = torch.from_numpy(splits["train"])
-    losses, valid_mrr = [], []
+    losses, valid_mrr, pens = [], [], []
     for _ in range(EPOCHS):
         perm = torch.randperm(len(train), generator=gen)
         tot = 0.0
+        pen_tot, n_batches = 0.0, 0
         for b in range(0, len(train), BS):
             tr = train[perm[b:b + BS]]
             opt.zero_grad()
@@ -149,13 +181,25 @@ def _unsharded_reference():
             for direction, e_col, lab_col in ((0, 0, 2), (1, 2, 0)):
                 q = _prep(direction, ent, tr[:, e_col], rel, tr[:, 1])
                 loss = loss + torch.nn.functional.cross_entropy(q @ ent.T, tr[:, lab_col], reduction="sum") / len(tr)
+            if penalties:  # kge_model.py:588-605: subjects, relations, objects
+                (we, pe, ee), (wr, pr, er) = PENALTIES[penalties]
+                pen = (_lp(ent, tr[:, 0], we, pe, ee) + _lp(rel, tr[:, 1], wr, pr, er)
+                       + _lp(ent, tr[:, 2], we, pe, ee))
+                pen_tot += float(pen.detach())
+                loss = loss + pen
+            n_batches += 1
             loss.backward()
             opt.step()
-            tot += float(loss.detach()) * len(tr)
+            tot += float(loss.detach()) * len(tr) - (float(pen.detach()) * len(tr) if penalties else 0.0)
         losses.append(tot / len(train))
+        pens.append(pen_tot / n_batches)
+        if penalties:
+            continue
         _, m = K.entity_ranking("complex", ent.detach().double().numpy(), rel.detach().double().numpy(), splits,
                                 eval_split="valid", filter_splits=("train", "valid"), batch_size=7)
         valid_mrr.append(m["mean_reciprocal_rank_filtered_with_test"])
+    if penalties:
+        return losses, pens, ent.detach().numpy(), rel.detach().numpy()
     return losses, valid_mrr, ent.detach().numpy(), rel.detach().numpy()
 
 
@@ -194,6 +238,32 @@ def test_sharded_training_and_eval_jobs_world2_match_unsharded():
             np.testing.assert_array_equal(ranks[k], v, err_msg=k)
         for k, v in ometrics.items():
             assert metrics[k] == pytest.approx(v, rel=1e-5, abs=1e-9), k
+
+
+@pytest.mark.parametrize("case", sorted(PENALTIES))
+def test_sharded_training_with_embedding_penalties_world2_matches_unsharded(case):
+    """Lp penalties on a row-sharded table: every rank differentiates the entity terms over its
+    own rows (frequency-weighted over the global batch's indexes that fall into them, or its
+    share of the whole-table norm), the relation term is replicated; loss, reported penalty and
+    trained tables equal the unsharded run's."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q, case)) for r in range(world)]
+    for pr in procs:
+        pr.start()
+    res = sorted([q.get(timeout=240) for _ in range(world)], key=lambda x: x[0])
+    for pr in procs:
+        pr.join(timeout=60)
+        assert pr.exitcode == 0
+    ref_losses, ref_pens, ref_ent, ref_rel = _unsharded_reference(case)
+    assert min(ref_pens) > 0
+    for rank, losses, pens, ent, rel in res:
+        np.testing.assert_allclose(losses, ref_losses, rtol=1e-5)
+        np.testing.assert_allclose(pens, ref_pens, rtol=1e-5)
+        np.testing.assert_allclose(ent, ref_ent, atol=2e-5)
+        np.testing.assert_allclose(rel, ref_rel, atol=2e-5)
 
 
 def _worker_reciprocal(rank, world, port, out_q):
