@@ -57,6 +57,7 @@ class TrainingJobNegativeSampling(TrainingJob):
 
     def _prepare(self):
         super()._prepare()
+        self._replicas_only()
         self.num_examples = self.dataset.split(self.train_split).size(0)
 
     def _collate(self, example_ids):

@@ -82,6 +82,20 @@ class TrainingJob(Job):
     def _prepare(self):
         self.model.prepare_job(self)
 
+    def _replicas_only(self):
+        """For the training types whose step has no all-entities softmax to split by rows (KvsAll,
+        negative sampling): engine.row_sharded "on" is refused, and under "auto" in a world of
+        several processes every process trains its own replica, which is said once."""
+        from ..sharded import sharding_enabled
+
+        if not sharding_enabled(self.config):
+            return
+        if self.config.get("engine.row_sharded") == "on":
+            raise NotImplementedError(f"engine.row_sharded: on -- the {self.type_str} training job does not shard "
+                                      f"the entity table (1vsAll training and entity ranking do)")
+        self.config.log(f"{self.type_str} training does not shard the entity table: every process of this "
+                        f"torch.distributed world trains a replica of its own (engine.row_sharded: auto)")
+
     def _run(self):
         """The epoch loop of train.py:136-250: train an epoch, validate every valid.every
         epochs (EvaluationJob on valid.split sharing this model), step the LR scheduler
@@ -676,6 +690,7 @@ class TrainingJobKvsAll(TrainingJob):
 
     def _prepare(self):
         super()._prepare()
+        self._replicas_only()
         self.query_types = [k for k, v in self.config.get("KvsAll.query_types").items() if v]
         self.query_indexes = []
         self.query_last_example = []

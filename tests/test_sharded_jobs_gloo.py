@@ -321,3 +321,27 @@ def test_sharded_rank_counts_reciprocal_relations_world2():
         np.testing.assert_array_equal(counts[:, :, :2 * B], ref[:, :, :2 * B])
     # and the two sides really differ (an undirected true score would be wrong here)
     assert not np.array_equal(ref[0], ref[1])
+
+
+@pytest.mark.parametrize("train_type", ["KvsAll", "negative_sampling"])
+def test_row_sharded_on_is_refused_by_the_training_types_that_do_not_shard(train_type):
+    """engine.row_sharded: on with a training type whose step has no all-entities softmax to
+    split by rows fails loudly instead of silently training replicas."""
+    from kge import Dataset
+    from kge.job import TrainingJob
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()))
+    dist.init_process_group("gloo", rank=0, world_size=1)
+    try:
+        c = _config()
+        c.set("train.type", train_type)
+        c.set("engine.row_sharded", "on")
+        ds = Dataset(c, None)
+        ds._triples = {k: torch.from_numpy(v.astype(np.int32)) for k, v in _splits().items()}
+        job = TrainingJob.create(c, ds)
+        with pytest.raises(NotImplementedError, match="does not shard"):
+            job._prepare()
+        c.set("engine.row_sharded", "auto")  # a world of one process: nothing to say, nothing sharded
+        job._replicas_only()
+    finally:
+        dist.destroy_process_group()
