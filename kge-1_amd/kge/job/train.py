@@ -83,9 +83,9 @@ class TrainingJob(Job):
         self.model.prepare_job(self)
 
     def _replicas_only(self):
-        """For the training types whose step has no all-entities softmax to split by rows (KvsAll,
-        negative sampling): engine.row_sharded "on" is refused, and under "auto" in a world of
-        several processes every process trains its own replica, which is said once."""
+        """For the training types without a row-sharded step (KvsAll, negative sampling; the
+        vocab-parallel step serves 1vsAll): engine.row_sharded "on" is refused, and under "auto"
+        in a world of several processes every process trains its own replica, which is said once."""
         from ..sharded import sharding_enabled
 
         if not sharding_enabled(self.config):

@@ -325,8 +325,8 @@ def test_sharded_rank_counts_reciprocal_relations_world2():
 
 @pytest.mark.parametrize("train_type", ["KvsAll", "negative_sampling"])
 def test_row_sharded_on_is_refused_by_the_training_types_that_do_not_shard(train_type):
-    """engine.row_sharded: on with a training type whose step has no all-entities softmax to
-    split by rows fails loudly instead of silently training replicas."""
+    """engine.row_sharded: on with a training type that has no row-sharded step fails loudly
+    instead of silently training replicas."""
     from kge import Dataset
     from kge.job import TrainingJob
 
