@@ -71,7 +71,37 @@ def parse():
                     help="N > 1: batches per rank exchanged by one all_gather in the grouped schedule")
     ap.add_argument("--c5", action="store_true", help="N = 1: also time one rank's Wikidata5M shard (configs[4])")
     ap.add_argument("--no-c5", action="store_true", help="N > 1: skip the row-sharded Wikidata5M step")
+    ap.add_argument("--launch-check", action="store_true",
+                    help="only join the process group, check that the world size equals --gpus and print "
+                         "{launch_check, n_gpus}: tests the N-rank launch without any GPU work")
     return ap.parse_args()
+
+
+def launch_ranks(args):
+    """`python bench.py --gpus N` outside torchrun: start the N ranks as a CHILD torchrun job (one
+    process per GPU, rendezvous on 127.0.0.1), relay rank 0's JSON line and return the job's exit
+    status.  Runs before this process has made any GPU call: a process that has initialised the GPU
+    must not be replaced, so the ranks are children and this process only waits for them.  The
+    reference's only multi-device launcher is a spawn pool of independent trials
+    (kge/job/search.py:20-38); this is its counterpart for ranks of one job."""
+    import socket
+    import subprocess
+
+    with socket.socket() as sk:  # a free rendezvous port
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    proc = subprocess.run(cmd, env=env, stdout=subprocess.PIPE, text=True)
+    lines = [ln for ln in proc.stdout.splitlines() if ln.startswith("{") and ln.rstrip().endswith("}")]
+    for ln in proc.stdout.splitlines():  # anything else the ranks printed goes to stderr, not the JSON channel
+        if ln not in lines and ln.strip():
+            print(ln, file=sys.stderr)
+    if lines:
+        print(lines[-1], flush=True)
+    return proc.returncode if proc.returncode != 0 or lines else 1
 
 
 def make_config(args, device):
@@ -284,9 +314,15 @@ def cpu_baseline(args, E, R, seconds, eval_ctx=None):
 
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:  # not under torchrun: launch the ranks ourselves
+        sys.exit(launch_ranks(args))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but the launcher started {world} rank(s) (WORLD_SIZE)")
+    if args.launch_check:
+        return launch_check(world, rank)
     ndev = max(1, torch.cuda.device_count())
     dev_index = local_rank % ndev  # == local_rank on a node with one GPU per rank
     if world > 1:
@@ -440,6 +476,20 @@ def main():
         out["speedup_vs_cpu"] = round(value / cb["value"], 1)
     if rank == 0:
         print(json.dumps(out))
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def launch_check(world, rank):
+    """--launch-check: the ranks meet over gloo (CPU tensors), count themselves and rank 0 prints
+    the result; no GPU call is made, so it runs on a machine without one."""
+    if world > 1:
+        dist.init_process_group("gloo")
+    t = torch.ones(1, dtype=torch.int64)
+    if world > 1:
+        dist.all_reduce(t)
+    if rank == 0:
+        print(json.dumps({"launch_check": True, "n_gpus": world, "ranks_counted": int(t)}))
     if world > 1:
         dist.destroy_process_group()
 

@@ -527,7 +527,15 @@ int kge_zero_rows(float* x, int64_t ldx, int64_t n, int d, hipStream_t st) {
 int kge_bwd3_q_splits(int64_t n, int64_t m, int d, int cus) {
   const int64_t tiles = ((n + BM - 1) / BM) * ((d + BN - 1) / BN);
   const int64_t by_k = std::max<int64_t>(1, (m + 8 * BK - 1) / (8 * BK));
-  return (int)std::max<int64_t>(1, std::min<int64_t>(by_k, cus / std::max<int64_t>(1, tiles)));
+  const int64_t asked = std::max<int64_t>(1, std::min<int64_t>(by_k, cus / std::max<int64_t>(1, tiles)));
+  // launch() rounds the K chunk up to whole BK stages, which can leave fewer chunks than asked
+  // (14,541 rows in 32 chunks -> 480-row chunks -> 31 of them): return the number of chunks that
+  // actually run, because that is how many slabs get written and must be summed.  The rounding is
+  // idempotent (c = round_up(ceil(K / s)) and s' = ceil(K / c) give round_up(ceil(K / s')) = c),
+  // so launch() arrives at the same chunk size from the returned count.
+  int64_t kchunk = (m + asked - 1) / asked;
+  kchunk = (kchunk + BK - 1) / BK * BK;
+  return (int)std::max<int64_t>(1, (m + kchunk - 1) / kchunk);
 }
 
 // Called from kge_score_dot_bwd_q / _t (gemm_bwd.hip) for KGE_PREC_BF16X3.  With a workspace

@@ -45,3 +45,24 @@ def test_bench_prints_one_json_line_with_the_contract_keys():
     for key in ("value", "unit", "cores", "kind", "sample"):
         assert key in c, key
     assert c["kind"] in ("reference", "port") and c["cores"] >= 1 and c["value"] > 0
+
+
+def test_bench_gpus_2_launches_its_own_ranks():
+    """`python bench.py --gpus 2` (no torchrun around it) starts two ranks itself and reports
+    n_gpus = 2.  A one-GPU box cannot run RCCL between two ranks, so the two share the card and
+    exchange over gloo through host memory (KGE_DIST_BACKEND, the rehearsal switch): the numbers say
+    nothing about RCCL, the launch path and the output contract are what is checked."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env["KGE_DIST_BACKEND"] = "gloo"
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "4", "--warmup",
+                          "2", "--no-c5"], capture_output=True, text=True, timeout=600, env=env)
+    assert out.returncode == 0, out.stderr[-3000:]
+    lines = [ln for ln in out.stdout.splitlines() if ln.strip()]
+    assert len(lines) == 1, lines
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["scaling"] == "weak" and d["steps"] == 4
+    assert d["config"]["global_batch"] == 2 * 1024
+    assert d["value"] == pytest.approx(2 * 1024 * d["config"]["entities"] / (d["ms_per_step"] / 1e3), rel=1e-6)
+    assert "row_sharded" in d and d["row_sharded"]["headline_schedule"] in ("pipelined", "serial", "grouped")

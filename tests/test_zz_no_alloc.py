@@ -89,3 +89,35 @@ def test_noalloc_rejects_unaligned(L):
     dq = torch.zeros(8, 64, device="cuda")
     with pytest.raises(L.EngineError):
         L.score_dot_bwd_q_noalloc(g, t, None, dq)
+
+
+@pytest.mark.parametrize("n, m, d", [(512, 14541, 512), (1024, 4100, 512)])
+def test_split_count_equals_launched_chunks(L, n, m, d):
+    """Shapes at which rounding the K chunk up to whole stages leaves FEWER chunks than the CU
+    count asks for (32 -> 31 at 512 x 14,541; 16 -> 15 at 1,024 x 4,100 on 256 CUs): the slab sum
+    must add exactly the slabs the GEMM wrote.  The workspace of the ws entry point and the
+    library's scratch are poisoned with NaN first, so a slab that is summed without having been
+    written shows up in dq."""
+    gen = torch.Generator(device="cuda").manual_seed(11)
+    t = torch.randn(m, d, device="cuda", generator=gen) * 0.1
+    g = _padded_g(n, m, gen)
+    ref64 = g.double() @ t.double()
+    scale = float(ref64.abs().max())
+    # ws entry point with a NaN-filled caller workspace (sized by the library)
+    ws_n = L.lib().kge_score_dot_bwd_q_ws_size(n, m, d, L.PREC_BF16X3)
+    assert ws_n % (n * d) == 0
+    ws = torch.full((max(ws_n, 1),), float("nan"), device="cuda")
+    dq = torch.full((n, d), float("nan"), device="cuda")
+    L._check(L.lib().kge_score_dot_bwd_q_ws(L.ptr(g), L.rows(g), L.ptr(t), L.rows(t), None, n, m, d, L.ptr(dq),
+                                            L.rows(dq), 0, L.PREC_BF16X3, L.ptr(ws), ws_n, L.stream()), "bwd_q_ws")
+    torch.cuda.synchronize()
+    assert torch.isfinite(dq).all()
+    assert float((dq.double() - ref64).abs().max()) / scale < 1e-4
+    # poison the static scratch: a call whose chunks fill all of it with NaN slabs (G = NaN)
+    gp = torch.full((2048, 14544), float("nan"), device="cuda")[:, :14541]
+    tp = torch.zeros(14541, 512, device="cuda")
+    L.score_dot_bwd_q_noalloc(gp, tp, None, torch.empty(2048, 512, device="cuda"))
+    got = torch.full((n, d), float("nan"), device="cuda")
+    L.score_dot_bwd_q_noalloc(g, t, None, got)
+    torch.cuda.synchronize()
+    assert torch.equal(got, dq)
