@@ -623,7 +623,7 @@ def sharded_c5(args, world, rank, device, prec):
            "per_gpu_mfma_frac": round(flops / sec / 1e12 / (BF16_DENSE_TFLOPS / 3.0), 4)}
     # configs[4] is a TRAINING configuration: the vocab-parallel 1vsAll gradients of one global
     # batch (world x B triples, the same on every rank: forward, cross-shard softmax statistics,
-    # gradient planes, dQ all_reduce, dE local) -- RowShardedScorer.train_1vsall_global, the body
+    # gradient planes, dQ reduce_scatter, dE local) -- RowShardedScorer.train_1vsall_global, the body
     # of ShardedTraining1vsAll's step without the optimizer
     try:
         gt = torch.Generator(device=device).manual_seed(11)  # the same batch on every rank
@@ -631,9 +631,10 @@ def sharded_c5(args, world, rank, device, prec):
                           torch.randint(0, R, (rows,), device=device, generator=gt),
                           torch.randint(0, E, (rows,), device=device, generator=gt)], 1)
         losses = []
+        tr_host = tr.cpu()  # a job's loader has the batch in host memory: the exchange plan needs no read-back
 
         def tstep(i):
-            loss, d_ent, d_rel = sharded.train_1vsall_global(tr)
+            loss, d_ent, d_rel = sharded.train_1vsall_global(tr, host_triples=tr_host)
             losses.append(loss)
             del d_ent, d_rel
         tsec = timed_loop(tstep, 3, 1, world)
@@ -643,6 +644,7 @@ def sharded_c5(args, world, rank, device, prec):
         res["train_triples_per_s"] = rows / tsec
         res["train_per_gpu_tflops"] = round(tflops / tsec / 1e12, 1)
         res["train_loss"] = float(losses[-1])
+        res["train_collectives_per_step"] = sharded.collectives_last_step
     except Exception as e:  # reported, not fatal: the scoring figures above stand
         res["train_error"] = f"{type(e).__name__}: {e}"[:300]
     del sharded, ent

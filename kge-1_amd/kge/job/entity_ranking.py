@@ -215,11 +215,8 @@ class EntityRankingJob(EvaluationJob):
         name = self.config.check("engine.eval_precision", list(_lib.PRECISIONS) + [REFINED])
         self._refine = name == REFINED
         if self._refine:
-            from ..sharded import sharding_enabled
-
-            # the row-sharded path and models without a split contraction rank exact scores
-            name = "fp32" if sharding_enabled(self.config) else "bf16x3"
-            self._refine = name == "bf16x3"
+            # models without a split contraction rank exact-fp32 scores (decided in _run_ranking)
+            name = "bf16x3"
         scorer.precision_override = name
         try:
             return self._run_ranking()
@@ -235,11 +232,18 @@ class EntityRankingJob(EvaluationJob):
         if not sharding_enabled(self.config):
             return None
         world = dist.get_world_size()
-        ent = self.model.get_s_embedder()._embeddings.weight.detach()
+        emb = self.model.get_s_embedder()
+        ent = emb._embeddings.weight.detach()
         rel = self.model.get_p_embedder()._embeddings.weight.detach()
-        lo, hi = shard_bounds(ent.shape[0], world, dist.get_rank())
+        E = self.dataset.num_entities()
+        lo, hi = shard_bounds(E, world, dist.get_rank())
         ops = self.sharded_ops if self.sharded_ops is not None else engine_ops_for(self.model)
-        return RowShardedScorer(ent[lo:hi], lo, hi, ent.shape[0], rel, ops)
+        held = getattr(emb, "shard", None)
+        if held is not None:  # a row-sharded training job's model: it holds exactly these rows
+            if held != (lo, hi):
+                raise RuntimeError(f"the model holds entity rows {held}, this rank ranks rows {(lo, hi)}")
+            return RowShardedScorer(ent, lo, hi, E, rel, ops)
+        return RowShardedScorer(ent[lo:hi], lo, hi, E, rel, ops)
 
     def _run_ranking(self) -> dict:
         was_training = self.model.training
@@ -258,6 +262,18 @@ class EntityRankingJob(EvaluationJob):
                        for name, (names, _) in self._groups.items()}
         tmax = None
         ent_rows = None
+        self._shard_refinement = None
+        if sharded is not None:
+            # per shard: near-ties of the true score among THIS rank's columns are rescored
+            # exactly (the band is |q_i| max |t_j| over the shard's rows); where that does not
+            # apply the shards rank exact-fp32 scores
+            want, self._refine = self._refine, False
+            if want and getattr(sharded.ops, "refinement", None) is not None:
+                self._shard_refinement = sharded.ops.refinement(sharded.ent)
+            if want and self._shard_refinement is None:
+                self.model.get_scorer().precision_override = "fp32"
+                if hasattr(sharded.ops, "precision"):
+                    sharded.ops.precision = self.model.get_scorer().precision()
         if self._refine:
             # refinement needs fp32 query rows that contract with whole entity rows: the bilinear
             # lookup models except CP; every other model ranks fp32 scores
@@ -335,16 +351,30 @@ class EntityRankingJob(EvaluationJob):
                 if sharded is not None:
                     # each rank counts over its own rows; one all_reduce of the int64 counts makes
                     # them global (the reference's chunk_size decomposition, entity_ranking.py:153-216)
-                    tf = self._t
-                    counts = sharded.rank_counts(
-                        s, p, o, (self._f["sp"][0][b0:], self._f["sp"][1]), (self._f["po"][0][b0:], self._f["po"][1]),
-                        (tf["sp"][0][b0:], tf["sp"][1]) if tf is not None else None,
-                        (tf["po"][0][b0:], tf["po"][1]) if tf is not None else None,
-                        p_inverse=(p + self.dataset.num_relations()) if self._two_sided else None)
+                    p_inv = (p + self.dataset.num_relations()) if self._two_sided else None
+                    counts = None
+                    if getattr(sharded.ops, "rank_rows", None) is not None:
+                        # one stacked pass per batch, as in the unsharded job
+                        (fp_sp, fp_po, f_col), tstack = self._stacked
+                        tp = (tstack[0][b0:], tstack[1][b0:]) if tstack is not None else None
+                        counts = sharded.rank_block(s, p, o, (fp_sp[b0:], fp_po[b0:]), f_col, tp,
+                                                    tstack[2] if tstack is not None else None, p_inverse=p_inv,
+                                                    refinement=self._shard_refinement)
                     rk = torch.empty(2, nrank, B, dtype=torch.int64, device=dev)
+                    if counts is not None:  # [2, rankings x (2 B)]: ranking-major, then direction
+                        c = counts.view(2, nrank, 2, B).permute(0, 2, 1, 3).contiguous()  # -> [.., direction, ranking, B]
+                        per_dir = [(c[0, di].view(-1), c[1, di].view(-1)) for di in range(2)]
+                    else:
+                        tf = self._t
+                        counts = sharded.rank_counts(
+                            s, p, o, (self._f["sp"][0][b0:], self._f["sp"][1]),
+                            (self._f["po"][0][b0:], self._f["po"][1]),
+                            (tf["sp"][0][b0:], tf["sp"][1]) if tf is not None else None,
+                            (tf["po"][0][b0:], tf["po"][1]) if tf is not None else None, p_inverse=p_inv)
+                        per_dir = [(counts[di, 0, :nrank * B], counts[di, 1, :nrank * B]) for di in range(2)]
                     for di, d in enumerate("os"):
-                        sharded.ops.rank_hist_multi(counts[di, 0, :nrank * B], counts[di, 1, :nrank * B], B,
-                                                    self.tie_handling, rk[di].view(-1), hists_sharded[di])
+                        sharded.ops.rank_hist_multi(per_dir[di][0], per_dir[di][1], B, self.tie_handling,
+                                                    rk[di].view(-1), hists_sharded[di])
                         if self.capture_ranks:
                             for ri, r in enumerate(self.rankings):
                                 ranks_out[f"{d}{r}"].append(rk[di, ri])

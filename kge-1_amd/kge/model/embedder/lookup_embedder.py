@@ -16,13 +16,40 @@ from torch import Tensor
 from ..kge_model import KgeEmbedder
 
 
+import contextlib
+import threading
+
+_state = threading.local()
+
+
+@contextlib.contextmanager
+def in_place_row_gradients():
+    """While active (this thread), the backward of embed() and of the recorded Lp penalty adds
+    its rows straight into a dense ``weight.grad`` that an earlier backward of the same step has
+    left, and hands autograd no gradient of its own.  That is only right when the caller wants
+    the gradients ACCUMULATED in ``.grad`` -- a training job around its own ``backward()`` calls.
+    Outside it the Functions return the dense gradient like any other op, so
+    ``torch.autograd.grad``, gradient hooks and accumulation wrappers see it."""
+    prev = getattr(_state, "on", False)
+    _state.on = True
+    try:
+        yield
+    finally:
+        _state.on = prev
+
+
+def _in_place_ok(held, weight, dtype) -> bool:
+    return (getattr(_state, "on", False) and held is not None and not held.is_sparse and held.dtype == dtype
+            and held.shape == weight.shape and not torch.is_grad_enabled())
+
+
 class _Rows(torch.autograd.Function):
     """weight[indexes] whose backward is one scatter-add (index_add_) -- a few microseconds on
     the device, against the sort-based embedding_dense_backward of nn.Embedding (~60 us per call
-    whatever the table's size).  When the table already holds a dense gradient (an earlier
-    backward of the step left it), the rows are added into it where it stands; otherwise into
-    a zero tensor that autograd then takes as the gradient.  Same values; rows that occur
-    several times sum their gradients by atomic adds."""
+    whatever the table's size).  Inside ``in_place_row_gradients()``, when the table already holds
+    a dense gradient (an earlier backward of the step left it), the rows are added into it where
+    it stands; otherwise into a zero tensor that autograd then takes as the gradient.  Same
+    values; rows that occur several times sum their gradients by atomic adds."""
 
     @staticmethod
     def forward(ctx, weight, indexes):
@@ -35,8 +62,7 @@ class _Rows(torch.autograd.Function):
         g = g.reshape(-1, g.shape[-1])
         idx = indexes.reshape(-1)
         held = weight.grad
-        if (held is not None and not held.is_sparse and held.dtype == g.dtype and held.shape == weight.shape
-                and not torch.is_grad_enabled()):
+        if _in_place_ok(held, weight, g.dtype):
             held.index_add_(0, idx, g)
             return None, None
         d_weight = torch.zeros(weight.shape[0], g.shape[1], device=g.device, dtype=g.dtype)
@@ -64,8 +90,7 @@ class _LpOccurrences(torch.autograd.Function):
         weight, indexes = ctx.saved_tensors
         gs = g.reshape(1).float().contiguous()
         held = weight.grad
-        if (held is not None and not held.is_sparse and held.dtype == torch.float32 and held.shape == weight.shape
-                and held.stride(1) == 1 and not torch.is_grad_enabled()):
+        if _in_place_ok(held, weight, torch.float32) and held.stride(1) == 1:
             # the loss backward has left the table's dense gradient: the touched rows are added
             # into it where it stands (no table-sized zero tensor, no table-sized add)
             _lib.lp_rows_bwd(weight, indexes, ctx.p, gs, ctx.coeff, held)
@@ -90,6 +115,39 @@ class LookupEmbedder(KgeEmbedder):
         if dropout < 0:
             dropout = 0.0
         self.dropout = torch.nn.Dropout(dropout)
+        #: (lo, hi) while this process holds only rows [lo, hi) of the table (a row-sharded job:
+        #: kge.sharded); the weight is then [hi - lo, dim] and nothing here can embed an id
+        self.shard = None
+
+    # ---- row sharding (kge.sharded): the table's rows split over the processes of a job
+    def shard_rows(self, lo: int, hi: int) -> torch.nn.Parameter:
+        """Keep only rows [lo, hi): the weight becomes a [hi - lo, dim] parameter of its own
+        storage (the full table is released) that the sharded job scores and trains.  embed /
+        embed_all / penalty and the fused scoring path refuse to run until ``unshard``."""
+        if self.shard is not None:
+            raise RuntimeError(f"{self.configuration_key}: already holds rows {self.shard} only")
+        w = self._embeddings.weight
+        return self.install_rows(torch.nn.Parameter(w.data[lo:hi].clone(), requires_grad=w.requires_grad), lo, hi)
+
+    def install_rows(self, param: torch.nn.Parameter, lo: int, hi: int) -> torch.nn.Parameter:
+        if param.shape != (hi - lo, self.dim):
+            raise ValueError(f"rows [{lo}, {hi}) of a {self.dim}-wide table, got {tuple(param.shape)}")
+        self._embeddings.weight = param
+        self.shard = (lo, hi)
+        return param
+
+    def unshard(self, full: Tensor):
+        """Install the whole [vocab_size, dim] table again (assembled from every process's rows)."""
+        if tuple(full.shape) != (self.vocab_size, self.dim):
+            raise ValueError(f"expected the whole [{self.vocab_size}, {self.dim}] table, got {tuple(full.shape)}")
+        self._embeddings.weight = torch.nn.Parameter(full)
+        self.shard = None
+
+    def _whole(self):
+        if self.shard is not None:
+            raise RuntimeError(f"{self.configuration_key}: this process holds rows [{self.shard[0]}, {self.shard[1]}) "
+                               f"of the table only (row-sharded job); score through kge.sharded.RowShardedScorer or "
+                               f"call the job's sync_model() first")
 
     def prepare_job(self, job, **kwargs):
         super().prepare_job(job, **kwargs)
@@ -111,9 +169,11 @@ class LookupEmbedder(KgeEmbedder):
         return not (self.dropout.p > 0 and self.training)
 
     def weight_for_scoring(self) -> Tensor:
+        self._whole()
         return self._embeddings.weight
 
     def embed(self, indexes: Tensor) -> Tensor:
+        self._whole()
         w = self._embeddings.weight
         if w.is_cuda and not self.sparse:
             return self._postprocess(_Rows.apply(w, indexes.long()))
@@ -121,6 +181,7 @@ class LookupEmbedder(KgeEmbedder):
 
     def embed_all(self) -> Tensor:
         # identical values and gradient to weight[arange(V)] (lookup_embedder.py:102-107)
+        self._whole()
         return self._postprocess(self._embeddings.weight)
 
     def _postprocess(self, embeddings: Tensor) -> Tensor:
@@ -165,6 +226,7 @@ class LookupEmbedder(KgeEmbedder):
         result = super().penalty(**kwargs)
         if self.regularize == "" or self.get_option("regularize_weight") == 0.0:
             return result
+        self._whole()
         p = self.get_option("regularize_args.p") if self.has_option("regularize_args.p") else 2
         w = self.get_option("regularize_weight")
         if not self.get_option("regularize_args.weighted"):

@@ -69,6 +69,54 @@ def all_gather_into_tensor(out: torch.Tensor, t: torch.Tensor, group=None, async
     return dist.all_gather_into_tensor(out, t, group=group, async_op=async_op)
 
 
+def reduce_scatter_tensor(out: torch.Tensor, t: torch.Tensor, group=None):
+    """out = this rank's block of the sum over ranks of t ([W * len(out), ...], rank-major blocks).
+    RCCL: one reduce_scatter.  gloo has no reduce_scatter: the rehearsal path all-reduces a host
+    copy and keeps the rank's block (same result, more bytes)."""
+    if dist.get_backend(group) == "gloo":
+        h = t.cpu() if t.is_cuda else t.clone()
+        dist.all_reduce(h, group=group)
+        r, n = dist.get_rank(group), out.shape[0]
+        out.copy_(h[r * n:(r + 1) * n])
+    else:
+        dist.reduce_scatter_tensor(out, t, group=group)
+    return out
+
+
+class ExchangePlan:
+    """Where every query row of a global batch lives during the owner-major exchange.
+
+    The m query rows (every rank holds the same index batch) are grouped by the rank that owns
+    their entity row; rank w contributes its c_w rows in one all_gather of cap = max_w c_w rows
+    per rank (equal block sizes: one plain all-gather), so row i of the batch sits at
+    ``slot[i] = owner_i * cap + (its position among owner_i's rows)`` of the gathered
+    [W * cap, d] block.  The same layout carries the partial query gradients back: one
+    reduce_scatter hands every owner the summed gradients of its own rows.  Built on the host
+    from the batch's entity ids (numpy, no device sync) and uploaded as one int64 vector."""
+
+    def __init__(self, e_ids, per: int, world: int, rank: int, device):
+        import numpy as np
+
+        e = np.asarray(e_ids, dtype=np.int64).reshape(-1)
+        m = e.shape[0]
+        owner = e // per if m else e
+        counts = np.bincount(owner, minlength=world)[:world] if m else np.zeros(world, np.int64)
+        order = np.argsort(owner, kind="stable")
+        starts = np.zeros(world + 1, np.int64)
+        np.cumsum(counts, out=starts[1:])
+        self.cap = int(max(1, counts.max() if m else 1))
+        slot = np.empty(m, np.int64)
+        slot[order] = owner[order] * self.cap + (np.arange(m, dtype=np.int64) - starts[owner[order]])
+        mine = order[starts[rank]:starts[rank + 1]]  # this rank's rows, ascending batch position
+        self.count = int(mine.shape[0])
+        self.m = m
+        packed = torch.from_numpy(np.concatenate([slot, mine]))
+        if torch.device(device).type == "cuda":
+            packed = packed.pin_memory().to(device, non_blocking=True)
+        self.slot, self.mine = packed[:m], packed[m:]
+        self.mine_host = mine
+
+
 class EngineOps:
     """Default compute: libkgescore."""
 
@@ -139,9 +187,9 @@ class EngineOps:
     def softmax_grad_planes(self, s, c0, labels, lse, scale):
         return self.L.softmax_grad_planes(s, c0, labels, lse, scale)
 
-    def score_bwd_planes(self, gp, hi, lo, tab, d_tab):
-        """Returns dq = G . tab (written); d_tab += G^T . Q."""
-        dq = self.L.score_dot_bwd_q_planes(gp, tab)
+    def score_bwd_planes(self, gp, hi, lo, tab, d_tab, dq=None):
+        """Returns dq = G . tab (written, into dq when given); d_tab += G^T . Q."""
+        dq = self.L.score_dot_bwd_q_planes(gp, tab, dq=dq)
         self.L.score_dot_bwd_t_planes(gp, hi, lo, d_tab, accumulate=True)
         return dq
 
@@ -179,6 +227,24 @@ class EngineOps:
 
     def rank_hist_multi(self, greater, ties, rows_per_hist, tie_handling, ranks, hists):
         self.L.rank_hist_multi(greater, ties, rows_per_hist, tie_handling, ranks, hists)
+
+    def rank_rows(self, s, n_a, c0, part_a, part_b, f_col, t_col, greater, ties, refine=None):
+        """Adds the stacked block's counts over columns [c0, c0 + s.shape[1]) (kge_rank_rows)."""
+        self.L.rank_rows(s, n_a, c0, part_a, part_b, f_col, t_col, greater, ties, accumulate=True, refine=refine)
+
+    def refinement(self, ent):
+        """(band relative to |q_i| max_j |t_j|, device scalar max_j |t_j| over ``ent``) when the
+        near-tie rescoring of kge_rank_rows applies to scores contracted against ``ent`` -- a
+        bf16x3 contraction of fp32 query rows with whole, float4-readable entity rows -- else
+        None: the caller then ranks exact-fp32 scores."""
+        from .job.entity_ranking import refine_band
+
+        if (self.precision != self.L.PREC_BF16X3
+                or self.kind not in (self.L.COMPLEX, self.L.DISTMULT, self.L.RESCAL, self.L.SIMPLE)
+                or ent.dim() != 2 or ent.stride(1) != 1 or ent.shape[1] % 4 or ent.stride(0) % 4
+                or ent.data_ptr() % 16 or ent.shape[0] == 0):
+            return None
+        return refine_band(ent.shape[1]), self.L.row_norm_max(ent)
 
 
 def sharding_enabled(config) -> bool:
@@ -375,55 +441,120 @@ class RowShardedScorer:
         loss, d_ent, d_rel = self.train_1vsall_global(self._all_gather_1d(tr.reshape(-1)).view(-1, 3))
         return float(loss), d_ent, d_rel
 
-    def train_1vsall_global(self, tr_all: torch.Tensor):
+    #: largest stacked [2 n, E_k] logits block (elements) scored in one pass; above it the two
+    #: directions run one after the other (half the live score memory)
+    STACK_MAX_ELEMS = 1 << 34
+
+    def train_1vsall_global(self, tr_all: torch.Tensor, host_triples=None):
         """train_1vsall_grads for a global batch [n, 3] that every rank already holds
         identically (the index batch is tiny, so a job hands every rank the whole batch
-        instead of gathering slices): no triple exchange, everything else as above."""
+        instead of gathering slices).  host_triples: the same batch in host memory (a job's
+        loader has it there); without it the batch is read back from the device once.
+
+        Collectives per step (4 when both directions share one contraction, else 5):
+          1. all_gather of the owner-computed query rows of BOTH directions, owner-major
+             (ExchangePlan) -- each row travels once, from its owner;
+          2. all_gather of the per-shard softmax statistics (max, sum-exp, target logit) as one
+             [3, m] block per rank; every rank forms the global max, the rescaled sum and the
+             target in the same fixed order, so lse is bit-identical everywhere;
+          3. reduce_scatter of the partial dQ = G_k . E_k in the same owner-major layout: every
+             owner receives the summed gradients of its own query rows only;
+          4. all_reduce of the relation gradient (each query's at its owner).
+        dE_k = G_k^T . Q stays local with the shard."""
         n = tr_all.shape[0]
         scale = 1.0 / n
         E_k = self.hi - self.lo
+        dev = self.ent.device
         d_ent = torch.zeros_like(self.ent)
         d_rel = torch.zeros_like(self.rel)
-        loss = torch.zeros((), device=self.ent.device, dtype=torch.float64)
-        for direction, e_col, lab_col in ((0, 0, 2), (1, 2, 0)):
-            e_all, p_all, labels = tr_all[:, e_col], tr_all[:, 1], tr_all[:, lab_col]
-            owned, local = self._owned_rows(e_all)
-            q = self.ops.prep(direction, self.ent, local, self.rel, p_all)
-            q = torch.where(owned[:, None], q, torch.zeros_like(q))
-            all_reduce(q, group=self.group)
-            buf = torch.empty(n, (E_k + 3) // 4 * 4, device=q.device, dtype=torch.float32)
+        loss = torch.zeros((), device=dev, dtype=torch.float64)
+        if n == 0:
+            return loss, d_ent, d_rel
+        dirs = ((0, 0, 2), (1, 2, 0))  # (direction, entity column, label column): sp_ then _po
+        # stacked query order: the n sp_ rows, then the n _po rows
+        e_all = torch.cat([tr_all[:, 0], tr_all[:, 2]])
+        p_all = torch.cat([tr_all[:, 1], tr_all[:, 1]])
+        labels = torch.cat([tr_all[:, 2], tr_all[:, 0]])
+        host = host_triples if host_triples is not None else tr_all.cpu()
+        host = host.numpy() if torch.is_tensor(host) else host
+        per = max(1, math.ceil(self.E / self.world))
+        import numpy as np
+
+        plan = ExchangePlan(np.concatenate([host[:, 0], host[:, 2]]), per, self.world, self.rank, dev)
+        cap, c_me = plan.cap, plan.count
+        n0 = int((plan.mine_host < n).sum())  # this rank's sp_ rows come first (stable order)
+        mine = plan.mine
+        e_mine, p_mine = e_all[mine] - self.lo, p_all[mine]
+        # ---- 1. owner-computed query rows, one all_gather
+        q_mine = None
+        for direction, a, b in ((0, 0, n0), (1, n0, c_me)):
+            if b > a:
+                part = self.ops.prep(direction, self.ent, e_mine[a:b], self.rel, p_mine[a:b])
+                if q_mine is None:
+                    q_mine = torch.empty(cap, part.shape[1], device=dev, dtype=part.dtype)
+                q_mine[a:b] = part
+        if q_mine is None:  # this rank owns none of the batch's query entities
+            q_mine = torch.empty(cap, self._win(0, self.ent).shape[1], device=dev, dtype=self.ent.dtype)
+        if c_me < cap:
+            q_mine[c_me:].zero_()
+        q_pad = torch.empty(self.world * cap, q_mine.shape[1], device=dev, dtype=q_mine.dtype)
+        all_gather_into_tensor(q_pad, q_mine, group=self.group)
+        q = q_pad.index_select(0, plan.slot)  # [2 n, d] in stacked order, identical on every rank
+        del q_pad
+        same_window = self._win(0, self.ent).data_ptr() == self._win(1, self.ent).data_ptr() and \
+            self._win(0, self.ent).shape == self._win(1, self.ent).shape
+        if same_window and 2 * n * E_k <= self.STACK_MAX_ELEMS:
+            groups = [(0, 0, 2 * n)]  # (direction of the window, first row, last row)
+        else:
+            groups = [(0, 0, n), (1, n, 2 * n)]
+        dq = torch.empty_like(q)
+        for direction, r0, r1 in groups:
+            m = r1 - r0
+            qg, lab = q[r0:r1], labels[r0:r1]
+            buf = torch.empty(m, (E_k + 3) // 4 * 4, device=dev, dtype=torch.float32)
             tab_w = self._win(direction, self.ent)
             # gradient planes pay off once the GEMMs dominate the step (a few more launches and
-            # one more [n, E_k] buffer: at 1,024 x 14,541 the fp32 path is 10 % faster, at
+            # one more [m, E_k] buffer: at 1,024 x 14,541 the fp32 path is 10 % faster, at
             # 1,024 x 574,311 the planes are 16 % faster)
-            planes = (n * E_k >= self.PLANES_MIN_ELEMS and getattr(self.ops, "train_planes_ok", None) is not None
+            planes = (m * E_k >= self.PLANES_MIN_ELEMS and getattr(self.ops, "train_planes_ok", None) is not None
                       and self.ops.train_planes_ok(self.ent, direction))
             if planes:
-                q_hi, q_lo = self.ops.split_padded(q)
-                logits = self.ops.score_split(q_hi, q_lo, n, tab_w, out=buf[:, :E_k])
+                q_hi, q_lo = self.ops.split_padded(qg)
+                logits = self.ops.score_split(q_hi, q_lo, m, tab_w, out=buf[:, :E_k])
             else:
-                logits = self.ops.score(q, tab_w, out=buf[:, :E_k])
-            mx, sm, tg = self.ops.row_stats(logits, self.lo, labels)
-            M = mx.clone()
-            all_reduce(M, op=dist.ReduceOp.MAX, group=self.group)
-            z = torch.where(mx == -math.inf, torch.zeros_like(sm), sm * torch.exp(mx - M))
-            all_reduce(z, group=self.group)
-            all_reduce(tg, group=self.group)
+                logits = self.ops.score(qg, tab_w, out=buf[:, :E_k])
+            # ---- 2. softmax statistics of every shard, one all_gather
+            mx, sm, tg = self.ops.row_stats(logits, self.lo, lab)
+            st = torch.stack([mx, sm, tg])
+            st_all = torch.empty(self.world, 3, m, device=dev, dtype=st.dtype)
+            all_gather_into_tensor(st_all.view(self.world * 3, m), st, group=self.group)
+            mx_w, sm_w, tg_w = st_all[:, 0], st_all[:, 1], st_all[:, 2]
+            M = mx_w.max(0).values
+            z = torch.where(mx_w == -math.inf, torch.zeros_like(sm_w), sm_w * torch.exp(mx_w - M)).sum(0)
             lse = M + torch.log(z)
-            loss += ((lse - tg).double().sum() * scale)
+            loss += ((lse - tg_w.sum(0)).double().sum() * scale)
             if planes:
-                gp = self.ops.softmax_grad_planes(logits, self.lo, labels, lse, scale)
+                gp = self.ops.softmax_grad_planes(logits, self.lo, lab, lse, scale)
                 del logits, buf
-                dq = self.ops.score_bwd_planes(gp, q_hi, q_lo, tab_w, self._win(direction, d_ent))
+                self.ops.score_bwd_planes(gp, q_hi, q_lo, tab_w, self._win(direction, d_ent), dq=dq[r0:r1])
                 del gp
             else:
-                g = self.ops.softmax_grad(logits, self.lo, labels, lse, scale, logits)
-                dq = torch.empty_like(q)
-                self.ops.score_bwd(g, q, tab_w, dq, self._win(direction, d_ent))
-            all_reduce(dq, group=self.group)
-            dq = torch.where(owned[:, None], dq, torch.zeros_like(dq))
-            self.ops.prep_bwd(direction, self.ent, local, self.rel, p_all, dq, d_ent, d_rel)
+                g = self.ops.softmax_grad(logits, self.lo, lab, lse, scale, logits)
+                self.ops.score_bwd(g, qg, tab_w, dq[r0:r1], self._win(direction, d_ent))
+                del g, logits, buf
+        # ---- 3. partial query gradients back to the owners, one reduce_scatter
+        dq_pad = torch.zeros(self.world * cap, dq.shape[1], device=dev, dtype=dq.dtype)
+        dq_pad.index_copy_(0, plan.slot, dq)
+        dq_mine = torch.empty(cap, dq.shape[1], device=dev, dtype=dq.dtype)
+        reduce_scatter_tensor(dq_mine, dq_pad, group=self.group)
+        del dq_pad
+        for direction, a, b in ((0, 0, n0), (1, n0, c_me)):
+            if b > a:
+                self.ops.prep_bwd(direction, self.ent, e_mine[a:b], self.rel, p_mine[a:b], dq_mine[a:b].contiguous(),
+                                  d_ent, d_rel)
+        # ---- 4. the replicated relation table's gradient
         all_reduce(d_rel, group=self.group)
+        self.collectives_last_step = 3 + len(groups)
         return loss, d_ent, d_rel  # loss: a 0-dim float64 tensor on the table's device (no host sync)
 
     # ---------------------------------------------------------------- eval
@@ -449,6 +580,45 @@ class RowShardedScorer:
             sc = self.ops.score(q, self._win(direction, self.ent))
             self.ops.rank_counts(sc, self.lo, tgt, true, f[0], f[1], t[0] if t is not None else None,
                                  t[1] if t is not None else None, counts[di, 0], counts[di, 1])
+        all_reduce(counts, group=self.group)
+        return counts
+
+    def rank_block(self, s, p, o, f_ptrs, f_col, t_ptrs=None, t_col=None, p_inverse=None, refinement=None):
+        """rank_counts as ONE stacked pass per batch: the (s, p, ?) rows on top of the (?, p, o)
+        rows, one contraction against the shard, one ranking launch over it (ops.rank_rows,
+        columns offset by this shard's first row) and one all_reduce of the counts.  f_ptrs /
+        t_ptrs: the (sp, po) CSR pointer vectors of the batch into the combined column arrays
+        f_col / t_col (EntityRankingJob._stack_csr).  refinement: ops.refinement(self.ent) --
+        near-ties of the true score inside this shard are rescored exactly, so bf16x3 scores give
+        the counts of exactly computed ones (the band is per shard: |q_i| max |t_j| over ITS
+        rows; no exchange).  Returns [2 (greater, ties), rankings x 2 B] global counts, or None
+        when the two directions contract with different entity-row windows (the caller then
+        takes rank_counts)."""
+        B = s.numel()
+        dir_b = 1 if p_inverse is None else 0
+        wa, wb = self._win(0, self.ent), self._win(dir_b, self.ent)
+        if wa.data_ptr() != wb.data_ptr() or wa.shape != wb.shape:
+            return None
+        dev = s.device
+        rows = self.gather_rows(torch.cat([s, o]))  # full s rows then o rows, on every rank
+        ar = torch.arange(B, device=dev)
+        true_o = self.ops.spo(rows[:B], self.rel, p, rows[B:]).view(-1).float().contiguous()
+        if p_inverse is None:
+            true_s, rel_b = true_o, p
+        else:
+            true_s, rel_b = self.ops.spo(rows[B:], self.rel, p_inverse, rows[:B]).view(-1).float().contiguous(), p_inverse
+        q = torch.cat([self.ops.prep(0, rows, ar, self.rel, p), self.ops.prep(dir_b, rows, ar + B, self.rel, rel_b)])
+        E_k = self.hi - self.lo
+        buf = torch.empty(2 * B, (E_k + 3) // 4 * 4, device=dev, dtype=torch.float32)
+        scores = self.ops.score(q, wa, out=buf[:, :E_k])
+        nrank = 1 + (f_ptrs is not None) + (t_ptrs is not None)
+        counts = torch.zeros(2, nrank * 2 * B, dtype=torch.int64, device=dev)
+        part_a = (o.contiguous(), true_o, f_ptrs[0] if f_ptrs is not None else None,
+                  t_ptrs[0] if t_ptrs is not None else None)
+        part_b = (s.contiguous(), true_s, f_ptrs[1] if f_ptrs is not None else None,
+                  t_ptrs[1] if t_ptrs is not None else None)
+        refine = (q, self.ent, refinement[0], refinement[1]) if refinement is not None else None
+        self.ops.rank_rows(scores, B, self.lo, part_a, part_b, f_col, t_col, counts[0], counts[1], refine=refine)
         all_reduce(counts, group=self.group)
         return counts
 

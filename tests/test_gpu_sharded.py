@@ -88,7 +88,7 @@ def test_train_1vsall_grads_world1_matches_fused(L, prec, planes):
             inner = sc.ops.softmax_grad_planes
             sc.ops.softmax_grad_planes = lambda *a: (used.append(1), inner(*a))[1]
         l2, d_ent, d_rel = sc.train_1vsall_grads(s, p, o)
-        assert len(used) == (2 if planes else 0)  # one per direction
+        assert len(used) == (1 if planes else 0)  # both directions in one stacked pass
         assert abs(l2 - loss.item()) <= 1e-5 * abs(loss.item())
         tol = 1e-4 if prec == "bf16x3" else 1e-5
         assert (d_ent - ent.grad).abs().max() <= tol * ent.grad.abs().max()
@@ -141,7 +141,12 @@ def test_sharded_jobs_world1_rccl_match_unsharded_jobs(L):
         np.testing.assert_allclose(runs["on"][0], runs["off"][0], rtol=1e-5)
         for i in (1, 2):  # tables after 16 Adagrad steps: all but a handful of ill-conditioned elements
             diff = np.abs(runs["on"][i] - runs["off"][i])
-            assert int((diff > 1e-4).sum()) <= max(4, 1e-3 * diff.size) and float(diff.mean()) < 1e-5
+            # Adagrad divides every gradient by its own running magnitude, so where the gradient is
+            # nearly zero a rounding-level difference becomes a visible step: here that is one
+            # complex component (columns 31 / 63), whose common-mode gradient sum_i q_i nearly
+            # cancels -- measured 44-64 of 44,800 elements beyond 1e-4, all in those two columns,
+            # whichever order the shards sum in
+            assert int((diff > 1e-4).sum()) <= max(4, 2e-3 * diff.size) and float(diff.mean()) < 1e-5
         same = sum(int((runs["on"][3][k] == runs["off"][3][k]).sum()) for k in runs["on"][3])
         total = sum(len(v) for v in runs["on"][3].values())
         assert same >= 0.99 * total  # two fp32 trajectories: a rare near-tie may sit on another side
@@ -555,8 +560,87 @@ def test_sharded_jobs_world2_on_the_engine_match_unsharded_jobs(L, penalties):
         np.testing.assert_allclose(on[0], off[0], rtol=1e-5)
         for i in (1, 2):
             diff = np.abs(on[i] - off[i])
-            assert int((diff > 1e-4).sum()) <= max(4, 1e-3 * diff.size) and float(diff.mean()) < 1e-5
+            # Adagrad divides every gradient by its own running magnitude, so where the gradient is
+            # nearly zero a rounding-level difference becomes a visible step: here that is one
+            # complex component (columns 31 / 63), whose common-mode gradient sum_i q_i nearly
+            # cancels -- measured 44-64 of 44,800 elements beyond 1e-4, all in those two columns,
+            # whichever order the shards sum in
+            assert int((diff > 1e-4).sum()) <= max(4, 2e-3 * diff.size) and float(diff.mean()) < 1e-5
         same = sum(int((on[3][k] == off[3][k]).sum()) for k in on[3])
         total = sum(len(v) for v in on[3].values())
         assert same >= 0.99 * total
         assert on[4] == pytest.approx(off[4], rel=1e-2)
+
+
+def _world2_fullsize_eval_worker(rank, world, port, eval_precision, out_q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import json
+
+        from conftest import GOLDEN
+        from kge import KgeModel
+        from kge.job import EntityRankingJob
+        from test_gpu_configs import base_config, dataset_from, seeded_tables, set_tables
+
+        f = np.load(os.path.join(GOLDEN, "eval_fullsize_normal.npz"))
+        meta = json.loads(str(f["meta"]))
+        E, R, dim = meta["E"], meta["R"], meta["dim"]
+        ent, rel = seeded_tables(meta["table_seed"], E, R, dim, dim, meta["std"])
+        c = base_config("complex", dim, E, R, {"eval.batch_size": meta["batch_size"], "eval.split": "valid",
+                                               "engine.row_sharded": "on", "engine.eval_precision": eval_precision})
+        ds = dataset_from(c, f)
+        model = KgeModel.create(c, ds)
+        set_tables(model, ent, rel)
+        job = EntityRankingJob(c, ds, model=model)
+        job.capture_ranks = True
+        trace = job.run()
+        out_q.put((rank, {k: v.copy() for k, v in job.ranks.items()},
+                   {k: v for k, v in trace.items() if isinstance(v, float)}, job._shard_refinement is not None))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("eval_precision", ["bf16x3_refined", "fp32"])
+def test_sharded_eval_world2_fullsize_vs_reference(L, eval_precision):
+    """The row-sharded EntityRankingJob over TWO ranks (both on this GPU, gloo through host
+    memory) against the reference's full-size capture (E = 14,541, ComplEx-512, 512 validation
+    triples, filtered + filtered-with-test): with the default eval precision every shard
+    contracts in bf16x3 and rescores the near-ties of the true score among its own columns, so
+    the summed counts are those of exactly computed scores -- every rank that differs from the
+    reference's must be explained by near-ties within 1e-5 of the row maximum, as for the
+    unsharded job."""
+    import json
+
+    import torch.multiprocessing as mp
+
+    from conftest import GOLDEN
+    from test_gpu_configs import assert_rank_moves_are_near_ties, seeded_tables
+
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_world2_fullsize_eval_worker, args=(r, world, port, eval_precision, q))
+             for r in range(world)]
+    for pr in procs:
+        pr.start()
+    res = sorted([q.get(timeout=300) for _ in range(world)], key=lambda x: x[0])
+    for pr in procs:
+        pr.join(timeout=60)
+        assert pr.exitcode == 0
+    f = np.load(os.path.join(GOLDEN, "eval_fullsize_normal.npz"))
+    meta = json.loads(str(f["meta"]))
+    ent, rel = seeded_tables(meta["table_seed"], meta["E"], meta["R"], meta["dim"], meta["dim"], meta["std"])
+    ref = {k[5:]: f[k] for k in f.files if k.startswith("full_")}
+    splits = {k: f["tri_" + k].astype(np.int64) for k in ("train", "valid", "test")}
+    total = sum(len(v) for v in ref.values())
+    for rank, ranks, metrics, refined in res:
+        assert refined == (eval_precision == "bf16x3_refined")
+        assert set(ranks) == set(ref)
+        moved, worst = assert_rank_moves_are_near_ties(ranks, ref, ent, rel, splits["valid"], splits, 1e-5,
+                                                       f"sharded x2 rank {rank} {eval_precision}")
+        print(f"\nsharded x2 rank {rank} ({eval_precision}): {moved} of {total} ranks differ, largest gap {worst:.2e}")
+        assert moved <= 0.005 * total
+    for k in res[0][1]:  # every rank holds the same global ranks
+        np.testing.assert_array_equal(res[0][1][k], res[1][1][k])

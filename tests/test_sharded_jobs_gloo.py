@@ -37,6 +37,18 @@ class JobOps(TorchOps):
     spo = OracleOps.spo
     rank_counts = OracleOps.rank_counts
 
+    def rank_rows(self, s, n_a, c0, part_a, part_b, f_col, t_col, greater, ties, refine=None):
+        """kge_rank_rows on the CPU: the stacked block's counts, laid out [ranking][row]."""
+        n = s.shape[0]
+        for first, rows, (true_idx, true_score, f_ptr, t_ptr) in ((0, s[:n_a], part_a), (n_a, s[n_a:], part_b)):
+            nb = rows.shape[0]
+            g = torch.zeros(3 * nb, dtype=torch.int64)
+            t = torch.zeros(3 * nb, dtype=torch.int64)
+            OracleOps.rank_counts(self, rows, c0, true_idx, true_score, f_ptr, f_col, t_ptr, t_col, g, t)
+            for r in range(1 + (f_ptr is not None) + (t_ptr is not None)):
+                greater[r * n + first:r * n + first + nb] += g[r * nb:(r + 1) * nb]
+                ties[r * n + first:r * n + first + nb] += t[r * nb:(r + 1) * nb]
+
     def rank_hist_multi(self, greater, ties, rows_per_hist, tie_handling, ranks, hists):
         assert tie_handling == "rounded_mean_rank"
         r = greater + ties // 2
@@ -345,3 +357,104 @@ def test_row_sharded_on_is_refused_by_the_training_types_that_do_not_shard(train
         job._replicas_only()
     finally:
         dist.destroy_process_group()
+
+
+def _worker_shard_only(rank, world, port, out_q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from kge import Dataset
+        from kge.job import TrainingJob
+
+        c = _config()
+        ds = Dataset(c, None)
+        ds._triples = {k: torch.from_numpy(v.astype(np.int32)) for k, v in _splits().items()}
+        job = TrainingJob.create(c, ds)
+        ent0, rel0 = _tables()
+        with torch.no_grad():
+            job.model._entity_embedder._embeddings.weight.copy_(ent0)
+            job.model._relation_embedder._embeddings.weight.copy_(rel0)
+        job.sharded_ops = JobOps()
+        seen = []
+
+        def after_epoch(j, trace):  # what the model holds while the job trains
+            emb = j.model._entity_embedder
+            seen.append((tuple(emb._embeddings.weight.shape), emb.shard, j._sharded.scorer.collectives_last_step,
+                         emb._embeddings.weight.detach().numpy().copy()))
+
+        job.post_epoch_hooks.append(after_epoch)
+        job.run()
+        emb = job.model._entity_embedder
+        after_run = (tuple(emb._embeddings.weight.shape), emb.shard)
+        # the unsharded scoring path takes the model again once sync_model has run (job.run ends
+        # with it): here it gets as far as the engine, which refuses CPU tensors ...
+        from kge._lib import EngineError
+
+        try:
+            job.model.score_sp(torch.tensor([1, 2]), torch.tensor([0, 1]))
+            full_ok = False
+        except EngineError:
+            full_ok = True
+        best = job.best_state_full()
+        key = "_entity_embedder._embeddings.weight"
+        best_shard_shape = tuple(job.best_state[key].shape)
+        best_epoch = max(range(len(job.valid_trace)), key=lambda i: job.valid_trace[i][c.get("valid.metric")])
+        # ... and a further batch cuts the model down to this rank's rows again
+        job._sharded.process_batch({"triples": ds.split("train")[:BS].long()})
+        refused = False
+        try:
+            job.model.score_sp(torch.tensor([1]), torch.tensor([0]))
+        except RuntimeError as e:
+            refused = "row-sharded" in str(e)
+        out_q.put((rank, job._sharded.lo, job._sharded.hi, seen, after_run, full_ok,
+                   best[key].numpy().copy(), best_shard_shape, best_epoch, emb.shard, refused))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_sharded_job_holds_only_its_rows_and_best_state_reassembles():
+    """While a row-sharded job trains, the model's entity parameter is [hi - lo, d] (the whole
+    table exists only after sync_model); a step takes 4 collectives; best_state keeps every
+    rank's rows of the best epoch and best_state_full() assembles that epoch's whole table."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_shard_only, args=(r, world, port, q)) for r in range(world)]
+    for pr in procs:
+        pr.start()
+    res = sorted([q.get(timeout=240) for _ in range(world)], key=lambda x: x[0])
+    for pr in procs:
+        pr.join(timeout=60)
+        assert pr.exitcode == 0
+    assert res[0][8] == res[1][8]  # both ranks picked the same best epoch
+    best_epoch = res[0][8]
+    for rank, lo, hi, seen, after_run, full_ok, best_full, best_shard_shape, _, shard_again, refused in res:
+        assert len(seen) == EPOCHS
+        for shape, shard, collectives, _rows in seen:
+            assert shape == (hi - lo, D) and shard == (lo, hi) and collectives == 4
+        assert after_run == ((E, D), None) and full_ok
+        assert best_shard_shape == (hi - lo, D) and best_full.shape == (E, D)
+        assert shard_again == (lo, hi) and refused
+        # the assembled best table is every rank's rows as they were after the best epoch
+        for r2 in res:
+            np.testing.assert_array_equal(best_full[r2[1]:r2[2]], r2[3][best_epoch][3])
+    np.testing.assert_array_equal(res[0][6], res[1][6])
+
+
+def test_exchange_plan_slots():
+    """ExchangePlan: owner-major slots with equal blocks of cap rows per rank."""
+    from kge.sharded import ExchangePlan
+
+    e = np.array([5, 0, 9, 3, 7, 1, 8, 4])  # per = 4: owners 1 0 2 0 1 0 2 1
+    plans = [ExchangePlan(e, 4, 3, r, "cpu") for r in range(3)]
+    assert [p.cap for p in plans] == [3, 3, 3] and [p.count for p in plans] == [3, 3, 2]
+    assert plans[0].mine.tolist() == [1, 3, 5] and plans[1].mine.tolist() == [0, 4, 7] and plans[2].mine.tolist() == [2, 6]
+    assert plans[0].slot.tolist() == [3, 0, 6, 1, 4, 2, 7, 5]
+    # gathering rank-major blocks of cap rows and reading them through slot gives the batch order back
+    blocks = np.full(9, -1)
+    for r, p in enumerate(plans):
+        blocks[r * 3:r * 3 + p.count] = e[p.mine.numpy()]
+    np.testing.assert_array_equal(blocks[plans[0].slot.numpy()], e)
+    empty = ExchangePlan(np.zeros(0, np.int64), 4, 2, 0, "cpu")
+    assert empty.cap == 1 and empty.count == 0 and empty.slot.numel() == 0
