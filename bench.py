@@ -286,6 +286,8 @@ def cpu_baseline(args, E, R, seconds, eval_ctx=None):
     out["train_step_1vsall"] = train
     out["train_step_note"] = ("N(0,1) is the reference's default init (lookup_embedder.yaml); its softmax gradients "
                               "are denormal-laden, which slows the CPU backward GEMMs")
+    out["train_step_kvsall_c3"] = cpu_kvsall_step(threads)
+    out["train_step_ns_c4"] = cpu_ns_step(threads)
     if eval_ctx is not None:  # filtered entity ranking on the same tables / triples as the GPU job
         ent_c, rel_c, splits, bs = eval_ctx
         t0 = time.perf_counter()
@@ -307,6 +309,86 @@ def cpu_baseline(args, E, R, seconds, eval_ctx=None):
                                  f"train + valid + test, batch {bs}: the reference's EntityRankingJob op sequence "
                                  f"(refseq.EntityRankingCPU, rank for rank vs reference-captured fixtures)"}
     return out
+
+
+def cpu_kvsall_step(threads, batch=512, dim=512, runs=5):
+    """BASELINE configs[2] on the host: one TrainingJobKvsAll batch of DistMult-512 on the WN18RR
+    shape (40,943 entities, B = 512, query types sp_ and _po, kl loss, Adagrad) through
+    refseq.train_step_kvsall -- the reference's op sequence incl. its dense [B, E] label matrix.
+    The batch comes from the reference's example layout (all sp_ keys, then all _po keys of the
+    synthetic training split), built with this package's host index (data preparation only)."""
+    from kge import Config, Dataset
+    from kge.dataset import KvsAllIndex
+    from oracle import refseq
+
+    c = Config()
+    c.set("model", "distmult")
+    c._import("distmult")
+    ds = Dataset.synthetic(c, "wn18rr", seed=0)
+    E, R = ds.num_entities(), ds.num_relations()
+    tri = ds.split("train").numpy().astype(np.int64)
+    idx = [KvsAllIndex(tri, (0, 1), 2), KvsAllIndex(tri, (1, 2), 0)]  # sp_ -> o, _po -> s
+    last = np.cumsum([len(ix) for ix in idx])
+    gen = torch.Generator().manual_seed(2)
+    ent = torch.nn.Parameter(torch.randn(E, dim, generator=gen) * 0.1)
+    rel = torch.nn.Parameter(torch.randn(R, dim, generator=gen) * 0.1)
+    opt = torch.optim.Adagrad([ent, rel], lr=0.2)
+    perm = torch.randperm(int(last[-1]), generator=gen).numpy()
+    ts, nnz = [], 0
+    for i in range(runs + 1):  # 1 warm-up + runs timed
+        ex = perm[i * batch:(i + 1) * batch]
+        qt = np.searchsorted(last, ex, side="right")
+        queries = np.zeros((batch, 2), np.int64)
+        coords = []
+        for b, (e, q) in enumerate(zip(ex, qt)):
+            ix = idx[q]
+            loc = int(e - (last[q - 1] if q else 0))
+            queries[b] = ix.keys[loc]
+            vals = ix.values[ix.offsets[loc]:ix.offsets[loc + 1]]
+            coords.append(np.stack([np.full(len(vals), b, np.int64), vals.astype(np.int64)], 1))
+        coords = np.concatenate(coords)
+        nnz = len(coords)
+        t0 = time.perf_counter()
+        refseq.train_step_kvsall(ent, rel, opt, torch.from_numpy(queries), torch.from_numpy(qt),
+                                 torch.from_numpy(coords).int(), 0.0, ("sp_", "_po"))
+        ts.append(time.perf_counter() - t0)
+    m = float(np.median(ts[1:]))
+    return {"ms_per_step": m * 1e3, "scored_triples_per_s": batch * E / m, "runs": runs, "cores": threads,
+            "labels_in_last_batch": int(nnz),
+            "sample": f"median of {runs} KvsAll steps (DistMult-{dim}, WN18RR shape E={E}, B={batch}, N(0,0.1) init, "
+                      f"Adagrad): refseq.train_step_kvsall, pinned to the reference-captured KvsAll trajectory"}
+
+
+def cpu_ns_step(threads, batch=8, dim=1024, negatives=1024, runs=5):
+    """BASELINE configs[3] on the host, bounded: one TrainingJobNegativeSampling batch of
+    RotatE-1024 (FB15K-237 shape, 1,024 negatives for the subject and for the object slot,
+    implementation "triple", kl loss, Adagrad) at B = 8 triples instead of 512 -- the reference
+    scores B x 1,025 gathered triples per slot through norm-over-stack ops, 7 s per 100 triples
+    for score_spo alone -- through refseq.train_step_ns_triple."""
+    from kge.dataset import SHAPES
+    from oracle import refseq
+
+    E, R, _ = SHAPES["fb15k-237"]
+    gen = torch.Generator().manual_seed(3)
+    ent = torch.nn.Parameter(torch.randn(E, dim, generator=gen) * 0.1)
+    rel = torch.nn.Parameter((torch.rand(R, dim // 2, generator=gen) * 2 - 1) * float(np.pi))  # rotate.yaml:20-24
+    opt = torch.optim.Adagrad([ent, rel], lr=0.1)
+    ts = []
+    for i in range(runs + 1):
+        tr = torch.stack([torch.randint(0, E, (batch,), generator=gen), torch.randint(0, R, (batch,), generator=gen),
+                          torch.randint(0, E, (batch,), generator=gen)], 1)
+        neg = {0: torch.randint(0, E, (batch, negatives), generator=gen),
+               2: torch.randint(0, E, (batch, negatives), generator=gen)}
+        t0 = time.perf_counter()
+        refseq.train_step_ns_triple(ent, rel, opt, tr, neg, 1.0)
+        ts.append(time.perf_counter() - t0)
+    m = float(np.median(ts[1:]))
+    scored = 2 * batch * (1 + negatives)
+    return {"ms_per_step": m * 1e3, "scored_triples_per_s": scored / m, "batch": batch, "runs": runs,
+            "cores": threads, "extrapolated_ms_per_step_b512": m * 1e3 * 512 / batch,
+            "sample": f"median of {runs} negative-sampling steps (RotatE-{dim}, FB15K-237 shape, {negatives} negatives "
+                      f"per slot (s, o), B={batch} of the configuration's 512, Adagrad): refseq.train_step_ns_triple, "
+                      f"pinned to the reference-captured negative-sampling trajectory"}
 
 
 # --------------------------------------------------------------------------------- main

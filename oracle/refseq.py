@@ -1,5 +1,6 @@
-"""Reference-op-sequence CPU replica of ComplEx score_sp / score_po.  TEST / BASELINE
-INFRASTRUCTURE ONLY (bench.py's ``cpu_baseline`` leg and tests/).
+"""Reference-op-sequence CPU replicas: ComplEx score_sp / score_po, the 1vsAll training step,
+entity ranking, the DistMult KvsAll training step and the RotatE negative-sampling step.
+TEST / BASELINE INFRASTRUCTURE ONLY (bench.py's ``cpu_baseline`` leg and tests/).
 
 Replays the exact ATen op sequence the reference issues on the CPU for
 KgeModel.score_sp -> ComplExScorer.score_emb(..., "sp_") (kge_model.py:652-659,
@@ -69,6 +70,112 @@ def train_step_1vsall(ent: torch.nn.Parameter, rel: torch.nn.Parameter, optimize
     loss_po.backward()
     optimizer.step()
     return loss
+
+
+def distmult_score_sp(ent, rel, s, p):
+    """KgeModel.score_sp -> DistMultScorer.score_emb(..., "sp_") (kge_model.py:652-659,
+    lookup_embedder.py:91-107, distmult.py:19-20)."""
+    s_emb, p_emb = _gather(ent, s), _gather(rel, p)
+    o_emb = _gather(ent, torch.arange(ent.shape[0]))
+    return (s_emb * p_emb).mm(o_emb.transpose(0, 1))
+
+
+def distmult_score_po(ent, rel, p, o):
+    """KgeModel.score_po -> DistMultScorer.score_emb(..., "_po") (kge_model.py:675-682,
+    distmult.py:21-22)."""
+    s_emb = _gather(ent, torch.arange(ent.shape[0]))
+    o_emb, p_emb = _gather(ent, o), _gather(rel, p)
+    return (o_emb * p_emb).mm(s_emb.transpose(0, 1))
+
+
+def train_step_kvsall(ent: torch.nn.Parameter, rel: torch.nn.Parameter, optimizer, queries: torch.Tensor,
+                      query_type_indexes: torch.Tensor, label_coords: torch.Tensor, label_smoothing: float = 0.0,
+                      query_types=("sp_", "_po")) -> float:
+    """One TrainingJobKvsAll batch of a DistMult model as the reference runs it on the CPU
+    (train.py:314-375, 679-756, job/util.py:41-57, loss.py:209-213): zero_grad; the label
+    coordinates densified into a [B, max(E, R)] matrix through a sparse tensor; per query type
+    the examples' label rows (smoothed as (1 - ls) * L + 1 / E), score_sp / score_po on the
+    examples' queries, KLDivLoss(sum)(log_softmax(scores), normalize(labels, p=1)) / B,
+    .item(), backward; optimizer.step().  Returns what the reference reports as the batch
+    loss: the LAST query type's (train.py:747 overwrites instead of summing).  The batch
+    itself (queries, query_type_indexes, label_coords) is what the reference's collate
+    (train.py:590-677) hands over; (s, ?, o) queries are not replayed here."""
+    kl = torch.nn.KLDivLoss(reduction="sum")
+    E, R = ent.shape[0], rel.shape[0]
+    n = len(queries)
+    optimizer.zero_grad()
+    examples_for = {qt: (query_type_indexes == qi).nonzero().view(-1) for qi, qt in enumerate(query_types)}
+    labels_batch = torch.sparse_coo_tensor(label_coords.long().t(), torch.ones([len(label_coords)], dtype=torch.float)
+                                           * 1.0, torch.Size([n, max(E, R)])).to_dense()
+    labels_for = {qt: labels_batch[ex, :E] for qt, ex in examples_for.items()}
+    if label_smoothing > 0.0:
+        for qt, labels in labels_for.items():
+            labels_for[qt] = (1.0 - label_smoothing) * labels + 1.0 / labels.size(1)
+    loss_value_total = 0.0
+    for qt, ex in examples_for.items():
+        if len(ex) > 0:
+            if qt == "sp_":
+                scores = distmult_score_sp(ent, rel, queries[ex, 0], queries[ex, 1])
+            elif qt == "_po":
+                scores = distmult_score_po(ent, rel, queries[ex, 0], queries[ex, 1])
+            else:
+                raise NotImplementedError(qt)
+            loss_value = kl(torch.nn.functional.log_softmax(scores, dim=1),
+                            torch.nn.functional.normalize(labels_for[qt].float(), p=1, dim=1)) / n
+            loss_value_total = loss_value.item()
+            loss_value.backward()
+    optimizer.step()
+    return loss_value_total
+
+
+def rotate_score_spo(ent, rel, s, p, o, l_norm: float = 1.0):
+    """KgeModel.score_spo -> RotatEScorer.score_emb(..., "spo") (kge_model.py:620-637,
+    rotate.py:18-40, 113-145): chunk, cos / sin of the phases, complex Hadamard product,
+    difference, |.| as the norm over a stacked (re, im) tensor, then the l_norm norm over the
+    components.  A positive distance (the reference does not negate it)."""
+    s_emb, p_emb, o_emb = _gather(ent, s), _gather(rel, p), _gather(ent, o)
+    s_re, s_im = torch.chunk(s_emb, 2, dim=1)
+    o_re, o_im = torch.chunk(o_emb, 2, dim=1)
+    p_re, p_im = torch.cos(p_emb), torch.sin(p_emb)
+    sp_re = s_re * p_re - s_im * p_im
+    sp_im = s_re * p_im + s_im * p_re
+    diff_re, diff_im = sp_re - o_re, sp_im - o_im
+    diff_abs = torch.norm(torch.stack((diff_re, diff_im), dim=0), dim=0)
+    return torch.norm(diff_abs, dim=1, p=l_norm).view(len(p), -1)
+
+
+def train_step_ns_triple(ent: torch.nn.Parameter, rel: torch.nn.Parameter, optimizer, triples: torch.Tensor,
+                         negatives, l_norm: float = 1.0) -> float:
+    """One TrainingJobNegativeSampling batch of a RotatE model with implementation "triple" and
+    train.loss kl, as the reference runs it on the CPU (train.py:314-375, 823-893, 982-999,
+    loss.py:192-213): zero_grad; per corrupted slot with samples (negatives = {slot: [B, N]},
+    slots 0 = S and 2 = O) the triples repeated 1 + N times with the slot overwritten by
+    (positive, negatives), score_spo on all B (1 + N) triples, a [B, 1 + N] label matrix with a
+    one in column 0, KLDivLoss(sum)(log_softmax(scores), normalize(labels, p=1)) / B, .item(),
+    backward; optimizer.step().  Returns the batch loss (summed over the slots)."""
+    kl = torch.nn.KLDivLoss(reduction="sum")
+    n = len(triples)
+    optimizer.zero_grad()
+    loss_value = 0.0
+    labels = None
+    for slot in (0, 1, 2):
+        neg = negatives.get(slot)
+        if neg is None or neg.shape[1] <= 0:
+            continue
+        num_samples = neg.shape[1]
+        if labels is None or labels.shape != torch.Size([n, 1 + num_samples]):
+            labels = torch.zeros((n, 1 + num_samples))
+            labels[:, 0] = 1
+        triples_to_score = triples.repeat(1, 1 + num_samples).view(-1, 3)
+        triples_to_score[:, slot] = torch.cat((triples[:, [slot]], neg), 1).view(-1)
+        scores = rotate_score_spo(ent, rel, triples_to_score[:, 0], triples_to_score[:, 1], triples_to_score[:, 2],
+                                  l_norm).view(n, -1)
+        loss_value_torch = kl(torch.nn.functional.log_softmax(scores, dim=1),
+                              torch.nn.functional.normalize(labels.float(), p=1, dim=1)) / n
+        loss_value += loss_value_torch.item()
+        loss_value_torch.backward()
+    optimizer.step()
+    return loss_value
 
 
 class EntityRankingCPU:

@@ -154,3 +154,56 @@ def test_refseq_train_step_reproduces_reference_trajectory():
     np.testing.assert_allclose(losses, f["losses"], rtol=1e-6)
     np.testing.assert_allclose(ent.detach().numpy(), f["ent1"], atol=1e-6)
     np.testing.assert_allclose(rel.detach().numpy(), f["rel1"], atol=1e-6)
+
+
+def test_refseq_kvsall_step_reproduces_reference_trajectory():
+    """The CPU KvsAll step replica (refseq.train_step_kvsall, bench.py's cpu_baseline C3 leg)
+    against the reference-captured three-batch DistMult KvsAll trajectory: teacher-forced from
+    each batch's captured tables the gradients, free-running the losses and final tables."""
+    import torch
+    from oracle import refseq
+
+    f = np.load(os.path.join(GOLDEN, "train_kvsall_distmult.npz"))
+    meta = json.loads(str(f["meta"]))
+    torch.set_num_threads(4)
+    ent = torch.nn.Parameter(torch.from_numpy(f["ent0"]).clone())
+    rel = torch.nn.Parameter(torch.from_numpy(f["rel0"]).clone())
+    opt = torch.optim.Adagrad([ent, rel], lr=meta["lr"])
+    losses = []
+    for b in range(meta["num_batches"]):
+        np.testing.assert_allclose(ent.detach().numpy(), f[f"ent_before_{b}"], atol=1e-6)
+        losses.append(refseq.train_step_kvsall(
+            ent, rel, opt, torch.from_numpy(f[f"queries_{b}"]), torch.from_numpy(f[f"qtype_{b}"]),
+            torch.from_numpy(f[f"label_coords_{b}"]), meta["label_smoothing"], tuple(meta["query_types"])))
+        np.testing.assert_allclose(ent.grad.numpy(), f[f"g_ent_{b}"], atol=1e-6 * np.abs(f[f"g_ent_{b}"]).max())
+        np.testing.assert_allclose(rel.grad.numpy(), f[f"g_rel_{b}"], atol=1e-6 * np.abs(f[f"g_rel_{b}"]).max())
+    np.testing.assert_allclose(losses, f["losses"], rtol=1e-6)
+    np.testing.assert_allclose(ent.detach().numpy(), f["ent1"], atol=1e-6)
+    np.testing.assert_allclose(rel.detach().numpy(), f["rel1"], atol=1e-6)
+
+
+def test_refseq_ns_step_reproduces_reference_trajectory():
+    """The CPU negative-sampling step replica (refseq.train_step_ns_triple, bench.py's
+    cpu_baseline C4 leg) against the reference-captured RotatE steps with the reference's
+    sampled negatives injected ("triple" implementation, kl loss)."""
+    import torch
+    from oracle import refseq
+
+    f = np.load(os.path.join(GOLDEN, "train_ns_rotate.npz"))
+    meta = json.loads(str(f["meta"]))
+    assert meta["implementation"] == "triple" and meta["loss"] == "kl"
+    torch.set_num_threads(4)
+    ent = torch.nn.Parameter(torch.from_numpy(f["ent0"]).clone())
+    rel = torch.nn.Parameter(torch.from_numpy(f["rel0"]).clone())
+    opt = torch.optim.Adagrad([ent, rel], lr=meta["lr"])
+    losses = []
+    for b in range(meta["num_batches"]):
+        np.testing.assert_allclose(ent.detach().numpy(), f[f"ent_before_{b}"], atol=1e-6)
+        neg = {0: torch.from_numpy(f[f"neg_s_{b}"]).long(), 2: torch.from_numpy(f[f"neg_o_{b}"]).long()}
+        losses.append(refseq.train_step_ns_triple(ent, rel, opt, torch.from_numpy(f[f"triples_{b}"]).long(), neg,
+                                                  meta["l_norm"]))
+        np.testing.assert_allclose(ent.grad.numpy(), f[f"g_ent_{b}"], atol=1e-6 * np.abs(f[f"g_ent_{b}"]).max())
+        np.testing.assert_allclose(rel.grad.numpy(), f[f"g_rel_{b}"], atol=1e-6 * np.abs(f[f"g_rel_{b}"]).max())
+    np.testing.assert_allclose(losses, f["losses"], rtol=1e-6)
+    np.testing.assert_allclose(ent.detach().numpy(), f["ent1"], atol=1e-6)
+    np.testing.assert_allclose(rel.detach().numpy(), f["rel1"], atol=1e-6)
