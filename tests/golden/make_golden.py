@@ -50,6 +50,14 @@ Fixtures written:
   relations cover all four cardinality classes: every metric of the epoch trace, and the
   reference's relation_types / frequency_percentiles indexes.
 
+* ``scorer_{rescal128,distmult512,transe_l1_512,rotate_l1_512}_<regime>.npz`` -- F1 / F2 at larger
+  shapes (RESCAL d = 128; d = 512 over 640 entities: three 256-wide entity panels): tables from a
+  recorded numpy seed, the reference's outputs and gradients stored;
+* ``eval_rescal128_normal.npz`` -- the reference EntityRankingJob with RESCAL at d = 128;
+* ``train1vsall_complex_large.npz`` -- three 1vsAll batches over 1,600 entities at d = 128, B = 300;
+* ``train_toy_complex_epochs.npz`` -- written with the toy fixture: after every epoch of that run the
+  tables and the validation ranks computed from them (teacher-forced validation checks).
+
 Run:  PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden.py [case,case,...]
 """
 import collections
@@ -226,6 +234,149 @@ def gen_scorer_fixture(name, model_key, dim, extra, regime, seed):
     )
     fn = os.path.join(OUT, f"scorer_{name}_{regime}.npz")
     np.savez_compressed(fn, **arrays)
+    return fn
+
+
+# Larger shapes: tables regenerated by the tests from a recorded numpy seed (only the reference's
+# OUTPUTS are stored).  d = 512 with E = 640 crosses the 256-wide tiles of the production kernels
+# (three entity panels, a ragged last one); RESCAL at d = 128 has 16,384-wide relation rows.
+LARGE_SCORER_CASES = [
+    # name, model key, entity dim, extra config, E, R, n, m
+    ("rescal128", "rescal", 128, {}, 200, 4, 16, 40),
+    ("distmult512", "distmult", 512, {}, 640, 8, 24, 300),
+    ("transe_l1_512", "transe", 512, {"transe.l_norm": 1.0}, 640, 8, 24, 300),
+    ("rotate_l1_512", "rotate", 512, {"rotate.l_norm": 1.0}, 640, 8, 24, 300),
+]
+
+
+def seeded_scorer_tables(seed, regime, model_key, E, R, d_e, d_r):
+    """Tables of a large scorer fixture from numpy's PCG64 stream: N(0, 0.1), or dyadic k / 8 with
+    |k| <= 16; RotatE relations are phases U(-pi, pi) in both regimes."""
+    rng = np.random.default_rng(seed)
+    if regime == "normal":
+        ent = (rng.standard_normal((E, d_e), dtype=np.float32) * np.float32(0.1)).astype(np.float32)
+        rel = (rng.standard_normal((R, d_r), dtype=np.float32) * np.float32(0.1)).astype(np.float32)
+    else:
+        ent = (rng.integers(-16, 17, (E, d_e)) / 8.0).astype(np.float32)
+        rel = (rng.integers(-16, 17, (R, d_r)) / 8.0).astype(np.float32)
+    if model_key == "rotate":
+        rel = ((rng.random((R, d_r)) * 2 - 1) * math.pi).astype(np.float32)
+    return ent, rel
+
+
+def gen_scorer_large(name, model_key, dim, extra, E, R, n, m, regime, seed):
+    config = make_config(model_key, dim, E, R, extra)
+    ds = Dataset(config, None)
+    model = KgeModel.create(config, ds)
+    d_e = model._entity_embedder.dim
+    d_r = model._relation_embedder.dim
+    ent, rel = seeded_scorer_tables(seed, regime, model_key, E, R, d_e, d_r)
+    set_tables(model, torch.from_numpy(ent), torch.from_numpy(rel))
+    gen = torch.Generator().manual_seed(seed)
+    s = torch.randint(0, E, (n,), generator=gen)
+    p = torch.randint(0, R, (n,), generator=gen)
+    o = torch.randint(0, E, (n,), generator=gen)
+    subset = torch.randperm(E, generator=gen)[:m]
+    # dyadic weights keep the dyadic regime's gradients exact sums
+    w_sp = dyadic(gen, (n, E)) if regime == "dyadic" else torch.randn(n, E, generator=gen)
+    w_po = dyadic(gen, (n, E)) if regime == "dyadic" else torch.randn(n, E, generator=gen)
+    w_spo = dyadic(gen, (n,)) if regime == "dyadic" else torch.randn(n, generator=gen)
+    model.train()
+    spo = model.score_spo(s, p, o)
+    sp_all = model.score_sp(s, p)
+    po_all = model.score_po(p, o)
+    loss = (w_sp * sp_all).sum() + (w_po * po_all).sum() + (w_spo * spo).sum()
+    model.zero_grad()
+    loss.backward()
+    g_ent = model._entity_embedder._embeddings.weight.grad.clone()
+    g_rel = model._relation_embedder._embeddings.weight.grad.clone()
+    with torch.no_grad():
+        sp_sub = model.score_sp(s, p, subset)
+        po_sub = model.score_po(p, o, subset)
+        sppo_sub = model.score_sp_po(s, p, o, subset)
+    arrays = dict(
+        s=s.numpy(), p=p.numpy(), o=o.numpy(), subset=subset.numpy(),
+        spo=spo.detach().numpy(), sp_all=sp_all.detach().numpy(), po_all=po_all.detach().numpy(),
+        sp_sub=sp_sub.numpy(), po_sub=po_sub.numpy(), sppo_sub=sppo_sub.numpy(),
+        w_sp=w_sp.numpy(), w_po=w_po.numpy(), w_spo=w_spo.numpy(), g_ent=g_ent.numpy(), g_rel=g_rel.numpy(),
+        meta=np.array(json.dumps(dict(
+            model=model_key, name=name, regime=regime, seed=seed, table_seed=seed, E=E, R=R, d_e=d_e, d_r=d_r,
+            l_norm=extra.get("transe.l_norm", extra.get("rotate.l_norm")),
+            ent_checksum=table_checksum(ent), rel_checksum=table_checksum(rel),
+            torch=torch.__version__, numpy=np.__version__))))
+    fn = os.path.join(OUT, f"scorer_{name}_{regime}.npz")
+    np.savez_compressed(fn, **arrays)
+    return fn
+
+
+def gen_eval_rescal128():
+    """The reference's EntityRankingJob with RESCAL at d = 128 (relation rows of 16,384 floats)."""
+    E, R, splits = make_dataset_splits(seed=21, E=200, R=4, n_train=1500, n_valid=100, n_test=100)
+    folder = os.path.join(TMP, "ds_eval_rescal128")
+    write_dataset(folder, E, R, splits)
+    dim, seed = 128, 4100
+    ent, rel = seeded_scorer_tables(seed, "normal", "rescal", E, R, dim, dim * dim)
+    config = ds_config("rescal", dim, folder, E, R)
+    ranks, metrics = run_eval(config, folder, torch.from_numpy(ent), torch.from_numpy(rel), -1, batch_size=32)
+    out = {f"tri_{k}": v.astype(np.int32) for k, v in splits.items()}
+    out.update({f"full_{k}": v for k, v in ranks.items()})
+    out["metrics"] = np.array(json.dumps({"full": metrics}))
+    out["meta"] = np.array(json.dumps(dict(
+        E=E, R=R, dim=dim, model="rescal", eval_split="valid", filter_splits=["train", "valid"],
+        filter_with_test=True, batch_size=32, tie_handling="rounded_mean_rank", table_seed=seed,
+        ent_checksum=table_checksum(ent), rel_checksum=table_checksum(rel), torch=torch.__version__,
+        numpy=np.__version__)))
+    fn = os.path.join(OUT, "eval_rescal128_normal.npz")
+    np.savez_compressed(fn, **out)
+    return fn
+
+
+def gen_train_fixture_large():
+    """Three 1vsAll batches (ComplEx-128, Adagrad, kl) over 1,600 entities with batches of 300
+    triples: the production kernels' tiles are multi-panel in every dimension (7 entity panels,
+    two query tiles).  Tables from a recorded numpy seed; per-batch losses, the first batch's
+    gradients and the final tables are stored."""
+    from kge.job import TrainingJob
+
+    E, R, dim, bs, nb = 1600, 12, 128, 300, 3
+    rng = np.random.default_rng(31)
+    allt = synth_triples_fast(rng, E, R, 6000)
+    splits = dict(train=allt[:5000], valid=allt[5000:5500], test=allt[5500:])
+    folder = os.path.join(TMP, "ds_train_large")
+    write_dataset(folder, E, R, splits)
+    config = ds_config("complex", dim, folder, E, R, {
+        "train.type": "1vsAll", "train.optimizer": "Adagrad", "train.optimizer_args": {"lr": 0.2},
+        "train.loss": "kl", "train.batch_size": bs})
+    ds = Dataset.create(config, folder=folder)
+    seed = 4200
+    ent, rel = seeded_scorer_tables(seed, "normal", "complex", E, R, dim, dim)
+    job = TrainingJob.create(config, ds)
+    set_tables(job.model, torch.from_numpy(ent), torch.from_numpy(rel))
+    job._prepare()
+    gen = torch.Generator().manual_seed(32)
+    perm = torch.randperm(len(splits["train"]), generator=gen)[:nb * bs]
+    train = torch.from_numpy(splits["train"])
+    losses, batches, g0 = [], [], None
+    for b in range(nb):
+        batch = train[perm[b * bs:(b + 1) * bs]].long()
+        batches.append(batch.numpy())
+        job.optimizer.zero_grad()
+        res = job._process_batch(b, {"triples": batch})
+        if b == 0:
+            g0 = (job.model._entity_embedder._embeddings.weight.grad.clone().numpy(),
+                  job.model._relation_embedder._embeddings.weight.grad.clone().numpy())
+        job.optimizer.step()
+        losses.append(res.avg_loss)
+    fn = os.path.join(OUT, "train1vsall_complex_large.npz")
+    np.savez_compressed(
+        fn, batches=np.stack(batches).astype(np.int32), losses=np.array(losses, dtype=np.float64),
+        g_ent_0=g0[0], g_rel_0=g0[1],
+        ent1=job.model._entity_embedder._embeddings.weight.detach().numpy(),
+        rel1=job.model._relation_embedder._embeddings.weight.detach().numpy(),
+        meta=np.array(json.dumps(dict(E=E, R=R, dim=dim, lr=0.2, optimizer="Adagrad", loss="kl", batch_size=bs,
+                                      table_seed=seed, ent_checksum=table_checksum(ent),
+                                      rel_checksum=table_checksum(rel), torch=torch.__version__,
+                                      numpy=np.__version__))))
     return fn
 
 
@@ -598,7 +749,35 @@ def gen_toy_fixture():
     epoch_traces, valid_traces = [], []
     job.post_epoch_hooks.append(lambda j, t: epoch_traces.append(dict(t)))
     job.post_valid_hooks.append(lambda j, t: valid_traces.append(dict(t)))
+    # per epoch: the tables the validation ranks were computed from, and those ranks
+    epoch_tables, epoch_ranks = [], []
+
+    def keep_tables(j, t):
+        epoch_tables.append((j.model._entity_embedder._embeddings.weight.detach().clone().numpy(),
+                             j.model._relation_embedder._embeddings.weight.detach().clone().numpy()))
+
+    job.post_epoch_hooks.append(keep_tables)
+    from kge.job.eval import hist_all
+
+    def keep_ranks(hists, s, p, o, s_ranks, o_ranks, job, **kwargs):
+        epoch_ranks.append((s_ranks.clone().numpy(), o_ranks.clone().numpy()))
+        return hist_all(hists, s, p, o, s_ranks, o_ranks, job, **kwargs)
+
+    job.valid_job.hist_hooks = [keep_ranks]
     job.run()
+    # the hook runs per validation batch for every ranking in turn (raw, filt, filt_test)
+    nrk = 3 if job.valid_job.filter_with_test else 2
+    per_epoch = len(epoch_ranks) // epochs
+    assert per_epoch * epochs == len(epoch_ranks) and per_epoch % nrk == 0
+    extra = {}
+    for e in range(epochs):
+        chunk = epoch_ranks[e * per_epoch:(e + 1) * per_epoch]
+        for ri, rname in enumerate(("raw", "filt", "filt_test")[:nrk]):
+            extra[f"s_{rname}_{e}"] = np.concatenate([c[0] for c in chunk[ri::nrk]])
+            extra[f"o_{rname}_{e}"] = np.concatenate([c[1] for c in chunk[ri::nrk]])
+        extra[f"ent_{e}"], extra[f"rel_{e}"] = epoch_tables[e]
+    np.savez_compressed(os.path.join(OUT, "train_toy_complex_epochs.npz"), **extra,
+                        meta=np.array(json.dumps(dict(epochs=epochs, rankings=nrk, torch=torch.__version__))))
     keep_e = ("epoch", "avg_loss", "avg_penalty", "avg_cost", "lr", "batches", "size")
     ep = [{k: t[k] for k in keep_e} for t in epoch_traces]
     va = [{k: v for k, v in t.items() if isinstance(v, (int, float)) and ("rank" in k or "hits" in k or k == "epoch")}
@@ -815,7 +994,16 @@ def main():
              "kvsall_so": lambda: gen_kvsall_fixture(with_so=True),
              "ns_rotate": lambda: gen_ns_fixture("rotate"), "ns_complex": lambda: gen_ns_fixture("complex"),
              "toy": gen_toy_fixture, "score_so": gen_score_so_fixture, "eval_metrics_per": gen_eval_metrics_per,
-             "penalties": gen_penalty_fixture}
+             "penalties": gen_penalty_fixture, "eval_rescal128": gen_eval_rescal128,
+             "train_large": gen_train_fixture_large}
+    seed = 3000
+    for name, key, dim, cfg, E, R, n, m in LARGE_SCORER_CASES:
+        for regime in ("normal", "dyadic"):
+            seed += 1
+            if key == "rotate" and regime == "dyadic":
+                continue  # cos / sin of the phases leave nothing exact: the normal regime says it all
+            if only is None or name in only:
+                written.append(gen_scorer_large(name, key, dim, cfg, E, R, n, m, regime, seed))
     for name, fn in extra.items():
         if only is None or name in only:
             written.append(fn())

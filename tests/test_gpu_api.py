@@ -9,7 +9,7 @@ import numpy as np
 import pytest
 import torch
 
-from conftest import GOLDEN
+from conftest import GOLDEN, load_scorer_fixture
 from oracle import kge_oracle as K
 
 pytestmark = pytest.mark.gpu
@@ -76,7 +76,7 @@ def check(meta, name, got, ref, prec):
 @pytest.mark.parametrize("prec", ["bf16x3", "fp32"])
 @pytest.mark.parametrize("fn", SCORER_FILES, ids=lambda f: os.path.basename(f)[7:-4])
 def test_model_scores_and_grads(fn, prec, path):
-    f = np.load(fn)
+    f = load_scorer_fixture(fn)
     m, meta = model_from_fixture(f, prec)
     dev = "cuda"
     s, p, o, sub = (torch.from_numpy(f[k]).to(dev) for k in ("s", "p", "o", "subset"))
@@ -99,7 +99,8 @@ def test_model_scores_and_grads(fn, prec, path):
         outs = dict(spo=spo, sp_all=sp_all, po_all=po_all, sp_sub=m.score_sp(s, p, sub), po_sub=m.score_po(p, o, sub),
                     sppo_sub=m.score_sp_po(s, p, o, sub), sppo_all=m.score_sp_po(s, p, o))
     for k, v in outs.items():
-        check(meta, k, v.detach().cpu().numpy(), f[k], prec)
+        if k in f:  # the larger fixtures leave the [n, 2 E] score_sp_po block out
+            check(meta, k, v.detach().cpu().numpy(), f[k], prec)
     ge = m._entity_embedder._embeddings.weight.grad.cpu().numpy()
     gr = m._relation_embedder._embeddings.weight.grad.cpu().numpy()
     tol = 1e-4 if (prec == "bf16x3" and meta["model"] in K.BILINEAR) else 1e-5
@@ -112,7 +113,7 @@ def test_model_scores_and_grads(fn, prec, path):
 def test_fused_xent_matches_unfused(fn, prec):
     """KgeModel.score_sp_xent / score_po_xent (scores -> CE -> gradient in the engine) give
     the loss and gradients of score_sp / score_po + torch CrossEntropyLoss(sum) / B."""
-    f = np.load(fn)
+    f = load_scorer_fixture(fn)
     if json.loads(str(f["meta"]))["regime"] != "normal":
         pytest.skip("one regime is enough")
     s, p, o = (torch.from_numpy(f[k]).cuda() for k in ("s", "p", "o"))
@@ -352,7 +353,7 @@ def test_reciprocal_relations_model():
 def test_fused_xent2_matches_separate(fn, prec):
     """KgeModel.score_sp_po_xent (both directions stacked into one contraction, one loss
     launch, one backward that writes dE) == score_sp_xent + score_po_xent."""
-    f = np.load(fn)
+    f = load_scorer_fixture(fn)
     if json.loads(str(f["meta"]))["regime"] != "normal":
         pytest.skip("one regime is enough")
     s, p, o = (torch.from_numpy(f[k]).cuda() for k in ("s", "p", "o"))

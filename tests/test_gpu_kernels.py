@@ -16,7 +16,7 @@ import numpy as np
 import pytest
 import torch
 
-from conftest import GOLDEN
+from conftest import GOLDEN, load_scorer_fixture
 from oracle import kge_oracle as K
 
 pytestmark = pytest.mark.gpu
@@ -93,7 +93,7 @@ def forward_all(L, meta, f, prec):
 @pytest.mark.parametrize("prec", ["bf16x3", "fp32"])
 @pytest.mark.parametrize("fn", SCORER_FILES, ids=lambda f: os.path.basename(f)[7:-4])
 def test_forward_vs_golden(L, fn, prec):
-    f = np.load(fn)
+    f = load_scorer_fixture(fn)
     meta = json.loads(str(f["meta"]))
     out = forward_all(L, meta, f, L.PRECISIONS[prec])
     model = meta["model"]
@@ -111,7 +111,7 @@ def test_forward_vs_golden(L, fn, prec):
 @pytest.mark.parametrize("prec", ["bf16x3", "fp32"])
 @pytest.mark.parametrize("fn", SCORER_FILES, ids=lambda f: os.path.basename(f)[7:-4])
 def test_gradients_vs_golden(L, fn, prec):
-    f = np.load(fn)
+    f = load_scorer_fixture(fn)
     meta = json.loads(str(f["meta"]))
     model = meta["model"]
     mk = MODEL_IDS[model]

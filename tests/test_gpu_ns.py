@@ -15,7 +15,7 @@ import numpy as np
 import pytest
 import torch
 
-from conftest import GOLDEN
+from conftest import GOLDEN, load_scorer_fixture
 from oracle import kge_oracle as K
 
 pytestmark = pytest.mark.gpu
@@ -38,7 +38,7 @@ def L():
 def test_score_cand_vs_oracle(L, fn, slot):
     from kge import engine
 
-    f = np.load(fn)
+    f = load_scorer_fixture(fn)
     meta = json.loads(str(f["meta"]))
     model, ln = meta["model"], meta["l_norm"] or 1.0
     ent64, rel64 = f["ent"].astype(np.float64), f["rel"].astype(np.float64)

@@ -12,7 +12,7 @@ import os
 import numpy as np
 import pytest
 
-from conftest import GOLDEN
+from conftest import GOLDEN, load_scorer_fixture
 from oracle import kge_oracle as K
 
 SCORER_FILES = sorted(glob.glob(os.path.join(GOLDEN, "scorer_*.npz")))
@@ -25,29 +25,34 @@ def _rel_err(x, ref):
 
 @pytest.mark.parametrize("fn", SCORER_FILES, ids=lambda f: os.path.basename(f)[7:-4])
 def test_scorer_outputs(fn):
-    f = np.load(fn)
+    f = load_scorer_fixture(fn)
     meta = json.loads(str(f["meta"]))
     out = K.model_scores(meta["model"], f["ent"], f["rel"], f["s"], f["p"], f["o"],
                          f["subset"], meta["l_norm"] or 1.0)
     exact = meta["regime"] == "dyadic" and meta["model"] in K.BILINEAR
     for k, v in out.items():
+        if k not in f:  # the larger fixtures leave the [n, 2 E] score_sp_po block out
+            continue
         ref = f[k]
         assert v.shape == ref.shape, k
         if exact:
             np.testing.assert_array_equal(v.astype(np.float32), ref, err_msg=k)
         else:
-            assert _rel_err(v, ref) < 1e-6, k
+            # the oracle is float64, the reference sums d fp32 terms: its own rounding grows with d
+            # (measured 1.3e-6 of the row maximum for the d = 512 L1 distances)
+            assert _rel_err(v, ref) < (1e-6 if meta["d_e"] <= 128 else 4e-6), k
 
 
 @pytest.mark.parametrize("fn", SCORER_FILES, ids=lambda f: os.path.basename(f)[7:-4])
 def test_scorer_gradients(fn):
-    f = np.load(fn)
+    f = load_scorer_fixture(fn)
     meta = json.loads(str(f["meta"]))
     ge, gr = K.model_grads(meta["model"], f["ent"], f["rel"], f["s"], f["p"], f["o"],
                            f["w_sp"].astype(np.float64), f["w_po"].astype(np.float64),
                            f["w_spo"].astype(np.float64), meta["l_norm"] or 1.0)
-    assert np.abs(ge - f["g_ent"]).max() <= 1e-6 * np.abs(f["g_ent"]).max()
-    assert np.abs(gr - f["g_rel"]).max() <= 1e-6 * np.abs(f["g_rel"]).max()
+    tol = 1e-6 if meta["d_e"] <= 128 else 4e-6
+    assert np.abs(ge - f["g_ent"]).max() <= tol * np.abs(f["g_ent"]).max()
+    assert np.abs(gr - f["g_rel"]).max() <= tol * np.abs(f["g_rel"]).max()
 
 
 @pytest.mark.parametrize("regime", ["dyadic", "normal"])
@@ -207,3 +212,43 @@ def test_refseq_ns_step_reproduces_reference_trajectory():
     np.testing.assert_allclose(losses, f["losses"], rtol=1e-6)
     np.testing.assert_allclose(ent.detach().numpy(), f["ent1"], atol=1e-6)
     np.testing.assert_allclose(rel.detach().numpy(), f["rel1"], atol=1e-6)
+
+
+def test_entity_ranking_rescal128():
+    """The oracle's entity ranking with RESCAL at d = 128 (16,384-wide relation rows) against the
+    reference's EntityRankingJob."""
+    from conftest import seeded_scorer_tables, table_checksum
+
+    f = np.load(os.path.join(GOLDEN, "eval_rescal128_normal.npz"))
+    meta = json.loads(str(f["meta"]))
+    ent, rel = seeded_scorer_tables(meta["table_seed"], "normal", "rescal", meta["E"], meta["R"], meta["dim"],
+                                    meta["dim"] ** 2)
+    assert table_checksum(ent) == meta["ent_checksum"] and table_checksum(rel) == meta["rel_checksum"]
+    splits = {k: f["tri_" + k].astype(np.int64) for k in ("train", "valid", "test")}
+    ranks, metrics = K.entity_ranking("rescal", ent.astype(np.float64), rel.astype(np.float64), splits,
+                                      batch_size=meta["batch_size"])
+    ref_metrics = json.loads(str(f["metrics"]))["full"]
+    same = sum(int((ranks[k] == f["full_" + k]).sum()) for k in ranks)
+    total = sum(len(v) for v in ranks.values())
+    # float64 scores against the reference's fp32 scores: a rank may move only at a near-tie
+    assert same >= total - 2, (same, total)
+    for k, v in ref_metrics.items():
+        assert metrics[k] == pytest.approx(v, rel=2e-3, abs=1e-9), k
+
+
+def test_train_1vsall_large():
+    """The oracle's 1vsAll trajectory over 1,600 entities at d = 128 with batches of 300."""
+    from conftest import seeded_scorer_tables, table_checksum
+
+    f = np.load(os.path.join(GOLDEN, "train1vsall_complex_large.npz"))
+    meta = json.loads(str(f["meta"]))
+    ent, rel = seeded_scorer_tables(meta["table_seed"], "normal", "complex", meta["E"], meta["R"], meta["dim"],
+                                    meta["dim"])
+    assert table_checksum(ent) == meta["ent_checksum"] and table_checksum(rel) == meta["rel_checksum"]
+    losses, e1, r1 = K.train_1vsall("complex", ent, rel, f["batches"].astype(np.int64), lr=meta["lr"])
+    np.testing.assert_allclose(losses, f["losses"], rtol=1e-6)
+    # Adagrad turns rounding-level gradient differences into visible steps where the gradient
+    # nearly cancels: all but a handful of elements agree closely
+    for mine, ref in ((e1, f["ent1"]), (r1, f["rel1"])):
+        diff = np.abs(mine - ref)
+        assert int((diff > 5e-5).sum()) <= max(4, 1e-3 * diff.size) and float(diff.mean()) < 1e-5
