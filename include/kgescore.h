@@ -447,6 +447,44 @@ int kge_rank_rows(const float* s, int64_t lds, int64_t n_a, int64_t n_b, int64_t
                   int64_t rows_per_hist, const float* q, int64_t ldq, const float* t, int64_t ldt,
                   int d, float band_rel, const float* t_norm_max, void* stream);
 
+/* The evaluation contraction with the ranking fused into its epilogue: S = Q . T^T as in
+ * kge_score_dot_split (bf16 hi / lo query planes, fp32 table rows t [m, d] = columns
+ * c0 .. c0 + m of the entity axis), but the scores never reach memory.  Each score is compared
+ * with its row's true score in registers and leaves as a 2-bit code -- 0: below (also the true
+ * column itself and columns past m), 1: above, 2: equal, 3: |score - true_score_i| <= band[i],
+ * to be rescored exactly by kge_rank_rows_codes -- 16 codes per 32-bit word, ldc words per row
+ * (ldc >= kge_rank_codes_ld(m)).  Rows [0, n_a) are query batch A, rows [n_a, n_a + n_b) batch B
+ * (the (s, p, ?) and the (?, p, o) queries of an evaluation batch): each brings its true scores
+ * and true columns (global ids); band: one per row, band < 0 switches code 3 off.  Replaces scores -> "scores > true" / "scores == true"
+ * sums of entity_ranking.py:164-216, 469-529 without the [n, m] score block in memory. */
+int kge_score_dot_split_rank(const void* q_hi, const void* q_lo, int64_t ldq, const float* t, int64_t ldt,
+                             int64_t n_a, int64_t n_b, int64_t m, int d, const float* true_score_a,
+                             const int64_t* true_idx_a, const float* true_score_b, const int64_t* true_idx_b,
+                             const float* band, int64_t c0, void* codes, int64_t ldc, void* stream);
+
+/* Words per row of the code block of kge_score_dot_split_rank for m columns. */
+int64_t kge_rank_codes_ld(int64_t m);
+
+/* band[i] = band_rel * |q_i|_2 * t_norm_max[0] for the n fp32 query rows q [n, d]: the per-row
+ * refinement band kge_score_dot_split_rank takes (the band kge_rank_rows derives for itself).
+ * No counterpart in the reference, which ranks exact fp32 scores (entity_ranking.py:469-529). */
+int kge_rank_band(const float* q, int64_t ldq, int64_t n, int d, float band_rel, const float* t_norm_max,
+                  float* band, void* stream);
+
+/* kge_rank_rows on the code block of kge_score_dot_split_rank instead of a score block: counts
+ * codes 1 / 2, rescores every code-3 entry exactly (q, t, d as in kge_rank_rows; q may be null
+ * only when no code 3 can occur, i.e. band < 0), adds the true entry's own tie, applies the
+ * filter lists (a listed column's code is looked up; code 3 is rescored), tie policy, ranks and
+ * histograms exactly as kge_rank_rows does (entity_ranking.py:172-216, 469-551). */
+int kge_rank_rows_codes(const void* codes, int64_t ldc, int64_t n_a, int64_t n_b, int64_t m, int64_t c0,
+                        const int64_t* true_idx_a, const float* true_score_a, const int64_t* f_ptr_a,
+                        const int64_t* t_ptr_a, const int64_t* true_idx_b, const float* true_score_b,
+                        const int64_t* f_ptr_b, const int64_t* t_ptr_b, const int64_t* f_col,
+                        const int64_t* t_col, int64_t* greater, int64_t* ties, int accumulate,
+                        int tie_handling, int64_t* ranks, float* hist, int64_t hist_len,
+                        int64_t rows_per_hist, const float* q, int64_t ldq, const float* t, int64_t ldt,
+                        int d, float band_rel, const float* t_norm_max, void* stream);
+
 /* out[0] = max_j |t_j|_2 over the m rows of t (device scalar; the refinement band of
  * kge_rank_rows).  No counterpart in the reference, which ranks exact fp32 scores
  * (entity_ranking.py:469-529). */

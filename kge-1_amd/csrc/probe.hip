@@ -129,7 +129,96 @@ __global__ void __launch_bounds__(512, 1) mfma_lds_kernel(int stages, float* __r
   out[blockIdx.x * 512 + tid] = s[0] + s[1] + s[2] + s[3];
 }
 
+// Scalar-fp32 VALU probes (one 256-thread workgroup = one wave per SIMD; the grid puts
+// `waves_per_simd` of them on every CU).  VARIANT 0: the L1-distance inner loop on registers
+// only -- 8 x 8 accumulators, acc += |q - t| as v_sub_f32 + v_add_f32 with an |.| source
+// modifier (128 instructions per iteration, + 16 that keep the operands changing);
+// 1: 64 independent v_fma_f32 chains; 2: the L1 loop with its operands read from a resident LDS
+// image the way the distance kernel reads them (4 ds_read_b128 per 128 VALU instructions).
+template <int VARIANT>
+__global__ void __launch_bounds__(256) valu_kernel(int iters, float* __restrict__ out) {
+  __shared__ __attribute__((aligned(16))) float img[2][16 * 132];
+  const int tid = threadIdx.x, tx = tid & 15, ty = tid >> 4;
+  for (int i = tid; i < 2 * 16 * 132; i += 256) (&img[0][0])[i] = (float)(mix(i + blockIdx.x) & 0xffff) * 1e-5f;
+  __syncthreads();
+  float acc[8][8];
+#pragma unroll
+  for (int a = 0; a < 8; ++a)
+#pragma unroll
+    for (int b = 0; b < 8; ++b) acc[a][b] = 0.f;
+  float q[8], t[8];
+#pragma unroll
+  for (int a = 0; a < 8; ++a) {
+    q[a] = (float)(mix(tid * 16 + a) & 0xff) * 0.01f;
+    t[a] = (float)(mix(tid * 16 + 8 + a) & 0xff) * 0.01f;
+  }
+  const float eps = out[0] == 123.f ? 0.5f : 0.001f;  // not a compile-time constant
+  for (int it = 0; it < iters; ++it) {
+    if constexpr (VARIANT == 2) {
+      const float* qb = &img[0][(it & 15) * 132];
+      const float* tb = &img[1][(it & 15) * 132];
+      const float4 q0 = *reinterpret_cast<const float4*>(qb + 4 * ty);
+      const float4 q1 = *reinterpret_cast<const float4*>(qb + 64 + 4 * ty);
+      const float4 t0 = *reinterpret_cast<const float4*>(tb + 4 * tx);
+      const float4 t1 = *reinterpret_cast<const float4*>(tb + 64 + 4 * tx);
+      q[0] = q0.x; q[1] = q0.y; q[2] = q0.z; q[3] = q0.w; q[4] = q1.x; q[5] = q1.y; q[6] = q1.z; q[7] = q1.w;
+      t[0] = t0.x; t[1] = t0.y; t[2] = t0.z; t[3] = t0.w; t[4] = t1.x; t[5] = t1.y; t[6] = t1.z; t[7] = t1.w;
+    }
+    if constexpr (VARIANT == 1) {
+#pragma unroll
+      for (int a = 0; a < 8; ++a)
+#pragma unroll
+        for (int b = 0; b < 8; ++b) acc[a][b] = __builtin_fmaf(acc[a][b], q[a], t[b]);
+#pragma unroll
+      for (int a = 0; a < 8; ++a)
+#pragma unroll
+        for (int b = 0; b < 8; ++b) acc[a][b] = __builtin_fmaf(acc[a][b], t[a], q[b]);
+    } else {
+#pragma unroll
+      for (int a = 0; a < 8; ++a)
+#pragma unroll
+        for (int b = 0; b < 8; ++b) {
+          const float dd = q[a] - t[b];
+          asm("v_add_f32 %0, %0, |%1|" : "+v"(acc[a][b]) : "v"(dd));
+        }
+    }
+    if constexpr (VARIANT != 2) {
+#pragma unroll
+      for (int a = 0; a < 8; ++a) {
+        q[a] += eps;
+        t[a] -= eps;
+      }
+    }
+  }
+  float s = 0.f;
+#pragma unroll
+  for (int a = 0; a < 8; ++a)
+#pragma unroll
+    for (int b = 0; b < 8; ++b) s += acc[a][b];
+  out[1 + blockIdx.x * 256 + tid] = s;
+}
+
 }  // namespace
+
+// VALU probe (see valu_kernel); returns the vector instructions issued per lane times the lanes
+// (lane-operations), 0 on error.  out: 1 + cus * waves_per_simd * 256 floats (out[0] is read).
+extern "C" int64_t kge_probe_valu(int variant, int waves_per_simd, int iters, float* out, int64_t out_elems,
+                                  void* stream) {
+  const int cus = num_cus();
+  if (cus <= 0 || !out || iters <= 0 || waves_per_simd < 1 || waves_per_simd > 8 ||
+      out_elems < 1 + (int64_t)cus * waves_per_simd * 256)
+    return 0;
+  const dim3 grid(cus * waves_per_simd), block(256);
+  switch (variant) {
+    case 0: valu_kernel<0><<<grid, block, 0, (hipStream_t)stream>>>(iters, out); break;
+    case 1: valu_kernel<1><<<grid, block, 0, (hipStream_t)stream>>>(iters, out); break;
+    case 2: valu_kernel<2><<<grid, block, 0, (hipStream_t)stream>>>(iters, out); break;
+    default: return 0;
+  }
+  if (hipGetLastError() != hipSuccess) return 0;
+  const int64_t per_iter = variant == 0 ? 144 : 128;
+  return (int64_t)cus * waves_per_simd * 256 * iters * per_iter;
+}
 
 // LDS-fed MFMA loop (see mfma_lds_kernel); returns the floating-point operations issued.
 extern "C" int64_t kge_probe_mfma_lds(int mode, int stages, float* out, int64_t out_elems, void* stream) {

@@ -117,6 +117,8 @@ struct RankPart {
 
 struct RankRowsArgs {
   const float* s;
+  const unsigned* codes;  // CODES kernels: the contraction's 2-bit codes instead of scores
+  int64_t ldc;
   int64_t lds, n_a, n, m, c0;
   RankPart part[2];
   const int64_t* f_col;
@@ -172,7 +174,17 @@ __device__ __forceinline__ void exact_dots_wave(const float* __restrict__ a, con
 
 constexpr int EV_CAP = 8 * NT;  // near-tie ring: one scan step pushes at most 8 entries per thread
 
-template <bool VEC, bool REFINE>
+// The 2-bit code of column j in a row of code words written by the ranking contraction
+// (kge_score_dot_split_rank): word (j / 64) * 4 + (j % 16) / 4, bit 8 * ((j % 64) / 16) + 2 * (j % 4).
+__device__ __forceinline__ unsigned kge_rank_code_of(const unsigned* __restrict__ crow, int64_t j) {
+  const unsigned w = crow[(j >> 6) * 4 + ((j & 15) >> 2)];
+  return (w >> (8 * ((j & 63) >> 4) + 2 * (j & 3))) & 3u;
+}
+
+// CODES: the row comes as 2-bit codes (0 below / not a competitor, 1 above, 2 equal, 3 inside the
+// refinement band) instead of scores; the band test has been made by the contraction's epilogue,
+// the exact rescoring of the code-3 entries happens here (REFINE must be set when any can occur).
+template <bool VEC, bool REFINE, bool CODES = false>
 __global__ void __launch_bounds__(NT) rank_rows_kernel(const RankRowsArgs a) {
   __shared__ int64_t sm[16];
   __shared__ float fsm[NT / 64];
@@ -184,7 +196,8 @@ __global__ void __launch_bounds__(NT) rank_rows_kernel(const RankRowsArgs a) {
   const RankPart& P = a.part[side];
   const float t = clean(P.true_score[li]);
   const int64_t tj = P.true_idx[li] - a.c0;
-  const float* row = a.s + i * a.lds;
+  const float* row = CODES ? nullptr : a.s + i * a.lds;
+  const unsigned* crow = CODES ? a.codes + i * a.ldc : nullptr;
   const int64_t m = a.m;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
 
@@ -218,6 +231,18 @@ __global__ void __launch_bounds__(NT) rank_rows_kernel(const RankRowsArgs a) {
     v = clean(v);
     gt += sign * (v > t);
     eq += sign * (v == t);
+  };
+  // the same for a column given by its code (never the true column: its code is 0)
+  auto count_code = [&](int64_t j, unsigned code, int sign) {
+    if (code == 3u) {
+      if (REFINE) {
+        ev[atomicAdd(&ev_total, 1u) % EV_CAP] = (int)j;
+        pushed = 1;
+      }
+      return;
+    }
+    gt += sign * (int)(code == 1u);
+    eq += sign * (int)(code == 2u);
   };
   // Rescore and count the entries pushed since `done` (block-uniform control flow): wave w
   // takes entries w, w + 4, ...; its lane 0 owns the counts.  Returns the new `done`.
@@ -271,6 +296,31 @@ __global__ void __launch_bounds__(NT) rank_rows_kernel(const RankRowsArgs a) {
   // wait in the ring for ONE drain after the scan (all their row loads in flight together).
   auto scan = [&](bool step_drain) {
     unsigned done = 0;
+    if (CODES) {
+      // 16 codes per word; a step of NT / 2 words covers 8 NT columns (what the ring holds)
+      const int64_t nwords = ((m + 63) >> 6) * 4;
+      for (int64_t base = 0; base < nwords; base += NT / 2) {  // uniform trip count
+        const int64_t wi = base + threadIdx.x;
+        if (threadIdx.x < NT / 2 && wi < nwords) {
+          const unsigned w = crow[wi];
+          if (w) {
+            const unsigned lo = w & 0x55555555u, hi = (w >> 1) & 0x55555555u;
+            gt += __popc(lo & ~hi);
+            eq += __popc(hi & ~lo);
+            unsigned near = lo & hi;  // bit 2 p set: code 3 at position p of the word
+            const int64_t jw = (wi >> 2) * 64 + (wi & 3) * 4;  // column of position (y = 0, r = 0)
+            while (REFINE && near) {
+              const int b = __ffs(near) - 1;
+              near &= near - 1;
+              count_code(jw + (b >> 3) * 16 + ((b >> 1) & 3), 3u, 1);
+            }
+          }
+        }
+        if (REFINE && step_drain) done = drain(done, 1);
+      }
+      if (threadIdx.x == 0 && tj >= 0 && tj < m) eq += 1;  // the true entry ties with itself
+      return done;
+    }
     if (VEC) {
       const int64_t m4 = m & ~(int64_t)3;
       for (int64_t base = 0; base < m4; base += 8 * NT) {  // uniform trip count
@@ -362,7 +412,10 @@ __global__ void __launch_bounds__(NT) rank_rows_kernel(const RankRowsArgs a) {
       if (x < e) {
         const int64_t j = col[x] - a.c0;
         if (j >= 0 && j < m && j != tj) {
-          count(j, row[j], -1);
+          if (CODES)
+            count_code(j, kge_rank_code_of(crow, j), -1);
+          else
+            count(j, row[j], -1);
           eq += (t == -INFINITY);  // the filtered entry is now -inf
         }
       }
@@ -463,17 +516,69 @@ extern "C" int kge_row_norm_max(const float* t, int64_t ldt, int64_t m, int d, f
   return 0;
 }
 
-extern "C" int kge_rank_rows(const float* s, int64_t lds, int64_t n_a, int64_t n_b, int64_t m, int64_t c0,
-                             const int64_t* true_idx_a, const float* true_score_a, const int64_t* f_ptr_a,
-                             const int64_t* t_ptr_a, const int64_t* true_idx_b, const float* true_score_b,
-                             const int64_t* f_ptr_b, const int64_t* t_ptr_b, const int64_t* f_col,
-                             const int64_t* t_col, int64_t* greater, int64_t* ties, int accumulate, int tie_handling,
-                             int64_t* ranks, float* hist, int64_t hist_len, int64_t rows_per_hist, const float* q,
-                             int64_t ldq, const float* t, int64_t ldt, int d, float band_rel, const float* t_norm_max,
-                             void* stream) {
+namespace {
+
+// band[i] = band_rel * |q_i|_2 * t_norm_max[0]: the refinement band of row i, as rank_rows_kernel
+// computes it for itself; a wave per row
+__global__ void __launch_bounds__(256) rank_band_kernel(const float* __restrict__ q, int64_t ldq, int64_t n, int d,
+                                                        float band_rel, const float* __restrict__ t_norm_max,
+                                                        float* __restrict__ band) {
+  const int lane = threadIdx.x & 63;
+  const int64_t i = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (i >= n) return;  // wave-uniform
+  float ss = 0.f;
+  for (int k = lane; k < d; k += 64) {
+    const float v = q[i * ldq + k];
+    ss += v * v;
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) ss += __shfl_xor(ss, off, 64);
+  // a hair wider than the kernel's own band (summation order): never narrower than the bound
+  if (lane == 0) band[i] = band_rel * sqrtf(ss) * t_norm_max[0] * 1.000001f;
+}
+
+int rank_rows_launch(RankRowsArgs& a, bool codes, hipStream_t st) {
+  const bool vec = !codes && a.lds % 4 == 0 && aligned16(a.s);
+  const unsigned n = (unsigned)a.n;
+  if (codes && a.q)
+    rank_rows_kernel<false, true, true><<<dim3(n), dim3(NT), 0, st>>>(a);
+  else if (codes)
+    rank_rows_kernel<false, false, true><<<dim3(n), dim3(NT), 0, st>>>(a);
+  else if (a.q && vec)
+    rank_rows_kernel<true, true><<<dim3(n), dim3(NT), 0, st>>>(a);
+  else if (a.q)
+    rank_rows_kernel<false, true><<<dim3(n), dim3(NT), 0, st>>>(a);
+  else if (vec)
+    rank_rows_kernel<true, false><<<dim3(n), dim3(NT), 0, st>>>(a);
+  else
+    rank_rows_kernel<false, false><<<dim3(n), dim3(NT), 0, st>>>(a);
+  KGE_CHECK_LAUNCH();
+  return 0;
+}
+
+}  // namespace
+
+extern "C" int kge_rank_band(const float* q, int64_t ldq, int64_t n, int d, float band_rel, const float* t_norm_max,
+                             float* band, void* stream) {
+  KGE_REQUIRE(n >= 0 && d > 0 && (q || n == 0) && ldq >= d && band_rel >= 0.f && t_norm_max && band && n < (1LL << 31));
+  if (n == 0) return 0;
+  rank_band_kernel<<<dim3((unsigned)((n + 3) / 4)), dim3(256), 0, as_stream(stream)>>>(q, ldq, n, d, band_rel,
+                                                                                       t_norm_max, band);
+  KGE_CHECK_LAUNCH();
+  return 0;
+}
+
+static int rank_rows_common(const float* s, int64_t lds, const unsigned* codes, int64_t ldc, int64_t n_a, int64_t n_b,
+                            int64_t m, int64_t c0, const int64_t* true_idx_a, const float* true_score_a,
+                            const int64_t* f_ptr_a, const int64_t* t_ptr_a, const int64_t* true_idx_b,
+                            const float* true_score_b, const int64_t* f_ptr_b, const int64_t* t_ptr_b,
+                            const int64_t* f_col, const int64_t* t_col, int64_t* greater, int64_t* ties,
+                            int accumulate, int tie_handling, int64_t* ranks, float* hist, int64_t hist_len,
+                            int64_t rows_per_hist, const float* q, int64_t ldq, const float* t, int64_t ldt, int d,
+                            float band_rel, const float* t_norm_max, void* stream) {
   const int64_t n = n_a + n_b;
-  KGE_REQUIRE(n_a >= 0 && n_b >= 0 && m >= 0 && m < (1LL << 31) && (m == 0 || s) && greater && ties && lds >= m &&
-              n < (1LL << 31));
+  KGE_REQUIRE(n_a >= 0 && n_b >= 0 && m >= 0 && m < (1LL << 31) && greater && ties && n < (1LL << 31));
+  KGE_REQUIRE(codes ? ldc >= ((m + 63) / 64) * 4 : ((m == 0 || s) && lds >= m));
   KGE_REQUIRE(n_a == 0 || (true_idx_a && true_score_a));
   KGE_REQUIRE(n_b == 0 || (true_idx_b && true_score_b));
   KGE_REQUIRE((!f_ptr_a && !f_ptr_b) || f_col);
@@ -489,22 +594,39 @@ extern "C" int kge_rank_rows(const float* s, int64_t lds, int64_t n_a, int64_t n
   }
   if (n == 0) return 0;
   RankRowsArgs a;
-  a.s = s; a.lds = lds; a.n_a = n_a; a.n = n; a.m = m; a.c0 = c0;
+  a.s = s; a.codes = codes; a.ldc = ldc; a.lds = lds; a.n_a = n_a; a.n = n; a.m = m; a.c0 = c0;
   a.part[0] = RankPart{true_idx_a, true_score_a, f_ptr_a, t_ptr_a};
   a.part[1] = RankPart{true_idx_b, true_score_b, f_ptr_b, t_ptr_b};
   a.f_col = f_col; a.t_col = t_col; a.greater = greater; a.ties = ties; a.accumulate = accumulate;
   a.tie = tie_handling; a.ranks = ranks; a.hist = hist; a.hist_len = hist_len; a.rows_per_hist = rows_per_hist;
   a.q = q; a.ldq = ldq; a.t = t; a.ldt = ldt; a.d = d; a.band_rel = band_rel; a.t_norm_max = t_norm_max;
-  hipStream_t st = as_stream(stream);
-  const bool vec = lds % 4 == 0 && aligned16(s);
-  if (q && vec)
-    rank_rows_kernel<true, true><<<dim3((unsigned)n), dim3(NT), 0, st>>>(a);
-  else if (q)
-    rank_rows_kernel<false, true><<<dim3((unsigned)n), dim3(NT), 0, st>>>(a);
-  else if (vec)
-    rank_rows_kernel<true, false><<<dim3((unsigned)n), dim3(NT), 0, st>>>(a);
-  else
-    rank_rows_kernel<false, false><<<dim3((unsigned)n), dim3(NT), 0, st>>>(a);
-  KGE_CHECK_LAUNCH();
-  return 0;
+  return rank_rows_launch(a, codes != nullptr, as_stream(stream));
+}
+
+extern "C" int kge_rank_rows(const float* s, int64_t lds, int64_t n_a, int64_t n_b, int64_t m, int64_t c0,
+                             const int64_t* true_idx_a, const float* true_score_a, const int64_t* f_ptr_a,
+                             const int64_t* t_ptr_a, const int64_t* true_idx_b, const float* true_score_b,
+                             const int64_t* f_ptr_b, const int64_t* t_ptr_b, const int64_t* f_col,
+                             const int64_t* t_col, int64_t* greater, int64_t* ties, int accumulate, int tie_handling,
+                             int64_t* ranks, float* hist, int64_t hist_len, int64_t rows_per_hist, const float* q,
+                             int64_t ldq, const float* t, int64_t ldt, int d, float band_rel, const float* t_norm_max,
+                             void* stream) {
+  return rank_rows_common(s, lds, nullptr, 0, n_a, n_b, m, c0, true_idx_a, true_score_a, f_ptr_a, t_ptr_a, true_idx_b,
+                          true_score_b, f_ptr_b, t_ptr_b, f_col, t_col, greater, ties, accumulate, tie_handling, ranks,
+                          hist, hist_len, rows_per_hist, q, ldq, t, ldt, d, band_rel, t_norm_max, stream);
+}
+
+extern "C" int kge_rank_rows_codes(const void* codes, int64_t ldc, int64_t n_a, int64_t n_b, int64_t m, int64_t c0,
+                                   const int64_t* true_idx_a, const float* true_score_a, const int64_t* f_ptr_a,
+                                   const int64_t* t_ptr_a, const int64_t* true_idx_b, const float* true_score_b,
+                                   const int64_t* f_ptr_b, const int64_t* t_ptr_b, const int64_t* f_col,
+                                   const int64_t* t_col, int64_t* greater, int64_t* ties, int accumulate,
+                                   int tie_handling, int64_t* ranks, float* hist, int64_t hist_len,
+                                   int64_t rows_per_hist, const float* q, int64_t ldq, const float* t, int64_t ldt,
+                                   int d, float band_rel, const float* t_norm_max, void* stream) {
+  KGE_REQUIRE(codes || m == 0);
+  return rank_rows_common(nullptr, 0, (const unsigned*)codes, ldc, n_a, n_b, m, c0, true_idx_a, true_score_a, f_ptr_a,
+                          t_ptr_a, true_idx_b, true_score_b, f_ptr_b, t_ptr_b, f_col, t_col, greater, ties, accumulate,
+                          tie_handling, ranks, hist, hist_len, rows_per_hist, q, ldq, t, ldt, d, band_rel, t_norm_max,
+                          stream);
 }

@@ -36,11 +36,43 @@ struct PCfg {
 // 8 = no barrier inside the K loop (timing only: the waves race on the LDS image).
 // PIPE: the K loop software-pipelined inside each wave (see the loop): same barriers, same
 // in-flight counts, same MFMA order per accumulator (bit-identical scores).
-template <int BM, int BN, int WM, int WN, int ABL = 0, bool PIPE = false>
+//
+// RANK (the evaluation job's contraction): the scores never leave the registers.  The epilogue
+// compares each accumulator with its row's true score and writes a 2-bit CODE per entry instead
+// of the fp32 score -- 0: below the true score (also: the true column itself, columns past m),
+// 1: above, 2: equal, 3: within the row's refinement band of the true score (to be rescored
+// exactly by the ranking kernel) -- 16 codes per 32-bit word, 1/16 of the score block's bytes.
+// Word layout of a row: word (j / 64) * 4 + (j % 16) / 4 holds column j's code at bit
+// 8 * ((j % 64) / 16) + 2 * (j % 4)  (kge_rank_code_of in rank.hip decodes it).
+struct RankEpi {
+  // rows [0, n_a) are query batch A, rows [n_a, n) batch B: each brings its true scores and the
+  // global column of its true entry
+  const float* true_score_a;
+  const int64_t* true_idx_a;
+  const float* true_score_b;
+  const int64_t* true_idx_b;
+  int n_a;
+  const float* band;        // [n] |score - true| <= band -> code 3 (negative: never)
+  int64_t c0;               // global column of this table's row 0
+  unsigned* codes;          // [n, ldc]
+  int64_t ldc;              // words per row: ceil(m / 256) * 16
+};
+
+// The lane id computed where it is called (volatile asm: never hoisted out of a loop and kept in
+// a register, or spilled, across it).
+__device__ __forceinline__ int lane_id_here() {
+  int l;
+  asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
+  return l;
+}
+
+template <int BM, int BN, int WM, int WN, int ABL = 0, bool PIPE = false, bool RANK = false>
 __global__ void __launch_bounds__(64 * WM * WN, 1)
     score_dot_persist16_kernel(const __bf16* __restrict__ qhi, const __bf16* __restrict__ qlo, int64_t ldq,
                                const float* __restrict__ t, int64_t ldt, const int64_t* __restrict__ tidx, int n,
-                               int m, int d, float* __restrict__ s, int64_t lds, int nrt, int ntiles) {
+                               int m, int d, float* __restrict__ s, int64_t lds, int nrt, int ntiles,
+                               const RankEpi re) {
+  static_assert(!RANK || (PIPE && BN == 256 && WN == 4), "the code words assume transposed accumulators, 64-column waves");
   using C = PCfg<BM, BN, WM, WN>;
   constexpr int NW = C::NT / 64;
   constexpr int TM = BM / WM / 16, TN = BN / WN / 16;  // 16 x 16 tiles per wave
@@ -87,11 +119,19 @@ __global__ void __launch_bounds__(64 * WM * WN, 1)
     // A planes by LDS-DMA: wave-instruction c fills rows 16c .. 16c+15 of a plane (64 B
     // each, lane-linear destination), so the 16x16x32 read swizzle goes on the source
     // address.  Rows past n read row n-1: their scores are never stored.
+    // RANK: the thread coordinates of the prologue are taken behind an opaque asm, so that the
+    // per-slot row numbers derived from them are recomputed per tile instead of being kept
+    // (spilled) across the K loop, whose registers that variant has no room to share
+    int tid_t = tid;
+    if constexpr (RANK) {  // the thread id anew (wave is scalar, the lane id comes from mbcnt)
+      tid_t = wave * 64 + lane_id_here();
+    }
+    const int lane_t = tid_t & 63;
     const __bf16* ga[A_G];
 #pragma unroll
     for (int i = 0; i < A_G; ++i) {
-      const int row = (wave * A_G + i) * 16 + (lane >> 2);
-      const int slot = (lane & 3) ^ ((0x78 >> (2 * ((row >> 2) & 3))) & 3);
+      const int row = (wave * A_G + i) * 16 + (lane_t >> 2);
+      const int slot = (lane_t & 3) ^ ((0x78 >> (2 * ((row >> 2) & 3))) & 3);
       ga[i] = qhi + (int64_t)min(m0 + row, n - 1) * ldq + slot * 8;
     }
     // B (entity rows, fp32) through registers: float4 f of the stage = row f / 8, cols 4 (f % 8)
@@ -100,14 +140,14 @@ __global__ void __launch_bounds__(64 * WM * WN, 1)
     static_assert(C::NT % 128 == 0, "B slot stride");
     const float* b_src[C::B_PER_T];
     constexpr bool B_RAGGED = BN * 8 % C::NT != 0;  // the last slot of some threads idles
-    const bool b_last = !B_RAGGED || tid + (C::B_PER_T - 1) * C::NT < BN * 8;
-    const int b_col = (tid & 7) * 4;
-    const int b_off0 = sw16_off(tid >> 3, b_col >> 3) + ((b_col >> 2) & 1) * 8;
+    const bool b_last = !B_RAGGED || tid_t + (C::B_PER_T - 1) * C::NT < BN * 8;
+    const int b_col = (tid_t & 7) * 4;
+    const int b_off0 = sw16_off(tid_t >> 3, b_col >> 3) + ((b_col >> 2) & 1) * 8;
 #pragma unroll
     for (int i = 0; i < C::B_PER_T; ++i) {
-      const int row = min((tid >> 3) + i * (C::NT / 8), BN - 1);
+      const int row = min((tid_t >> 3) + i * (C::NT / 8), BN - 1);
       const int ej = n0 + row;  // rows past m read row 0: their scores are never stored
-      const int64_t er = ej < m ? (tidx ? tidx[ej] : (int64_t)ej) : 0;
+      const int64_t er = ej < m ? ((!RANK && tidx) ? tidx[ej] : (int64_t)ej) : 0;
       b_src[i] = t + ((ABL & 64) ? (er & 63) : er) * ldt + b_col;  // dev 64: every panel reads rows 0 .. 63
     }
     u32x4 rv[C::B_PER_T];
@@ -321,6 +361,53 @@ __global__ void __launch_bounds__(64 * WM * WN, 1)
 #undef KGE_WAIT_VM
     if (ABL & 4) t_loop1 = __builtin_amdgcn_s_memtime();
 
+    if constexpr (RANK) {
+      // transposed accumulators: acc[x][y][r] = row (lane & 15) of band x, column 16 y + 4 fs + r
+      // of this wave's 64 columns; one code word per lane and band.  The lane coordinates are
+      // re-derived behind an opaque asm so that nothing of the epilogue's address arithmetic is
+      // hoisted out of the tile loop and kept alive across the K loop (no register to spare there);
+      // the lane id itself comes from mbcnt, not from a register kept since kernel entry.
+      const int lane_e = lane_id_here();
+      const int fr_e = lane_e & 15, fs_e = lane_e >> 4;
+      const int jw = n0 + wc * WCOLS;  // first column of the wave (a multiple of 64)
+      auto row_info = [&](int x, float& ts, float& bd, int& tjr) {
+        const int ic = min(m0 + wr * (BM / WM) + x * 16 + fr_e, n - 1);
+        const bool in_a = ic < re.n_a;
+        const float v = in_a ? re.true_score_a[ic] : re.true_score_b[ic - re.n_a];
+        ts = v == v ? v : -INFINITY;
+        bd = re.band[ic];
+        const int64_t tj = (in_a ? re.true_idx_a[ic] : re.true_idx_b[ic - re.n_a]) - re.c0 - jw;  // wave-relative
+        tjr = (tj >= 0 && tj < WCOLS) ? (int)tj : -1;
+      };
+      float ts_n, bd_n;
+      int tj_n;
+      row_info(0, ts_n, bd_n, tj_n);
+#pragma unroll
+      for (int x = 0; x < TM; ++x) {
+        const float ts = ts_n, bd = bd_n;
+        const int tjr = tj_n;
+        if (x + 1 < TM) row_info(x + 1, ts_n, bd_n, tj_n);
+        unsigned word = 0;
+#pragma unroll
+        for (int y = 0; y < TN; ++y) {
+          const int jb = y * 16 + 4 * fs_e;  // of the wave's 64 columns
+          const int rem = m - jw - jb;       // columns jb + r with r >= rem lie past m
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            float v = acc[x][y][r];
+            v = v == v ? v : -INFINITY;
+            unsigned code = (v > ts) ? 1u : ((v == ts) ? 2u : 0u);
+            code = (__builtin_fabsf(v - ts) <= bd) ? 3u : code;
+            code = (r < rem && jb + r != tjr) ? code : 0u;
+            word |= code << (8 * y + 2 * r);
+          }
+        }
+        const int i = m0 + wr * (BM / WM) + x * 16 + fr_e;
+        if (i < n) re.codes[(int64_t)i * re.ldc + (jw >> 6) * 4 + fs_e] = word;
+      }
+      __syncthreads();  // every wave has read its last K stage: the next tile's prologue may overwrite LDS
+      continue;
+    }
     // epilogue: C/D of 16x16 -- lane holds column (lane & 15), rows 4 (lane >> 4) + r
     __syncthreads();  // stage buffers free: per-wave scratch of 16 rows x WCOLS (+4) floats
     float* scr = reinterpret_cast<float*>(smem) + wave * 16 * SCR_LD;
@@ -369,22 +456,24 @@ __global__ void __launch_bounds__(64 * WM * WN, 1)
   }
 }
 
-template <int BM, int BN, int WM, int WN, int ABL = 0, bool PIPE = false>
+template <int BM, int BN, int WM, int WN, int ABL = 0, bool PIPE = false, bool RANK = false>
 int launch_persist16(const __bf16* qhi, const __bf16* qlo, int64_t ldq, const float* t, int64_t ldt,
-                     const int64_t* tidx, int64_t n, int64_t m, int d, float* s, int64_t lds, hipStream_t st) {
+                     const int64_t* tidx, int64_t n, int64_t m, int d, float* s, int64_t lds, hipStream_t st,
+                     const RankEpi re = RankEpi{}) {
   using C = PCfg<BM, BN, WM, WN>;
   const int nrt = (int)((n + BM - 1) / BM);
   const int64_t ntiles = (int64_t)nrt * ((m + BN - 1) / BN);
   if (ntiles > 0x7fffffff) return KGE_ERR_ARG;
   const size_t shmem = 2 * C::STAGE;
   static std::atomic<bool> lds_ok[KGE_MAX_DEVICES];
-  if (const int e = kge_allow_lds((const void*)score_dot_persist16_kernel<BM, BN, WM, WN, ABL, PIPE>, (int)shmem, lds_ok))
+  if (const int e = kge_allow_lds((const void*)score_dot_persist16_kernel<BM, BN, WM, WN, ABL, PIPE, RANK>, (int)shmem,
+                                  lds_ok))
     return e;
   int grid = kge_num_cus();
   grid = (int)std::min<int64_t>(grid, (ntiles + 7) / 8 * 8);
   grid = std::max(8, grid / 8 * 8);
-  score_dot_persist16_kernel<BM, BN, WM, WN, ABL, PIPE><<<dim3(grid), dim3(C::NT), shmem, st>>>(
-      qhi, qlo, ldq, t, ldt, tidx, (int)n, (int)m, d, s, lds, nrt, (int)ntiles);
+  score_dot_persist16_kernel<BM, BN, WM, WN, ABL, PIPE, RANK><<<dim3(grid), dim3(C::NT), shmem, st>>>(
+      qhi, qlo, ldq, t, ldt, tidx, (int)n, (int)m, d, s, lds, nrt, (int)ntiles, re);
   KGE_CHECK_LAUNCH();
   return 0;
 }
@@ -452,6 +541,34 @@ extern "C" int kge_score_dot_split(const void* qhi, const void* qlo, int64_t ldq
   if (n > 128 && cost256 <= cost128)
     return launch_persist16<256, 256, 2, 4, 0, true>(h, l, ldq, t, ldt, tidx, n, m, d, s, lds, st);
   return launch_persist16<128, 256, 2, 4, 0, true>(h, l, ldq, t, ldt, tidx, n, m, d, s, lds, st);
+}
+
+extern "C" int64_t kge_rank_codes_ld(int64_t m) { return m <= 0 ? 0 : (m + 255) / 256 * 16; }
+
+extern "C" int kge_score_dot_split_rank(const void* qhi, const void* qlo, int64_t ldq, const float* t, int64_t ldt,
+                                        int64_t n_a, int64_t n_b, int64_t m, int d, const float* true_score_a,
+                                        const int64_t* true_idx_a, const float* true_score_b,
+                                        const int64_t* true_idx_b, const float* band, int64_t c0, void* codes,
+                                        int64_t ldc, void* stream) {
+  const int64_t n = n_a + n_b;
+  KGE_REQUIRE(n_a >= 0 && n_b >= 0 && m >= 0 && d >= 4 && n < (1LL << 31) && m < (1LL << 31));
+  KGE_REQUIRE(qhi && qlo && t && ldt >= d && band && codes && ldc >= kge_rank_codes_ld(m));
+  KGE_REQUIRE((n_a == 0 || (true_score_a && true_idx_a)) && (n_b == 0 || (true_score_b && true_idx_b)));
+  KGE_REQUIRE(ldq % 8 == 0 && ldq >= ((d + 31) / 32) * 32);
+  if (d % 4 != 0 || ldt % 4 != 0 || !aligned16(t) || !aligned16(qhi) || !aligned16(qlo)) return KGE_ERR_ALIGN;
+  if (n == 0 || m == 0) return 0;
+  hipStream_t st = as_stream(stream);
+  const __bf16* h = (const __bf16*)qhi;
+  const __bf16* l = (const __bf16*)qlo;
+  const RankEpi re{true_score_a, true_idx_a, true_score_b, true_idx_b, (int)n_a, band, c0, (unsigned*)codes, ldc};
+  // tile height as in kge_score_dot_split (the code words do not depend on it)
+  const int64_t slots = std::max(8, kge_num_cus() / 8 * 8);
+  const int64_t panels = (m + 255) / 256;
+  const double cost256 = (double)((((n + 255) / 256) * panels + slots - 1) / slots);
+  const double cost128 = 0.55 * (double)((((n + 127) / 128) * panels + slots - 1) / slots);
+  if (n > 128 && cost256 <= cost128)
+    return launch_persist16<256, 256, 2, 4, 0, true, true>(h, l, ldq, t, ldt, nullptr, n, m, d, nullptr, 0, st, re);
+  return launch_persist16<128, 256, 2, 4, 0, true, true>(h, l, ldq, t, ldt, nullptr, n, m, d, nullptr, 0, st, re);
 }
 
 #ifdef KGE_DEV_BUILD  // libkgescore_dev.so only: ablation / probe variants for scripts/dev

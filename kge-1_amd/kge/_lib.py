@@ -77,6 +77,12 @@ SIGNATURES = {
     "kge_rank_rows": ([_P, _I64, _I64, _I64, _I64, _I64, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _P, _P,
                        _I64, _I64, _P, _I64, _P, _I64, _I, _F, _P, _P], _I),
     "kge_row_norm_max": ([_P, _I64, _I64, _I, _P, _P], _I),
+    "kge_score_dot_split_rank": ([_P, _P, _I64, _P, _I64, _I64, _I64, _I64, _I, _P, _P, _P, _P, _P, _I64, _P, _I64,
+                                  _P], _I),
+    "kge_rank_codes_ld": ([_I64], _I64),
+    "kge_rank_band": ([_P, _I64, _I64, _I, _F, _P, _P, _P], _I),
+    "kge_rank_rows_codes": ([_P, _I64, _I64, _I64, _I64, _I64, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I,
+                             _P, _P, _I64, _I64, _P, _I64, _P, _I64, _I, _F, _P, _P], _I),
     "kge_softmax_planes_max_columns": ([], _I64),
     "kge_softmax_xent_planes": ([_P, _I64, _I64, _I64, _I64, _P, _F, _P, _P], _I),
     "kge_softmax_kl_planes": ([_P, _I64, _I64, _I64, _I64, _P, _P, _F, _F, _P, _P], _I),
@@ -480,14 +486,65 @@ def _i64c(t, what):
     return t
 
 
+def rank_codes_ld(m: int) -> int:
+    """Words per row of the code block of score_dot_split_rank for m columns."""
+    return (m + 255) // 256 * 16
+
+
+def rank_band(q, band_rel, t_norm_max):
+    """kge_rank_band: the per-row refinement bands band_rel * |q_i| * t_norm_max of fp32 rows q."""
+    n, d = q.shape
+    band = torch.empty(n, device=q.device, dtype=torch.float32)
+    _check(lib().kge_rank_band(ptr(q), rows(q), n, d, float(band_rel), ptr(t_norm_max), ptr(band), stream()),
+           "kge_rank_band")
+    return band
+
+
+def score_dot_split_rank(q_hi, q_lo, t, d, n_a, part_a, part_b, band, c0, codes=None):
+    """kge_score_dot_split_rank: the contraction of score_dot_split whose epilogue compares every
+    score with its row's true score and writes 2-bit codes [n, rank_codes_ld(m)] (int32 words)
+    instead of scores.  t: the fp32 rows of columns c0 .. c0 + len(t) of the entity axis;
+    part = (true_idx, true_score) of rows [0, n_a) and of the rest (part_b None: one batch)."""
+    require_device(q_hi, t)
+    n, m = q_hi.shape[0], t.shape[0]
+    n_b = n - n_a
+    if part_b is None:
+        part_b = (None, None)
+        if n_b:
+            raise ValueError("score_dot_split_rank: rows beyond n_a need part_b")
+    args = []
+    for (true_idx, true_score), k in ((part_a, n_a), (part_b, n_b)):
+        if k and (true_score.dtype != torch.float32 or not true_score.is_contiguous() or true_score.numel() < k
+                  or _i64c(true_idx, "true_idx").numel() < k):
+            raise ValueError("score_dot_split_rank: true scores (contiguous float32) and columns (int64) per row")
+        args += [ptr(true_score), ptr(true_idx)]
+    if band.dtype != torch.float32 or not band.is_contiguous() or band.numel() < n:
+        raise ValueError("score_dot_split_rank: band is contiguous float32 [n]")
+    ldc = rank_codes_ld(m)
+    if codes is None:
+        codes = torch.empty(n, ldc, device=t.device, dtype=torch.int32)
+    elif codes.dtype != torch.int32 or codes.shape[0] < n or codes.stride(0) < ldc or codes.stride(1) != 1:
+        raise ValueError("score_dot_split_rank: codes must be int32 [n, >= rank_codes_ld(m)]")
+    _check(lib().kge_score_dot_split_rank(ptr(q_hi), ptr(q_lo), q_hi.stride(0), ptr(t), rows(t), n_a, n_b, m, d,
+                                          *args, ptr(band), int(c0), ptr(codes), codes.stride(0), stream()),
+           "kge_score_dot_split_rank")
+    return codes
+
+
 def rank_rows(s, n_a, c0, part_a, part_b, f_col, t_col, greater, ties, accumulate, tie_handling=None, ranks=None,
-              hists=None, rows_per_hist=0, refine=None):
-    """kge_rank_rows: one ranking launch for the stacked score block s [n_a + n_b, m].
+              hists=None, rows_per_hist=0, refine=None, codes=None, m=None):
+    """kge_rank_rows: one ranking launch for the stacked score block s [n_a + n_b, m] -- or, with
+    codes (and m columns; s None), kge_rank_rows_codes on the code block of score_dot_split_rank.
     part = (true_idx, true_score, f_ptr, t_ptr) of each batch (part_b None: one batch);
     tie_handling (a name) also writes ranks / hists [k, hist_len]; refine = (q, t_rows,
     band_rel, t_norm_max) rescoring near-ties exactly.  Nothing is copied: every tensor
     must already have the kernel's layout."""
-    n, m = s.shape
+    if codes is not None:
+        if s is not None or m is None or codes.dtype != torch.int32 or codes.stride(1) != 1:
+            raise ValueError("rank_rows: codes are an int32 [n, ldc] block and come with m, without scores")
+        n = codes.shape[0]
+    else:
+        n, m = s.shape
     n_b = n - n_a
     if part_b is None:
         part_b = (None, None, None, None)
@@ -521,11 +578,13 @@ def rank_rows(s, n_a, c0, part_a, part_b, f_col, t_col, greater, ties, accumulat
         d = q.shape[1]
         if q.shape[0] != n or t_rows.shape[0] != m or t_rows.shape[1] != d:
             raise ValueError("rank_rows: refinement operands do not match the score block")
-    _check(lib().kge_rank_rows(ptr(s), rows(s), n_a, n_b, m, c0, *args, ptr(_i64c(f_col, "f_col")),
-                               ptr(_i64c(t_col, "t_col")), ptr(greater), ptr(ties), int(accumulate), tie, ptr(ranks),
-                               ptr(hists), hist_len, rows_per_hist, ptr(q), rows(q) if q is not None else 0,
-                               ptr(t_rows), rows(t_rows) if t_rows is not None else 0, d, float(band), ptr(tmax),
-                               stream()), "kge_rank_rows")
+    fn, src, ld = ((lib().kge_rank_rows, s, rows(s)) if codes is None
+                   else (lib().kge_rank_rows_codes, codes, codes.stride(0)))
+    _check(fn(ptr(src), ld, n_a, n_b, m, c0, *args, ptr(_i64c(f_col, "f_col")),
+              ptr(_i64c(t_col, "t_col")), ptr(greater), ptr(ties), int(accumulate), tie, ptr(ranks),
+              ptr(hists), hist_len, rows_per_hist, ptr(q), rows(q) if q is not None else 0,
+              ptr(t_rows), rows(t_rows) if t_rows is not None else 0, d, float(band), ptr(tmax),
+              stream()), "kge_rank_rows")
 
 
 def row_norm_max(t):

@@ -544,6 +544,45 @@ def score_parts(kind: int, precision: int, l_norm: float, ent: torch.Tensor, rel
     return out, None
 
 
+def rank_codes_applicable(kind: int, precision: int, ent: torch.Tensor) -> bool:
+    """Whether rank_parts serves this scorer / table: a bilinear model whose queries contract
+    with whole entity rows, on the split bf16x3 contraction."""
+    ent = _rows(ent)
+    return (kind in (L.COMPLEX, L.DISTMULT, L.RESCAL, L.SIMPLE) and ent.dim() == 2 and ent.stride(1) == 1
+            and L.split_ok(L.query_width(kind, ent.shape[1]), ent, precision))
+
+
+@torch.no_grad()
+def rank_parts(kind: int, ent: torch.Tensor, rel: torch.Tensor, parts, true_parts, c0: int, c1: int, band_rel,
+               t_norm_max):
+    """The evaluation contraction with the ranking fused in (kge_score_dot_split_rank): the
+    stacked query batches parts = [(direction, eidx, ridx), ...] (one or two) against entity rows
+    [c0, c1), each score compared with its row's true score in the contraction's epilogue;
+    true_parts = [(true_idx, true_score), ...] per batch.  band_rel None: plain comparison of
+    the bf16x3 scores; else entries within band_rel |q_i| t_norm_max of the true score are marked
+    for exact rescoring.  Returns (codes [n, ldc] int32, fp32 query rows or None, n_a)."""
+    L.require_device(ent, rel)
+    ent, rel = _rows(ent), _rows(rel)
+    parts = [(d, L.idx64(e), L.idx64(r)) for d, e, r in parts]
+    n = sum(e.numel() for _, e, _ in parts)
+    d_e, d_r = ent.shape[1], rel.shape[1]
+    qw = L.query_width(kind, d_e)
+    refine = band_rel is not None
+    q = torch.empty(n, qw, device=ent.device, dtype=torch.float32) if refine else None
+    ldp = (qw + 31) // 32 * 32
+    hi = torch.empty(n, ldp, device=ent.device, dtype=torch.bfloat16)
+    lo = torch.empty_like(hi)
+    sq = StackedQueries.of(parts)
+    L.prep_query_split2(kind, sq.dir_a, sq.dir_b, sq.n_a, None, ent, sq.eidx, rel, sq.ridx, d_e, d_r, out=(q, hi, lo))
+    if refine:
+        band = L.rank_band(q, band_rel, t_norm_max)
+    else:
+        band = torch.full((n,), -1.0, device=ent.device, dtype=torch.float32)
+    codes = _timed(L.score_dot_split_rank, hi, lo, ent[c0:c1], qw, sq.n_a, true_parts[0],
+                   true_parts[1] if len(true_parts) > 1 else None, band, c0)
+    return codes, q, sq.n_a
+
+
 class _ScoreSpo(torch.autograd.Function):
     @staticmethod
     def forward(ctx, kind, l_norm, ent, sidx, rel, pidx, oidx):

@@ -289,6 +289,18 @@ class EntityRankingJob(EvaluationJob):
             if not self._refine:
                 ent_rows = None
                 self.model.get_scorer().precision_override = "fp32"
+        # Ranking fused into the contraction (engine.fused_rank): bilinear lookup models on the split
+        # bf16x3 contraction, with or without refinement; everything else ranks a score block
+        self._fused_rank = False
+        if sharded is None and self.config.get("engine.fused_rank"):
+            from .. import engine
+
+            tabs = self.model._lookup_tables()
+            sc = self.model.get_scorer()
+            if tabs is not None and engine.rank_codes_applicable(sc.engine_kind, sc.precision(), tabs[0].detach()):
+                self._fused_rank = True
+                if ent_rows is None:
+                    ent_rows = tabs[0].detach()
         ranks_out = {f"{d}{r}": [] for d in "so" for r in self.rankings}
         epoch_time = -time.time()
         N = len(self.triples)
@@ -394,6 +406,24 @@ class EntityRankingJob(EvaluationJob):
                 rk = torch.empty(nrank * 2 * B, dtype=torch.int64, device=dev)
                 for c0 in range(0, E, chunk):
                     c1 = min(E, c0 + chunk)
+                    finish = dict(accumulate=not single, tie_handling=self.tie_handling if single else None,
+                                  ranks=rk if single else None, hists=hists_flat if single else None, rows_per_hist=B)
+                    if self._fused_rank:
+                        # the contraction compares every score with its row's true score in registers
+                        # and leaves 2-bit codes: no [2B, C] score block is written or read
+                        if self._refine and tmax is None:
+                            tmax = _lib.row_norm_max(ent_rows)
+                        fused = self.model.rank_sp_po_codes(
+                            s, p, o, o_true, s_true, c0, c1, refine_band(ent_rows.shape[1]) if self._refine else None,
+                            tmax, p_po=p_po)
+                        if fused is None:
+                            raise RuntimeError("the model stopped serving the fused ranking contraction")
+                        codes, q = fused
+                        refine = (q, ent_rows[c0:c1], refine_band(q.shape[1]), tmax) if self._refine else None
+                        _lib.rank_rows(None, B, c0, part_a, part_b, f_col, t_col, counts[0], counts[1], codes=codes,
+                                       m=c1 - c0, refine=refine, **finish)
+                        del codes
+                        continue
                     subset = None if single else torch.arange(c0, c1, device=dev)
                     # [2B, C]: the (s, p, ?) rows on top of the (?, p, o) rows, one engine pass
                     scores, q = self.model.score_sp_po_rows(s, p, o, subset, want_q=self._refine, p_po=p_po)
@@ -406,10 +436,8 @@ class EntityRankingJob(EvaluationJob):
                         raise RuntimeError("engine.eval_precision bf16x3_refined: the engine returned no fp32 query "
                                            "rows to rescore near-ties with")
                     # a single chunk finishes the batch in the same launch: ranks + histograms
-                    _lib.rank_rows(scores, B, c0, part_a, part_b, f_col, t_col, counts[0], counts[1],
-                                   accumulate=not single, tie_handling=self.tie_handling if single else None,
-                                   ranks=rk if single else None, hists=hists_flat if single else None,
-                                   rows_per_hist=B, refine=refine)
+                    _lib.rank_rows(scores, B, c0, part_a, part_b, f_col, t_col, counts[0], counts[1], refine=refine,
+                                   **finish)
                     del scores
                 if not single:
                     _lib.rank_hist_multi(counts[0], counts[1], B, self.tie_handling, rk, hists_flat)

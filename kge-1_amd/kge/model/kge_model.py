@@ -550,6 +550,25 @@ class KgeModel(KgeBase):
         C = both.shape[1] // 2
         return torch.cat((both[:, :C], both[:, C:]), dim=0), None
 
+    def rank_sp_po_codes(self, s: Tensor, p: Tensor, o: Tensor, true_o: Tensor, true_s: Tensor, c0: int, c1: int,
+                         band_rel=None, t_norm_max=None, p_po: Tensor = None):
+        """What the evaluation job ranks from, without the score block: the scores of
+        score_sp_po_rows over entities [c0, c1) compared with each query's true score inside the
+        contraction (engine.rank_parts) -- rows [0, n) the (s, p, ?) queries against true_o (true
+        column o), rows [n, 2n) the (?, p, o) queries against true_s (true column s).  Returns
+        (codes, fp32 query rows or None) or None when the model is not served (the caller then
+        ranks score_sp_po_rows)."""
+        from .. import engine, _lib
+
+        tabs = self._lookup_tables()
+        sc = self._scorer
+        if tabs is None or not engine.rank_codes_applicable(sc.engine_kind, sc.precision(), tabs[0].detach()):
+            return None
+        parts = [((_lib.DIR_SP if d == "sp_" else _lib.DIR_PO), e, r) for d, e, r in self._sp_po_parts(s, p, o, p_po)]
+        codes, q, _ = engine.rank_parts(sc.engine_kind, tabs[0].detach(), tabs[1].detach(), parts,
+                                        [(o, true_o), (s, true_s)], c0, c1, band_rel, t_norm_max)
+        return codes, q
+
     def score_sp_po(self, s: Tensor, p: Tensor, o: Tensor, entity_subset: Tensor = None) -> Tensor:
         """cat(score_sp(s,p,subset), score_po(p,o,subset)) -> [n, 2|subset|]
         (kge_model.py:706-746)."""

@@ -228,9 +228,26 @@ class EngineOps:
     def rank_hist_multi(self, greater, ties, rows_per_hist, tie_handling, ranks, hists):
         self.L.rank_hist_multi(greater, ties, rows_per_hist, tie_handling, ranks, hists)
 
-    def rank_rows(self, s, n_a, c0, part_a, part_b, f_col, t_col, greater, ties, refine=None):
-        """Adds the stacked block's counts over columns [c0, c0 + s.shape[1]) (kge_rank_rows)."""
-        self.L.rank_rows(s, n_a, c0, part_a, part_b, f_col, t_col, greater, ties, accumulate=True, refine=refine)
+    def rank_rows(self, s, n_a, c0, part_a, part_b, f_col, t_col, greater, ties, refine=None, codes=None, m=None):
+        """Adds the stacked block's counts over columns [c0, c0 + m) (kge_rank_rows on a score
+        block s, or kge_rank_rows_codes on the code block of rank_codes)."""
+        self.L.rank_rows(s, n_a, c0, part_a, part_b, f_col, t_col, greater, ties, accumulate=True, refine=refine,
+                         codes=codes, m=m)
+
+    def rank_codes(self, q, tab, n_a, true_a, true_b, refinement, c0):
+        """The stacked fp32 query rows q against the rows of tab (columns c0 .. of the entity
+        axis) with the ranking fused into the contraction (kge_score_dot_split_rank): 2-bit codes
+        instead of a score block, or None when this scorer / layout is not served."""
+        from .engine import rank_codes_applicable
+
+        if not rank_codes_applicable(self.kind, self.precision, tab) or q.shape[1] != tab.shape[1]:
+            return None
+        hi, lo = self.L.split_rows(q)
+        if refinement is not None:
+            band = self.L.rank_band(q, refinement[0], refinement[1])
+        else:
+            band = torch.full((q.shape[0],), -1.0, device=q.device, dtype=torch.float32)
+        return self.L.score_dot_split_rank(hi, lo, tab, q.shape[1], n_a, true_a, true_b, band, c0)
 
     def refinement(self, ent):
         """(band relative to |q_i| max_j |t_j|, device scalar max_j |t_j| over ``ent``) when the
@@ -609,16 +626,21 @@ class RowShardedScorer:
             true_s, rel_b = self.ops.spo(rows[B:], self.rel, p_inverse, rows[:B]).view(-1).float().contiguous(), p_inverse
         q = torch.cat([self.ops.prep(0, rows, ar, self.rel, p), self.ops.prep(dir_b, rows, ar + B, self.rel, rel_b)])
         E_k = self.hi - self.lo
-        buf = torch.empty(2 * B, (E_k + 3) // 4 * 4, device=dev, dtype=torch.float32)
-        scores = self.ops.score(q, wa, out=buf[:, :E_k])
         nrank = 1 + (f_ptrs is not None) + (t_ptrs is not None)
         counts = torch.zeros(2, nrank * 2 * B, dtype=torch.int64, device=dev)
-        part_a = (o.contiguous(), true_o, f_ptrs[0] if f_ptrs is not None else None,
-                  t_ptrs[0] if t_ptrs is not None else None)
-        part_b = (s.contiguous(), true_s, f_ptrs[1] if f_ptrs is not None else None,
-                  t_ptrs[1] if t_ptrs is not None else None)
+        o, s = o.contiguous(), s.contiguous()
+        part_a = (o, true_o, f_ptrs[0] if f_ptrs is not None else None, t_ptrs[0] if t_ptrs is not None else None)
+        part_b = (s, true_s, f_ptrs[1] if f_ptrs is not None else None, t_ptrs[1] if t_ptrs is not None else None)
         refine = (q, self.ent, refinement[0], refinement[1]) if refinement is not None else None
-        self.ops.rank_rows(scores, B, self.lo, part_a, part_b, f_col, t_col, counts[0], counts[1], refine=refine)
+        fused = getattr(self.ops, "rank_codes", None)
+        codes = fused(q, wa, B, (o, true_o), (s, true_s), refinement, self.lo) if fused is not None else None
+        if codes is not None:  # the scores are compared inside the contraction: no score block
+            self.ops.rank_rows(None, B, self.lo, part_a, part_b, f_col, t_col, counts[0], counts[1], refine=refine,
+                               codes=codes, m=E_k)
+        else:
+            buf = torch.empty(2 * B, (E_k + 3) // 4 * 4, device=dev, dtype=torch.float32)
+            scores = self.ops.score(q, wa, out=buf[:, :E_k])
+            self.ops.rank_rows(scores, B, self.lo, part_a, part_b, f_col, t_col, counts[0], counts[1], refine=refine)
         all_reduce(counts, group=self.group)
         return counts
 

@@ -1,7 +1,7 @@
 """Where an EntityRankingJob run spends its wall time: issuing the batch loop (host), the
 device finishing it, and the metric arithmetic after it.
 
-    python scripts/dev/eval_phases.py [streams] [head_and_tail 0|1]
+    python scripts/dev/eval_phases.py [streams] [head_and_tail 0|1] [fused_rank 0|1]
 """
 import os
 import sys
@@ -33,6 +33,8 @@ def main():
     c.set("eval.split", "test")
     c.set("eval.batch_size", 1024)
     c.set("entity_ranking.metrics_per.head_and_tail", hat)
+    if len(sys.argv) > 3:
+        c.set("engine.fused_rank", bool(int(sys.argv[3])))
     ds = Dataset.synthetic(c, "fb15k-237", seed=0)
     torch.manual_seed(0)
     model = KgeModel.create(c, ds)

@@ -308,3 +308,117 @@ def test_refined_eval_job_every_model_vs_exact_scoring(model, dim, chunk):
             delta = abs(int(job.ranks[key][i]) - int(exp[i]))
             assert np.sort(dist)[delta - 1] <= 1e-6, (key, i, delta, np.sort(dist)[:delta])
     assert moved <= 0.02 * sum(len(v) for v in ranks.values())
+
+
+def _near_tie_tables(rng, n, m, d, copies):
+    """Query rows, candidate rows and true columns with `copies` near-copies of every query's
+    true row at relative distances 1e-7 .. 1e-5 (scores the bf16x3 contraction mis-orders)."""
+    q = (rng.standard_normal((n, d)) * 0.3).astype(np.float32)
+    t = (rng.standard_normal((m, d)) * 0.3).astype(np.float32)
+    true_idx = rng.choice(m, size=n, replace=False).astype(np.int64)
+    for i in range(n):
+        for c in range(copies):
+            j = (true_idx[i] + 1 + c * 53 + i) % m
+            if j in true_idx:
+                continue
+            eps = 10.0 ** rng.uniform(-7, -5) * rng.choice([-1.0, 1.0])
+            t[j] = (t[true_idx[i]].astype(np.float64) * (1.0 + eps) + rng.standard_normal(d) * 1e-7).astype(np.float32)
+    return q, t, true_idx
+
+
+@pytest.mark.parametrize("n_a,n_b,m,c0,d,with_test,refined", [
+    (300, 300, 3001, 0, 512, True, True),     # two 256-row tiles per batch, a ragged last entity panel
+    (100, 100, 1000, 700, 128, True, True),   # 128-row tiles; a chunk starting at column 700
+    (64, 0, 257, 0, 64, False, True),         # one batch; one column past a panel
+    (300, 211, 2050, 0, 256, True, False),    # no refinement: the bf16x3 scores compared as they are
+])
+def test_fused_rank_codes_give_the_score_block_counts(L, n_a, n_b, m, c0, d, with_test, refined):
+    """kge_score_dot_split_rank + kge_rank_rows_codes (the scores never written: compared with
+    the true score in the contraction's epilogue, 2-bit codes out) against kge_score_dot_split +
+    kge_rank_rows on the score block: the same contraction, the same band, the same exact
+    rescoring -- every count, rank and histogram must be IDENTICAL, with filter lists, a true
+    column outside the chunk, NaN / -inf true scores and near-ties in the table."""
+    rng = np.random.default_rng(n_a + 3 * m)
+    n = n_a + n_b
+    E = c0 + m + 40
+    q, t, true_local = _near_tie_tables(rng, n, m, d, 12)
+    true_idx = true_local + c0
+    true_idx[1] = c0 + m + 5  # the true entity lies outside this chunk
+    exact = (q.astype(np.float64) @ t.astype(np.float64).T).astype(np.float32)
+    true_score = exact[np.arange(n), true_local].copy()
+    true_score[2] = np.nan
+    true_score[4] = -np.inf
+    f_ptr_a, f_col_a = _csr(rng, n_a, E, 30)
+    f_ptr_b, f_col_b = _csr(rng, n_b, E, 30) if n_b else (np.zeros(1, np.int64), np.zeros(0, np.int64))
+    t_a = _minus(*_csr(rng, n_a, E, 20), f_ptr_a, f_col_a)
+    t_b = _minus(*_csr(rng, n_b, E, 20), f_ptr_b, f_col_b) if n_b else (np.zeros(1, np.int64), np.zeros(0, np.int64))
+    nrank = 3 if with_test else 2
+    qd, td = _dev(q), _dev(t)
+    hi, lo = L.split_rows(qd)
+    ti, ts = _dev(true_idx), _dev(true_score)
+    f_col = _dev(np.concatenate([f_col_a, f_col_b, np.zeros(1, np.int64)]))
+    t_col = _dev(np.concatenate([t_a[1], t_b[1], np.zeros(1, np.int64)])) if with_test else None
+    fpa, fpb = _dev(f_ptr_a), _dev(f_ptr_b + len(f_col_a))
+    tpa, tpb = (_dev(t_a[0]), _dev(t_b[0] + len(t_a[1]))) if with_test else (None, None)
+    part_a = (ti[:n_a], ts[:n_a], fpa, tpa)
+    part_b = (ti[n_a:], ts[n_a:], fpb, tpb) if n_b else None
+    tmax = L.row_norm_max(td)
+    band_rel = 1e-4
+    refine = (qd, td, band_rel, tmax) if refined else None
+    rows_per_hist = n_a if n_b == n_a else n
+
+    def run(codes_path):
+        g = torch.full((nrank * n,), -7, dtype=torch.int64, device="cuda")
+        tt = torch.full((nrank * n,), -7, dtype=torch.int64, device="cuda")
+        rk = torch.empty(nrank * n, dtype=torch.int64, device="cuda")
+        hists = torch.zeros(nrank * n // rows_per_hist, E, device="cuda")
+        kw = dict(accumulate=False, tie_handling="rounded_mean_rank", ranks=rk, hists=hists,
+                  rows_per_hist=rows_per_hist, refine=refine)
+        if codes_path:
+            band = L.rank_band(qd, band_rel, tmax) if refined else torch.full((n,), -1.0, device="cuda")
+            codes = L.score_dot_split_rank(hi, lo, td, d, n_a, (ti[:n_a], ts[:n_a]),
+                                           (ti[n_a:], ts[n_a:]) if n_b else None, band, c0)
+            assert codes.shape == (n, L.rank_codes_ld(m)) and L.lib().kge_rank_codes_ld(m) == codes.shape[1]
+            L.rank_rows(None, n_a, c0, part_a, part_b, f_col, t_col, g, tt, codes=codes, m=m, **kw)
+        else:
+            buf = torch.empty(n, (m + 3) // 4 * 4, device="cuda")
+            s = L.score_dot_split(hi, lo, td, None, d, out=buf[:, :m])
+            L.rank_rows(s, n_a, c0, part_a, part_b, f_col, t_col, g, tt, **kw)
+        torch.cuda.synchronize()
+        return g.cpu().numpy(), tt.cpu().numpy(), rk.cpu().numpy(), hists.cpu().numpy()
+
+    ref, got = run(False), run(True)
+    for a, b, name in zip(ref, got, ("greater", "ties", "ranks", "histograms")):
+        assert np.array_equal(a, b), name
+    if refined:  # and both equal exact scoring (the near-ties are there: plain bf16x3 differs)
+        exp = _oracle_counts(exact[:n_a], c0, true_idx[:n_a], np.where(np.isnan(true_score[:n_a]), -np.inf,
+                                                                         true_score[:n_a]), [])
+        assert np.array_equal(got[0][:n_a], exp[0][0])
+        assert np.array_equal(got[1][:n_a], exp[0][1])
+
+
+def test_fused_rank_codes_rows_with_thousands_of_near_ties(L):
+    """More code-3 entries in a row than the ranking kernel's near-tie ring holds: the row is
+    scanned a second time with a drain per step -- same counts as exact scoring."""
+    rng = np.random.default_rng(77)
+    n, m, d, near = 6, 6000, 128, 5000
+    q = (rng.standard_normal((n, d)) * 0.3).astype(np.float32)
+    t = (rng.standard_normal((m, d)) * 0.3).astype(np.float32)
+    true_idx = np.array([3, 100, 2000, 4000, 5999, 17], np.int64)
+    for j in range(near):  # row 0's true row copied (almost) into most of the table
+        if j not in true_idx:
+            t[j] = (t[true_idx[0]].astype(np.float64) * (1.0 + rng.uniform(-1e-6, 1e-6))).astype(np.float32)
+    exact = (q.astype(np.float64) @ t.astype(np.float64).T).astype(np.float32)
+    true_score = exact[np.arange(n), true_idx].copy()
+    exp = _oracle_counts(exact, 0, true_idx, true_score, [])
+    qd, td = _dev(q), _dev(t)
+    hi, lo = L.split_rows(qd)
+    tmax = L.row_norm_max(td)
+    ti, ts = _dev(true_idx), _dev(true_score)
+    codes = L.score_dot_split_rank(hi, lo, td, d, n, (ti, ts), None, L.rank_band(qd, 1e-4, tmax), 0)
+    g = torch.empty(n, dtype=torch.int64, device="cuda")
+    tt = torch.empty(n, dtype=torch.int64, device="cuda")
+    L.rank_rows(None, n, 0, (ti, ts, None, None), None, None, None, g, tt, accumulate=False, codes=codes, m=m,
+                refine=(qd, td, 1e-4, tmax))
+    torch.cuda.synchronize()
+    assert np.array_equal(g.cpu().numpy(), exp[0][0]) and np.array_equal(tt.cpu().numpy(), exp[0][1])
