@@ -282,6 +282,26 @@ int kge_softmax_xent_planes(float* s, int64_t lds, int64_t n, int64_t n_pad, int
 int kge_softmax_kl_planes(float* s, int64_t lds, int64_t n, int64_t n_pad, int64_t m, const int64_t* l_ptr,
                           const int64_t* l_col, float smoothing, float scale, float* loss, void* stream);
 
+/* The "bce" loss (BCEWithLogitsLoss, reduction sum: kge/util/loss.py:137-158) in the same
+ * in-place plane form: x = s + offset, label row y_j = (1 - smoothing) [j in P_i] + (smoothing > 0
+ * ? 1 / m : 0) (KvsAll's smoothed labels, train.py:715-721; they are not normalised for this
+ * loss), loss[i] = sum_j softplus(x_j) - y_j x_j, G = scale (sigmoid(x) - y) as bf16 hi / lo
+ * planes.  l_ptr NULL: one positive per row, l_col[i] (1vsAll index labels, loss.py:109-117;
+ * smoothing must be 0); else CSR positives.  Buffer requirements as kge_softmax_kl_planes. */
+int kge_bce_planes(float* s, int64_t lds, int64_t n, int64_t n_pad, int64_t m, const int64_t* l_ptr,
+                   const int64_t* l_col, float smoothing, float offset, float scale, float* loss, void* stream);
+
+/* Negative-sampling losses on a [n, k] score block whose column 0 is each row's positive and
+ * whose columns 1 .. k-1 are its negatives (the label matrix [1, 0, ..., 0] of train.py:858-871),
+ * loss[i] and g = scale * dloss/ds in one launch:
+ *   KGE_NS_MARGIN: sum_j max(0, arg - s_i0 + s_ij)  -- MarginRankingLoss(positives, negatives, +1)
+ *                  with margin = arg, reduction sum (loss.py:227-250);
+ *   KGE_NS_BCE:    BCEWithLogitsLoss(sum) of s + arg against that label row (loss.py:137-158). */
+#define KGE_NS_MARGIN 0
+#define KGE_NS_BCE 1
+int kge_ns_loss(int kind, const float* s, int64_t lds, int64_t n, int64_t k, float arg, float scale, float* loss,
+                float* g, int64_t ldg, void* stream);
+
 /* The per-row losses of a fused two-part step reduced in one launch, in a fixed order:
  * parts[0] = scale * sum loss[0 .. n_first), parts[1] = scale * sum loss[n_first .. n),
  * total[0] = parts[0] + parts[1]  (the sp_ and _po losses of train.py:1042-1053 and their sum).

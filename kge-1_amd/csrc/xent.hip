@@ -371,11 +371,23 @@ int launch(const float* s, int64_t lds, int64_t n, int64_t m, const int64_t* l_p
 // reproduces the value to 2^-16 relative, far below the 2^-16 of the products it feeds.
 typedef __bf16 kge_bf16_t;
 
-template <int NI, int NTH>
+//
+// BCE: the binary cross entropy with logits of the reference's "bce" loss (kge/util/loss.py:137-158,
+// reduction "sum") on x = s + offset against the label row y_j = (1 - eps) [j in P_i] + (eps > 0 ?
+// 1 / m : 0) (train.py:715-721: smoothed labels are NOT normalised for this loss):
+//   loss_i = sum_j softplus(x_j) - y_j x_j,     G_ij = scale (sigmoid(x_j) - y_j)
+// in the same in-place plane form; no row statistics are needed, only the three sums.
+__device__ __forceinline__ float softplus_f(float x) { return fmaxf(x, 0.f) + log1pf(__expf(-fabsf(x))); }
+__device__ __forceinline__ float sigmoid_f(float x) {
+  const float e = __expf(-fabsf(x));  // in (0, 1]: no overflow for any x
+  return x >= 0.f ? 1.f / (1.f + e) : e / (1.f + e);
+}
+
+template <int NI, int NTH, bool BCE = false>
 __global__ void __launch_bounds__(NTH) softmax_planes_kernel(float* s, int64_t lds, int n, int m,
                                                              const int64_t* __restrict__ l_ptr,
                                                              const int64_t* __restrict__ l_col, float eps, float scale,
-                                                             float* __restrict__ loss) {
+                                                             float* __restrict__ loss, float offset = 0.f) {
   __shared__ float red[3][NTH / 64];
   const int64_t row = blockIdx.x;
   float* sr = s + row * lds;
@@ -398,6 +410,69 @@ __global__ void __launch_bounds__(NTH) softmax_planes_kernel(float* s, int64_t l
   float mx, sm, rs;
   RowRegs<NI> regs;
   row_load_regs<NI, NTH>(sr, m, regs);
+  if constexpr (BCE) {
+    float sp = 0.f, sx = 0.f;  // sum of softplus(x), sum of x over this thread's elements
+#pragma unroll
+    for (int i = 0; i < NI; ++i)
+#pragma unroll
+      for (int q = 0; q < U; ++q) {
+        if (i * NTH * 4 * U + (q * NTH + tid) * 4 >= m4) continue;
+        const float4 v = regs.v[i][q];
+        const float x0 = v.x + offset, x1 = v.y + offset, x2 = v.z + offset, x3 = v.w + offset;
+        sp += (softplus_f(x0) + softplus_f(x1)) + (softplus_f(x2) + softplus_f(x3));
+        sx += (x0 + x1) + (x2 + x3);
+      }
+    if (m4 + tid < m) {
+      sp += softplus_f(tail + offset);
+      sx += tail + offset;
+    }
+    // every read of the score row is done once these sums have passed their barriers
+    sp = block_sum<NTH>(sp, red[0]);
+    sx = block_sum<NTH>(sx, red[1]);
+    ps = block_sum<NTH>(ps, red[0]);
+    const int64_t np = p1 - p0;
+    const float u = eps > 0.f ? 1.f / (float)m : 0.f;
+    if (tid == 0) loss[row] = sp - u * sx - (1.f - eps) * (ps + (float)np * offset);
+    kge_bf16_t* hi = reinterpret_cast<kge_bf16_t*>(sr);
+    kge_bf16_t* lo = hi + lds;
+    const float b = scale * u;
+#pragma unroll
+    for (int i = 0; i < NI; ++i)
+#pragma unroll
+      for (int q = 0; q < U; ++q) {
+        const int j = i * NTH * 4 * U + (q * NTH + tid) * 4;
+        if (j >= m4) continue;
+        const float4 v = regs.v[i][q];
+        const float4 gv = make_float4(scale * sigmoid_f(v.x + offset) - b, scale * sigmoid_f(v.y + offset) - b,
+                                      scale * sigmoid_f(v.z + offset) - b, scale * sigmoid_f(v.w + offset) - b);
+        bf16x4 h, l;
+        split_bf16x4_pk(gv, h, l);
+        *reinterpret_cast<bf16x4*>(hi + j) = h;
+        *reinterpret_cast<bf16x4*>(lo + j) = l;
+      }
+    if (m4 + tid < m) {
+      kge_bf16_t h, l;
+      split_bf16(scale * sigmoid_f(tail + offset) - b, h, l);
+      hi[m4 + tid] = h;
+      lo[m4 + tid] = l;
+    }
+    for (int64_t j = m + tid; j < lds; j += NTH) {  // K padding columns
+      hi[j] = (kge_bf16_t)0.f;
+      lo[j] = (kge_bf16_t)0.f;
+    }
+    __syncthreads();  // the row's planes are complete before the positives' fix-up
+    const float dpos = scale * (1.f - eps);
+    for (int64_t k = p0 + tid; k < p1; k += NTH) {
+      const int64_t c = l_col[k];
+      if (c >= 0 && c < m) {
+        kge_bf16_t h, l;
+        split_bf16(((float)hi[c] + (float)lo[c]) - dpos, h, l);
+        hi[c] = h;
+        lo[c] = l;
+      }
+    }
+    return;
+  }
   row_stats_regs<NI, NTH>(sr, m, regs, red, mx, sm, rs);
   ps = block_sum<NTH>(ps, red[0]);
 
@@ -456,26 +531,37 @@ __global__ void __launch_bounds__(NTH) softmax_planes_kernel(float* s, int64_t l
   }
 }
 
-int launch_planes(float* s, int64_t lds, int64_t n, int64_t n_pad, int64_t m, const int64_t* l_ptr,
-                  const int64_t* l_col, float eps, float scale, float* loss, hipStream_t st) {
+template <bool BCE>
+int launch_planes_t(float* s, int64_t lds, int64_t n, int64_t n_pad, int64_t m, const int64_t* l_ptr,
+                    const int64_t* l_col, float eps, float scale, float* loss, float offset, hipStream_t st) {
   const int64_t m4 = m & ~3LL;
   const dim3 grid((unsigned)n_pad);
   if (m4 <= 256 * 4 * U)
-    softmax_planes_kernel<1, 256><<<grid, dim3(256), 0, st>>>(s, lds, (int)n, (int)m, l_ptr, l_col, eps, scale, loss);
+    softmax_planes_kernel<1, 256, BCE><<<grid, dim3(256), 0, st>>>(s, lds, (int)n, (int)m, l_ptr, l_col, eps, scale,
+                                                                   loss, offset);
   else if (m4 <= 2 * 256 * 4 * U)
-    softmax_planes_kernel<2, 256><<<grid, dim3(256), 0, st>>>(s, lds, (int)n, (int)m, l_ptr, l_col, eps, scale, loss);
+    softmax_planes_kernel<2, 256, BCE><<<grid, dim3(256), 0, st>>>(s, lds, (int)n, (int)m, l_ptr, l_col, eps, scale,
+                                                                   loss, offset);
   // wider rows: 512 threads holding 2 .. 4 register slabs each (1,024-thread workgroups cap a
   // thread at 128 VGPRs, which the two-slab row does not fit: it spilled 34 of them)
   else if (m4 <= 2 * 512 * 4 * U)
-    softmax_planes_kernel<2, 512><<<grid, dim3(512), 0, st>>>(s, lds, (int)n, (int)m, l_ptr, l_col, eps, scale, loss);
+    softmax_planes_kernel<2, 512, BCE><<<grid, dim3(512), 0, st>>>(s, lds, (int)n, (int)m, l_ptr, l_col, eps, scale,
+                                                                   loss, offset);
   else if (m4 <= 3 * 512 * 4 * U)
-    softmax_planes_kernel<3, 512><<<grid, dim3(512), 0, st>>>(s, lds, (int)n, (int)m, l_ptr, l_col, eps, scale, loss);
+    softmax_planes_kernel<3, 512, BCE><<<grid, dim3(512), 0, st>>>(s, lds, (int)n, (int)m, l_ptr, l_col, eps, scale,
+                                                                   loss, offset);
   else if (m4 <= 4 * 512 * 4 * U)
-    softmax_planes_kernel<4, 512><<<grid, dim3(512), 0, st>>>(s, lds, (int)n, (int)m, l_ptr, l_col, eps, scale, loss);
+    softmax_planes_kernel<4, 512, BCE><<<grid, dim3(512), 0, st>>>(s, lds, (int)n, (int)m, l_ptr, l_col, eps, scale,
+                                                                   loss, offset);
   else
     return KGE_ERR_ARG;
   KGE_CHECK_LAUNCH();
   return 0;
+}
+
+int launch_planes(float* s, int64_t lds, int64_t n, int64_t n_pad, int64_t m, const int64_t* l_ptr,
+                  const int64_t* l_col, float eps, float scale, float* loss, hipStream_t st) {
+  return launch_planes_t<false>(s, lds, n, n_pad, m, l_ptr, l_col, eps, scale, loss, 0.f, st);
 }
 
 // parts[0] = scale * sum of loss[0 .. n_first), parts[1] = scale * sum of loss[n_first .. n),
@@ -531,6 +617,80 @@ extern "C" int kge_softmax_kl_planes(float* s, int64_t lds, int64_t n, int64_t n
   if (lds % 32 != 0 || !aligned16(s)) return KGE_ERR_ALIGN;
   if (n_pad == 0) return 0;
   return launch_planes(s, lds, n, n_pad, m, l_ptr, l_col, smoothing, scale, loss, as_stream(stream));
+}
+
+// ---------------------------------------------------------------------------------------
+// Negative-sampling losses on a [n, k] score block whose column 0 is the positive and whose other
+// columns are its negatives (train.py:858-871, 982-993), loss and gradient in one launch:
+//   KGE_NS_MARGIN  loss_i = sum_{j >= 1} max(0, arg - s_i0 + s_ij)            (loss.py:227-250:
+//                  MarginRankingLoss(positives, negatives, +1), margin = arg, reduction sum)
+//   KGE_NS_BCE     loss_i = softplus(x_i0) - x_i0 + sum_{j >= 1} softplus(x_ij), x = s + arg
+//                  (loss.py:137-158: BCEWithLogitsLoss against the label matrix [1, 0, ..., 0])
+// g = scale * dloss/ds; one workgroup per row, fixed summation order.
+namespace {
+template <int KIND>
+__global__ void __launch_bounds__(NT) ns_loss_kernel(const float* __restrict__ s, int64_t lds, int k, float arg,
+                                                     float scale, float* __restrict__ loss, float* __restrict__ g,
+                                                     int64_t ldg) {
+  __shared__ float red[2][NT / 64];
+  const int64_t row = blockIdx.x;
+  const float* sr = s + row * lds;
+  float* gr = g + row * ldg;
+  const int tid = threadIdx.x;
+  const float pos = sr[0];
+  float acc = 0.f, cnt = 0.f;
+  for (int j = 1 + tid; j < k; j += NT) {
+    const float v = sr[j];
+    if (KIND == KGE_NS_MARGIN) {
+      const float h = (v - pos) + arg;  // torch: -(x1 - x2) + margin, clamped at 0
+      const bool on = h >= 0.f;         // clamp_min's backward passes the gradient where h >= 0
+      acc += on ? h : 0.f;
+      cnt += on ? 1.f : 0.f;
+      gr[j] = on ? scale : 0.f;
+    } else {
+      const float x = v + arg;
+      acc += softplus_f(x);
+      gr[j] = scale * sigmoid_f(x);
+    }
+  }
+  acc = block_sum<NT>(acc, red[0]);
+  cnt = block_sum<NT>(cnt, red[1]);
+  if (tid == 0) {
+    if (KIND == KGE_NS_MARGIN) {
+      loss[row] = acc;
+      gr[0] = -scale * cnt;
+    } else {
+      const float x = pos + arg;
+      loss[row] = acc + softplus_f(x) - x;
+      gr[0] = -scale * sigmoid_f(-x);  // sigmoid(x) - 1 without the cancellation
+    }
+  }
+}
+}  // namespace
+
+extern "C" int kge_ns_loss(int kind, const float* s, int64_t lds, int64_t n, int64_t k, float arg, float scale,
+                           float* loss, float* g, int64_t ldg, void* stream) {
+  KGE_REQUIRE(n >= 0 && k >= 1 && k < (1LL << 31) && n < (1LL << 31) && s && loss && g && lds >= k && ldg >= k);
+  KGE_REQUIRE(kind == KGE_NS_MARGIN || kind == KGE_NS_BCE);
+  if (n == 0) return 0;
+  hipStream_t st = as_stream(stream);
+  if (kind == KGE_NS_MARGIN)
+    ns_loss_kernel<KGE_NS_MARGIN><<<dim3((unsigned)n), dim3(NT), 0, st>>>(s, lds, (int)k, arg, scale, loss, g, ldg);
+  else
+    ns_loss_kernel<KGE_NS_BCE><<<dim3((unsigned)n), dim3(NT), 0, st>>>(s, lds, (int)k, arg, scale, loss, g, ldg);
+  KGE_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int kge_bce_planes(float* s, int64_t lds, int64_t n, int64_t n_pad, int64_t m, const int64_t* l_ptr,
+                              const int64_t* l_col, float smoothing, float offset, float scale, float* loss,
+                              void* stream) {
+  KGE_REQUIRE(n >= 0 && n_pad >= n && m >= 4 && m <= kge_softmax_planes_max_columns() && n_pad < (1LL << 31));
+  KGE_REQUIRE(s && l_col && loss && lds >= m);
+  KGE_REQUIRE(smoothing >= 0.f && smoothing < 1.f && (l_ptr || smoothing == 0.f));
+  if (lds % 32 != 0 || !aligned16(s)) return KGE_ERR_ALIGN;
+  if (n_pad == 0) return 0;
+  return launch_planes_t<true>(s, lds, n, n_pad, m, l_ptr, l_col, smoothing, scale, loss, offset, as_stream(stream));
 }
 
 extern "C" int kge_softmax_xent(const float* s, int64_t lds, int64_t n, int64_t m, const int64_t* labels,

@@ -90,6 +90,8 @@ SIGNATURES = {
     "kge_score_dot_bwd_q_planes": ([_P, _P, _I64, _P, _I64, _I64, _I64, _I, _P, _I64, _I, _P, _P, _I64, _P], _I),
     "kge_score_dot_bwd_t_planes": ([_P, _P, _I64, _P, _P, _I64, _I64, _I64, _I, _P, _I64, _I, _P, _P], _I),
     "kge_loss_sums": ([_P, _I64, _I64, _P, _F, _P, _P, _P], _I),
+    "kge_bce_planes": ([_P, _I64, _I64, _I64, _I64, _P, _P, _F, _F, _F, _P, _P], _I),
+    "kge_ns_loss": ([_I, _P, _I64, _I64, _I64, _F, _F, _P, _P, _I64, _P], _I),
     "kge_prep_query_split2": ([_I, _I, _I, _I64, _P, _P, _I64, _P, _P, _I64, _P, _I64, _I, _I, _P, _I64, _P, _P, _I64,
                                _P], _I),
     "kge_prep_query_bwd2": ([_I, _I, _I, _I64, _P, _P, _I64, _P, _P, _I64, _P, _I64, _I, _I, _P, _I64, _P, _I64, _P,
@@ -745,9 +747,10 @@ def planes_ok(m: int) -> bool:
     return 4 <= m <= lib().kge_softmax_planes_max_columns()
 
 
-def softmax_planes(buf, n, m, labels, l_ptr, smoothing, scale) -> tuple:
+def softmax_planes(buf, n, m, labels, l_ptr, smoothing, scale, loss_kind="kl", offset=0.0) -> tuple:
     """Per-row losses [n] of the scores in buf[:n, :m]; the buffer is left holding the
-    gradient planes (GradPlanes).  l_ptr None: index labels (cross entropy), else CSR positives."""
+    gradient planes (GradPlanes).  l_ptr None: index labels (cross entropy), else CSR positives.
+    loss_kind "bce": binary cross entropy with logits on scores + offset instead (kge_bce_planes)."""
     require_device(buf)
     labels, l_ptr = idx64(labels), idx64(l_ptr)
     n_pad, ld = buf.shape
@@ -758,13 +761,32 @@ def softmax_planes(buf, n, m, labels, l_ptr, smoothing, scale) -> tuple:
             raise ValueError(f"l_ptr has {l_ptr.numel()} entries, expected {n + 1}")
         check_index(labels, m, "label column")
     loss = torch.empty(n, device=buf.device, dtype=torch.float32)
-    if l_ptr is None:
+    if loss_kind == "bce":
+        _check(lib().kge_bce_planes(ptr(buf), ld, n, n_pad, m, ptr(l_ptr), ptr(labels), float(smoothing),
+                                    float(offset), float(scale), ptr(loss), stream()), "kge_bce_planes")
+    elif loss_kind != "kl":
+        raise ValueError(f"softmax_planes: unknown loss kind {loss_kind!r}")
+    elif l_ptr is None:
         _check(lib().kge_softmax_xent_planes(ptr(buf), ld, n, n_pad, m, ptr(labels), float(scale), ptr(loss),
                                              stream()), "kge_softmax_xent_planes")
     else:
         _check(lib().kge_softmax_kl_planes(ptr(buf), ld, n, n_pad, m, ptr(l_ptr), ptr(labels), float(smoothing),
                                            float(scale), ptr(loss), stream()), "kge_softmax_kl_planes")
     return loss, GradPlanes(buf, n, m)
+
+
+NS_MARGIN, NS_BCE = 0, 1
+
+
+def ns_loss(kind, s, arg, scale):
+    """kge_ns_loss on a [n, k] block (column 0 the positive): (per-row losses [n], g [n, k])."""
+    require_device(s)
+    n, k = s.shape
+    loss = torch.empty(n, device=s.device, dtype=torch.float32)
+    g = torch.empty(n, k, device=s.device, dtype=torch.float32)
+    _check(lib().kge_ns_loss(int(kind), ptr(s), rows(s), n, k, float(arg), float(scale), ptr(loss), ptr(g), rows(g),
+                             stream()), "kge_ns_loss")
+    return loss, g
 
 
 def loss_sums(loss_rows, n_first, scale, n_first_dev=None):

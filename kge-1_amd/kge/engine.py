@@ -15,6 +15,7 @@ accumulated into ONE dense buffer, the layout torch's embedding_dense_backward p
 from __future__ import annotations
 
 import contextlib
+import threading
 from typing import Optional
 
 import torch
@@ -211,6 +212,31 @@ class _ScoreXent(torch.autograd.Function):
         return None, None, None, None, d_ent, None, d_rel, None, d_tab, None, None, None, None, None
 
 
+class _FusedLoss(threading.local):
+    """Which loss the fused passes of this thread compute: "kl" (softmax cross entropy / KL, the
+    default) or "bce" (binary cross entropy with logits on scores + offset)."""
+    kind = "kl"
+    offset = 0.0
+
+
+_LOSS = _FusedLoss()
+
+
+@contextlib.contextmanager
+def fused_loss_kind(kind: str, offset: float = 0.0):
+    """Inside, the fused losses (score_all_xent and its relatives) compute ``kind`` instead of the
+    softmax loss.  "bce" is served by the plane-fed pass only: where that does not apply the
+    fused entry points return None and the caller scores and applies the loss unfused."""
+    if kind not in ("kl", "bce"):
+        raise ValueError(f"fused loss kind {kind!r}")
+    prev = (_LOSS.kind, _LOSS.offset)
+    _LOSS.kind, _LOSS.offset = kind, float(offset)
+    try:
+        yield
+    finally:
+        _LOSS.kind, _LOSS.offset = prev
+
+
 class StackedQueries:
     """Two query batches stacked by rows: rows [0, n_a) are direction dir_a queries, rows
     [n_a, n) direction dir_b queries; eidx / ridx index all n rows.  n_a_dev (an int64 device
@@ -265,7 +291,7 @@ class _ScoreXentPlanes(torch.autograd.Function):
         L.prep_query_split2(kind, sq.dir_a, sq.dir_b, sq.n_a, sq.n_a_dev, ent, sq.eidx, rel, sq.ridx, d_e, d_r,
                             out=(None, hi[:n], lo[:n]))
         _timed(L.score_dot_split, hi[:n], lo[:n], tab_w, None, qw, out=buf[:n, :m])
-        loss_rows, _ = L.softmax_planes(buf, n, m, labels, l_ptr, smoothing, scale)
+        loss_rows, _ = L.softmax_planes(buf, n, m, labels, l_ptr, smoothing, scale, _LOSS.kind, _LOSS.offset)
         ctx.meta = (kind, n, m, d_e, d_r, sq.dir_a, sq.dir_b, sq.n_a, sq.n_a_dev is not None, tab is None)
         ctx.save_for_backward(ent, rel, hi, lo, buf, sq.eidx, sq.ridx,
                               sq.n_a_dev if sq.n_a_dev is not None else sq.eidx.new_empty(0), cand)
@@ -347,6 +373,8 @@ def score_all_xent(kind: int, direction: int, precision: int, l_norm: float, ent
         total, _ = _ScoreXentPlanes.apply(kind, ent, rel, StackedQueries.of([(direction, rows, rows)]),
                                           L.idx64(labels), L.idx64(l_ptr), float(smoothing), float(scale), tab)
         return total
+    if _LOSS.kind != "kl":
+        return None  # only the plane-fed pass computes the other losses
     return _ScoreXent.apply(kind, direction, precision, float(l_norm), ent, L.idx64(eidx), rel, L.idx64(ridx),
                             tab, L.idx64(tidx), L.idx64(labels), L.idx64(l_ptr), float(smoothing), float(scale))
 
@@ -446,6 +474,8 @@ def score_all_xent2(kind: int, precision: int, ent: torch.Tensor, rel: torch.Ten
             l_ptr = torch.cat((lptr_a[:-1], lptr_b + lptr_a[-1]))
         return _ScoreXentPlanes.apply(kind, ent, rel, StackedQueries.of([(dir_a, eidx_a, ridx_a), (dir_b, eidx_b, ridx_b)]),
                                       lab, l_ptr, float(smoothing), float(scale))
+    if _LOSS.kind != "kl":
+        return None
     return _ScoreXent2.apply(kind, precision, ent, rel, dir_a, L.idx64(eidx_a), L.idx64(ridx_a), L.idx64(lab_a),
                              L.idx64(lptr_a), dir_b, L.idx64(eidx_b), L.idx64(ridx_b), L.idx64(lab_b),
                              L.idx64(lptr_b), float(smoothing), float(scale))
@@ -677,6 +707,31 @@ class _XentColumn0(torch.autograd.Function):
 def xent_column0(scores: torch.Tensor, scale: float) -> torch.Tensor:
     L.require_device(scores)
     return _XentColumn0.apply(scores, float(scale))
+
+
+class _NsLossColumn0(torch.autograd.Function):
+    """scale * sum_i loss_i of a [n, 1 + N] negative-sampling score block whose column 0 is the
+    positive, for the margin-ranking loss (loss.py:227-250) and for bce (loss.py:137-158), one
+    engine kernel for loss and gradient (kge_ns_loss) instead of torch's index / repeat chains."""
+
+    @staticmethod
+    def forward(ctx, scores, kind, arg, scale):
+        s = _rows(scores.float())
+        loss_rows, g = L.ns_loss(kind, s, arg, scale)
+        ctx.save_for_backward(g)
+        return loss_rows.sum() * scale
+
+    @staticmethod
+    def backward(ctx, grad):
+        (g,) = ctx.saved_tensors
+        return g * grad, None, None, None
+
+
+def ns_loss_column0(scores: torch.Tensor, kind: str, arg: float, scale: float) -> torch.Tensor:
+    """kind "margin_ranking" (arg = the margin) or "bce" (arg = the offset added to the scores)."""
+    L.require_device(scores)
+    return _NsLossColumn0.apply(scores, {"margin_ranking": L.NS_MARGIN, "bce": L.NS_BCE}[kind], float(arg),
+                                float(scale))
 
 
 def score_spo_emb(kind: int, l_norm: float, s_emb, p_emb, o_emb) -> torch.Tensor:

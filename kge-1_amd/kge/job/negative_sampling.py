@@ -48,12 +48,20 @@ class TrainingJobNegativeSampling(TrainingJob):
         self._implementation = impl
         self._max_chunk_size = config.get("negative_sampling.chunk_size")
         self.type_str = "negative_sampling"
-        from ..util.loss import KLDivWithSoftmaxKgeLoss
+        from ..util.loss import BCEWithLogitsKgeLoss, KLDivWithSoftmaxKgeLoss, MarginRankingKgeLoss
 
-        #: "kl" on the one-hot label matrix of a [chunk, 1 + N] block == cross entropy against
-        #: column 0: one engine kernel (engine.xent_column0) instead of torch's loss chain
-        self._fused_loss = (type(self.loss) is KLDivWithSoftmaxKgeLoss and bool(config.get("engine.fused_loss"))
-                            and str(self.device).startswith("cuda"))
+        #: The loss of a [chunk, 1 + N] block whose column 0 is the positive as ONE engine kernel
+        #: (loss + gradient) instead of torch's loss chain: "kl" on the one-hot label matrix is the
+        #: cross entropy against column 0 (engine.xent_column0); "margin_ranking" and "bce" (sum)
+        #: run kge_ns_loss (engine.ns_loss_column0).  None: kge.util.loss on the score block.
+        self._fused_loss = None
+        if bool(config.get("engine.fused_loss")) and str(self.device).startswith("cuda"):
+            if type(self.loss) is KLDivWithSoftmaxKgeLoss:
+                self._fused_loss = ("kl", 0.0)
+            elif type(self.loss) is MarginRankingKgeLoss:
+                self._fused_loss = ("margin_ranking", float(self.loss._loss.margin))
+            elif type(self.loss) is BCEWithLogitsKgeLoss and not self.loss._mean:
+                self._fused_loss = ("bce", float(self.loss._offset))
 
     def _prepare(self):
         super()._prepare()
@@ -125,10 +133,12 @@ class TrainingJobNegativeSampling(TrainingJob):
                     labels[:, 0] = 1.0
                 fwd -= time.time()
                 scores = self._scores(tr, slot, negs[slot][lo:hi])
-                if self._fused_loss and scores.is_cuda:
+                if self._fused_loss is not None and scores.is_cuda:
                     from .. import engine
 
-                    loss = engine.xent_column0(scores, 1.0 / bs)
+                    kind, arg = self._fused_loss
+                    loss = (engine.xent_column0(scores, 1.0 / bs) if kind == "kl"
+                            else engine.ns_loss_column0(scores, kind, arg, 1.0 / bs))
                 else:
                     loss = self.loss(scores, labels, num_negatives=ns) / bs
                 fwd += time.time()

@@ -19,7 +19,7 @@ import torch
 
 from .. import _lib
 from ..model.kge_model import KgeModel
-from ..util.loss import KgeLoss, KLDivWithSoftmaxKgeLoss
+from ..util.loss import BCEWithLogitsKgeLoss, KgeLoss, KLDivWithSoftmaxKgeLoss
 from ..util.optimizer import KgeLRScheduler, KgeOptimizer
 from .job import Job
 
@@ -255,8 +255,27 @@ class TrainingJob(Job):
     def _collate(self, example_ids):
         raise NotImplementedError
 
+    def _fused_loss_kind(self):
+        """(kind, offset) of the loss the engine fuses into the scoring pass for this job --
+        ("kl", 0.0) for train.loss kl (softmax cross entropy / KL), ("bce", loss_arg) for
+        train.loss bce (sum reduction; loss.py:137-158) -- or None: engine.fused_loss is off or
+        the loss is computed by kge.util.loss on the score matrix."""
+        if not self.config.get("engine.fused_loss"):
+            return None
+        if isinstance(self.loss, KLDivWithSoftmaxKgeLoss):
+            return ("kl", 0.0)
+        if type(self.loss) is BCEWithLogitsKgeLoss and not self.loss._mean:
+            return ("bce", float(self.loss._offset))
+        return None
+
     def process_batch(self, batch_index, batch) -> "TrainingJob._ProcessBatchResult":
-        return self._process_batch(batch_index, batch)
+        kind = self._fused_loss_kind()
+        if kind is None or kind[0] == "kl":
+            return self._process_batch(batch_index, batch)
+        from .. import engine
+
+        with engine.fused_loss_kind(*kind):  # the fused passes inside compute this loss
+            return self._process_batch(batch_index, batch)
 
     def train_step(self, batch_index, batch):
         """One optimizer step on one batch -- zero_grad, forward/backward (process_batch),
@@ -515,8 +534,7 @@ class TrainingJob1vsAll(TrainingJob):
             return
         opt = self.optimizer
         self._graph_step = None  # decided anew by every _prepare
-        if (self.config.get("engine.graph_step") and self.config.get("engine.fused_loss")
-                and isinstance(self.loss, KLDivWithSoftmaxKgeLoss)
+        if (self.config.get("engine.graph_step") and self._fused_loss_kind() is not None
                 and torch.device(self.device).type == "cuda"
                 and hasattr(opt, "graph_safe") and opt.graph_safe()
                 and not self.pre_batch_hooks  # e.g. the embedding normaliser re-creates the weights
@@ -552,7 +570,7 @@ class TrainingJob1vsAll(TrainingJob):
         s_, o_, s2_, p_, p2_ = cols[0], cols[1], cols[2], cols[3], cols[4]
         bs = cols.shape[1]
         t += time.time()
-        fused = self.config.get("engine.fused_loss") and isinstance(self.loss, KLDivWithSoftmaxKgeLoss)
+        fused = self._fused_loss_kind() is not None
         fwd = -time.time()
         both = None
         if fused:
@@ -766,8 +784,7 @@ class TrainingJobKvsAll(TrainingJob):
 
         opt = self.optimizer
         self._graph_step = None  # decided anew by every _prepare
-        if (self.config.get("engine.graph_step") and self.config.get("engine.fused_loss")
-                and isinstance(self.loss, KLDivWithSoftmaxKgeLoss)
+        if (self.config.get("engine.graph_step") and self._fused_loss_kind() is not None
                 and 1 <= len(self.query_types) <= 2 and entity_targets
                 and torch.device(self.device).type == "cuda"
                 and hasattr(opt, "graph_safe") and opt.graph_safe()
@@ -908,7 +925,7 @@ class TrainingJobKvsAll(TrainingJob):
         t += time.time()
         fwd = bwd = 0.0
         total = None
-        fused = self.config.get("engine.fused_loss") and isinstance(self.loss, KLDivWithSoftmaxKgeLoss)
+        fused = self._fused_loss_kind() is not None
         if fused and len(self.query_types) == 2 and "s_o" not in self.query_types:
             res = self._process_batch_fused2(ex, bs)
             if res is not None:

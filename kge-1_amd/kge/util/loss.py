@@ -40,7 +40,8 @@ class KgeLoss:
         if labels.dim() == 2:
             return labels
         x = torch.zeros(scores.shape, dtype=torch.float, device=scores.device)
-        x[range(len(scores)), labels] = 1.0
+        # scatter on the device: no host index list, so the step can be recorded into a graph
+        x.scatter_(1, labels.view(-1, 1).to(device=scores.device, dtype=torch.int64), 1.0)
         return x
 
     def _labels_as_indexes(self, scores, labels):

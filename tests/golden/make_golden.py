@@ -537,6 +537,49 @@ def gen_train_fixture():
     return fn
 
 
+def gen_1vsall_bce_fixture():
+    """Three 1vsAll batches with train.loss bce (BCEWithLogitsLoss(sum) against the one-hot label
+    matrix the index labels turn into, loss.py:109-117, 137-158): ComplEx-32, Adagrad."""
+    from kge.job import TrainingJob
+
+    E, R, splits = make_dataset_splits()
+    folder = os.path.join(TMP, "ds_train_bce")
+    write_dataset(folder, E, R, splits)
+    dim, bs, nb = 32, 128, 3
+    config = ds_config("complex", dim, folder, E, R, {
+        "train.type": "1vsAll", "train.optimizer": "Adagrad", "train.optimizer_args": {"lr": 0.2},
+        "train.loss": "bce", "train.batch_size": bs})
+    ds = Dataset.create(config, folder=folder)
+    gen = torch.Generator().manual_seed(15)
+    ent = torch.randn(E, dim, generator=gen) * 0.1
+    rel = torch.randn(R, dim, generator=gen) * 0.1
+    job = TrainingJob.create(config, ds)
+    set_tables(job.model, ent, rel)
+    job._prepare()
+    perm = torch.randperm(len(splits["train"]), generator=gen)[:nb * bs]
+    train = torch.from_numpy(splits["train"])
+    losses, batches, g0 = [], [], None
+    for b in range(nb):
+        batch = train[perm[b * bs:(b + 1) * bs]].long()
+        batches.append(batch.numpy())
+        job.optimizer.zero_grad()
+        res = job._process_batch(b, {"triples": batch})
+        if b == 0:
+            g0 = (job.model._entity_embedder._embeddings.weight.grad.clone().numpy(),
+                  job.model._relation_embedder._embeddings.weight.grad.clone().numpy())
+        job.optimizer.step()
+        losses.append(res.avg_loss)
+    fn = os.path.join(OUT, "train1vsall_bce_complex.npz")
+    np.savez_compressed(
+        fn, ent0=ent.numpy(), rel0=rel.numpy(), batches=np.stack(batches), losses=np.array(losses, dtype=np.float64),
+        g_ent_0=g0[0], g_rel_0=g0[1],
+        ent1=job.model._entity_embedder._embeddings.weight.detach().numpy(),
+        rel1=job.model._relation_embedder._embeddings.weight.detach().numpy(),
+        meta=np.array(json.dumps(dict(E=E, R=R, dim=dim, lr=0.2, optimizer="Adagrad", loss="bce", batch_size=bs,
+                                      torch=torch.__version__))))
+    return fn
+
+
 def synth_triples_fast(rng, E, R, n):
     """Unique random triples, skewed entity distribution, vectorised (large E)."""
     w = 1.0 / np.arange(1, E + 1) ** 0.6
@@ -595,7 +638,7 @@ def gen_eval_fullsize():
     return fn
 
 
-def gen_kvsall_fixture(with_so=False):
+def gen_kvsall_fixture(with_so=False, loss="kl", loss_arg=float("nan")):
     from kge.job import TrainingJob
 
     E, R, splits = make_dataset_splits()
@@ -604,7 +647,7 @@ def gen_kvsall_fixture(with_so=False):
     dim, bs, nb = 32, 64, 3
     config = ds_config("distmult", dim, folder, E, R, {
         "train.type": "KvsAll", "train.optimizer": "Adagrad", "train.optimizer_args": {"lr": 0.2},
-        "train.loss": "kl", "train.batch_size": bs, "KvsAll.label_smoothing": 0.1,
+        "train.loss": loss, "train.loss_arg": loss_arg, "train.batch_size": bs, "KvsAll.label_smoothing": 0.1,
         "KvsAll.query_types.s_o": with_so,
     })
     ds = Dataset.create(config, folder=folder)
@@ -637,14 +680,16 @@ def gen_kvsall_fixture(with_so=False):
     out["ent1"] = job.model._entity_embedder._embeddings.weight.detach().numpy()
     out["rel1"] = job.model._relation_embedder._embeddings.weight.detach().numpy()
     out["meta"] = np.array(json.dumps(dict(
-        E=E, R=R, dim=dim, model="distmult", lr=0.2, optimizer="Adagrad", loss="kl", batch_size=bs,
+        E=E, R=R, dim=dim, model="distmult", lr=0.2, optimizer="Adagrad", loss=loss,
+        loss_arg=None if math.isnan(loss_arg) else loss_arg, batch_size=bs,
         label_smoothing=0.1, query_types=job.query_types, num_batches=nb, torch=torch.__version__)))
-    fn = os.path.join(OUT, "train_kvsall_so_distmult.npz" if with_so else "train_kvsall_distmult.npz")
+    tag = "" if loss == "kl" else "_" + loss
+    fn = os.path.join(OUT, f"train_kvsall{'_so' if with_so else ''}{tag}_distmult.npz")
     np.savez_compressed(fn, **out)
     return fn
 
 
-def gen_ns_fixture(model_key):
+def gen_ns_fixture(model_key, loss="kl", loss_arg=float("nan")):
     from kge.job import TrainingJob
 
     E, R, splits = make_dataset_splits()
@@ -653,7 +698,8 @@ def gen_ns_fixture(model_key):
     dim, bs, nb, nneg = 32, 64, 2, 8
     config = ds_config(model_key, dim, folder, E, R, {
         "train.type": "negative_sampling", "train.optimizer": "Adagrad", "train.optimizer_args": {"lr": 0.1},
-        "train.loss": "kl", "train.batch_size": bs, "negative_sampling.num_samples.s": nneg,
+        "train.loss": loss, "train.loss_arg": loss_arg, "train.batch_size": bs,
+        "negative_sampling.num_samples.s": nneg,
         "negative_sampling.num_samples.o": -1, "negative_sampling.num_samples.p": 0,
         "negative_sampling.implementation": "triple", "negative_sampling.filtering.implementation": "standard",
     })
@@ -690,11 +736,11 @@ def gen_ns_fixture(model_key):
     out["ent1"] = job.model._entity_embedder._embeddings.weight.detach().numpy()
     out["rel1"] = job.model._relation_embedder._embeddings.weight.detach().numpy()
     out["meta"] = np.array(json.dumps(dict(
-        E=E, R=R, dim=dim, d_e=d_e, d_r=d_r, model=model_key, lr=0.1, optimizer="Adagrad", loss="kl",
-        batch_size=bs, num_negatives=nneg, implementation="triple", num_batches=nb,
+        E=E, R=R, dim=dim, d_e=d_e, d_r=d_r, model=model_key, lr=0.1, optimizer="Adagrad", loss=loss,
+        loss_arg=None if math.isnan(loss_arg) else loss_arg, batch_size=bs, num_negatives=nneg, implementation="triple", num_batches=nb,
         l_norm=config.get(model_key + ".l_norm") if model_key in ("rotate", "transe") else None,
         torch=torch.__version__)))
-    fn = os.path.join(OUT, f"train_ns_{model_key}.npz")
+    fn = os.path.join(OUT, f"train_ns_{model_key}{'' if loss == 'kl' else '_' + loss}.npz")
     np.savez_compressed(fn, **out)
     return fn
 
@@ -994,6 +1040,10 @@ def main():
              "kvsall_so": lambda: gen_kvsall_fixture(with_so=True),
              "ns_rotate": lambda: gen_ns_fixture("rotate"), "ns_complex": lambda: gen_ns_fixture("complex"),
              "toy": gen_toy_fixture, "score_so": gen_score_so_fixture, "eval_metrics_per": gen_eval_metrics_per,
+             "kvsall_bce": lambda: gen_kvsall_fixture(loss="bce", loss_arg=0.5),
+             "ns_complex_margin": lambda: gen_ns_fixture("complex", "margin_ranking", 2.0),
+             "ns_rotate_bce": lambda: gen_ns_fixture("rotate", "bce", -3.0),
+             "onevsall_bce": gen_1vsall_bce_fixture,
              "penalties": gen_penalty_fixture, "eval_rescal128": gen_eval_rescal128,
              "train_large": gen_train_fixture_large}
     seed = 3000
