@@ -134,7 +134,8 @@ __global__ void __launch_bounds__(512, 1) mfma_lds_kernel(int stages, float* __r
 // only -- 8 x 8 accumulators, acc += |q - t| as v_sub_f32 + v_add_f32 with an |.| source
 // modifier (128 instructions per iteration, + 16 that keep the operands changing);
 // 1: 64 independent v_fma_f32 chains; 2: the L1 loop with its operands read from a resident LDS
-// image the way the distance kernel reads them (4 ds_read_b128 per 128 VALU instructions).
+// image the way the distance kernel reads them (4 ds_read_b128 per 128 VALU instructions);
+// 3 / 4: the three-instruction L1 distance-backward update with the pair weight in an SGPR.
 template <int VARIANT>
 __global__ void __launch_bounds__(256) valu_kernel(int iters, float* __restrict__ out) {
   __shared__ __attribute__((aligned(16))) float img[2][16 * 132];
@@ -146,6 +147,15 @@ __global__ void __launch_bounds__(256) valu_kernel(int iters, float* __restrict_
   for (int a = 0; a < 8; ++a)
 #pragma unroll
     for (int b = 0; b < 8; ++b) acc[a][b] = 0.f;
+  if constexpr (VARIANT == 3 || VARIANT == 4) {
+#pragma unroll
+    for (int a = 0; a < 8; ++a)
+#pragma unroll
+      for (int b = 4; b < 8; ++b) {
+        acc[a][b] = (float)(mix(tid * 64 + a * 8 + b) & 0xff) * 0.01f;
+        asm volatile("" : "+v"(acc[a][b]));
+      }
+  }
   float q[8], t[8];
 #pragma unroll
   for (int a = 0; a < 8; ++a) {
@@ -163,6 +173,36 @@ __global__ void __launch_bounds__(256) valu_kernel(int iters, float* __restrict_
       const float4 t1 = *reinterpret_cast<const float4*>(tb + 64 + 4 * tx);
       q[0] = q0.x; q[1] = q0.y; q[2] = q0.z; q[3] = q0.w; q[4] = q1.x; q[5] = q1.y; q[6] = q1.z; q[7] = q1.w;
       t[0] = t0.x; t[1] = t0.y; t[2] = t0.z; t[3] = t0.w; t[4] = t1.x; t[5] = t1.y; t[6] = t1.z; t[7] = t1.w;
+    }
+    if constexpr (VARIANT == 3 || VARIANT == 4) {
+      // the L1 distance-backward update: d = x - y, s = med3(d, -u, u), acc = fma(s, w, acc) with
+      // the weight w in an SGPR; u in a VGPR (3) or an SGPR (4).  8 rows x 4 components x 2 y rows
+      // per iteration = 192 instructions + 16 that keep the operands changing.  The 32 x values
+      // live in acc[a][4 ..] / xv (distinct registers, opaque to the optimiser).
+      float u = eps * 1e-10f;
+      int wbits[8];
+#pragma unroll
+      for (int a = 0; a < 8; ++a) wbits[a] = __builtin_amdgcn_readfirstlane(__float_as_int(q[a]) + it);
+      int ub = __builtin_amdgcn_readfirstlane(__float_as_int(u));
+#pragma unroll
+      for (int e = 0; e < 2; ++e)
+#pragma unroll
+        for (int a = 0; a < 8; ++a)
+#pragma unroll
+          for (int b = 0; b < 4; ++b) {
+            float dd;
+            asm("v_sub_f32 %0, %1, %2" : "=v"(dd) : "v"(acc[a][4 + b]), "v"(t[4 * e + b]));
+            float sg;
+            if constexpr (VARIANT == 3) {
+              asm("v_med3_f32 %0, %1, -%2, %2" : "=v"(sg) : "v"(dd), "v"(u));
+            } else {
+              asm("v_med3_f32 %0, %1, -%2, %2" : "=v"(sg) : "v"(dd), "s"(ub));
+            }
+            asm("v_fmac_f32 %0, %1, %2" : "+v"(acc[a][b]) : "s"(wbits[a]), "v"(sg));
+          }
+#pragma unroll
+      for (int a = 0; a < 8; ++a) t[a] -= eps;
+      continue;
     }
     if constexpr (VARIANT == 1) {
 #pragma unroll
@@ -198,6 +238,55 @@ __global__ void __launch_bounds__(256) valu_kernel(int iters, float* __restrict_
   out[1 + blockIdx.x * 256 + tid] = s;
 }
 
+// Issue cost of single VALU instruction forms: 32 independent destination registers, the same
+// instruction 32 times per iteration, operands in registers (a: 32 VGPRs, b / c: VGPRs, s: SGPR).
+#define KGE_OP_LOOP(STR)                                                            \
+  for (int it = 0; it < iters; ++it) {                                              \
+    _Pragma("unroll") for (int i = 0; i < 32; ++i)                                  \
+        asm volatile(STR : "+v"(a[i]) : "v"(b[i & 7]), "v"(c[i & 3]), "s"(sv), "v"(a[(i + 5) & 31])); \
+  }
+
+template <int OP>
+__global__ void __launch_bounds__(256) valu_op_kernel(int iters, float* __restrict__ out) {
+  const int tid = threadIdx.x;
+  float a[32], b[8], c[4];
+#pragma unroll
+  for (int i = 0; i < 32; ++i) a[i] = (float)(mix(tid * 64 + i) & 0xff) * 0.01f;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) b[i] = (float)(mix(tid * 8 + i) & 0xff) * 0.02f;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) c[i] = (float)(mix(tid * 4 + i) & 0xff) * 1e-3f;
+  const int sv = __builtin_amdgcn_readfirstlane(__float_as_int(out[0] == 123.f ? 0.5f : 1.0001f));
+  if constexpr (OP == 0) { KGE_OP_LOOP("v_sub_f32 %0, %1, %0") }
+  if constexpr (OP == 1) { KGE_OP_LOOP("v_add_f32 %0, %0, |%1|") }
+  if constexpr (OP == 2) { KGE_OP_LOOP("v_fma_f32 %0, %1, %2, %0") }
+  if constexpr (OP == 3) { KGE_OP_LOOP("v_fmac_f32 %0, %1, %2") }
+  if constexpr (OP == 4) { KGE_OP_LOOP("v_fmac_f32 %0, %3, %1") }
+  if constexpr (OP == 5) { KGE_OP_LOOP("v_med3_f32 %0, %0, -%2, %2") }
+  if constexpr (OP == 6) { KGE_OP_LOOP("v_med3_f32 %0, %0, -%3, %3") }
+  if constexpr (OP == 7) { KGE_OP_LOOP("v_mul_f32 %0, %3, %0") }
+  if constexpr (OP == 8) { KGE_OP_LOOP("v_sub_f32 %0, %3, %0") }
+  if constexpr (OP == 9) { KGE_OP_LOOP("v_max_f32 %0, %1, %0") }
+  if constexpr (OP == 10) { KGE_OP_LOOP("v_and_b32 %0, %1, %0") }
+  if constexpr (OP == 11) { KGE_OP_LOOP("v_bfi_b32 %0, %3, %1, %0") }
+  if constexpr (OP == 12) { KGE_OP_LOOP("v_sad_u32 %0, %1, %2, %0") }
+  if constexpr (OP == 13) { KGE_OP_LOOP("v_cmp_lt_f32 vcc, %1, %0\n v_cndmask_b32 %0, %0, %2, vcc") }
+  if constexpr (OP == 14) { KGE_OP_LOOP("v_mul_legacy_f32 %0, %1, %0") }
+  if constexpr (OP == 15) { KGE_OP_LOOP("v_mul_f32 %0, %1, %0") }
+  if constexpr (OP == 16) { KGE_OP_LOOP("v_add_f32 %0, %1, %0") }
+  if constexpr (OP == 17) { KGE_OP_LOOP("v_sub_f32 %0, %1, %4") }
+  if constexpr (OP == 18) { KGE_OP_LOOP("v_fma_f32 %0, %1, %3, %0") }
+  if constexpr (OP == 19) { KGE_OP_LOOP("v_mul_f32 %0, 2.0, %0") }
+  if constexpr (OP == 20) { KGE_OP_LOOP("v_med3_f32 %0, %0, -1.0, 1.0") }
+  if constexpr (OP == 21) { KGE_OP_LOOP("v_xor_b32 %0, %3, %0") }
+  if constexpr (OP == 22) { KGE_OP_LOOP("v_cmp_lt_f32 vcc, %1, %0") }
+  if constexpr (OP == 23) { KGE_OP_LOOP("v_cndmask_b32 %0, %0, %2, vcc") }
+  float sum = 0.f;
+#pragma unroll
+  for (int i = 0; i < 32; ++i) sum += a[i];
+  out[1 + blockIdx.x * 256 + tid] = sum;
+}
+
 }  // namespace
 
 // VALU probe (see valu_kernel); returns the vector instructions issued per lane times the lanes
@@ -213,11 +302,71 @@ extern "C" int64_t kge_probe_valu(int variant, int waves_per_simd, int iters, fl
     case 0: valu_kernel<0><<<grid, block, 0, (hipStream_t)stream>>>(iters, out); break;
     case 1: valu_kernel<1><<<grid, block, 0, (hipStream_t)stream>>>(iters, out); break;
     case 2: valu_kernel<2><<<grid, block, 0, (hipStream_t)stream>>>(iters, out); break;
+    case 3: valu_kernel<3><<<grid, block, 0, (hipStream_t)stream>>>(iters, out); break;
+    case 4: valu_kernel<4><<<grid, block, 0, (hipStream_t)stream>>>(iters, out); break;
     default: return 0;
   }
   if (hipGetLastError() != hipSuccess) return 0;
-  const int64_t per_iter = variant == 0 ? 144 : 128;
+  const int64_t per_iter = variant == 0 ? 144 : variant >= 3 ? 200 : 128;
   return (int64_t)cus * waves_per_simd * 256 * iters * per_iter;
+}
+
+#include "probe_bank.inc"
+
+// VGPR bank probe: the same instruction 32 times per iteration on explicit registers whose
+// sources sit in different banks (register number mod 4) or in one bank.  The registers hold
+// whatever the zero-initialising moves below leave (timing only).
+template <int MODE>
+__global__ void __launch_bounds__(256) valu_bank_kernel(int iters, float* __restrict__ out) {
+  for (int it = 0; it < iters; ++it) {
+    if constexpr (MODE == 0) asm volatile(KGE_BANK_FMA_FREE ::: KGE_BANK_CLOBBERS);
+    if constexpr (MODE == 1) asm volatile(KGE_BANK_FMA_SAME ::: KGE_BANK_CLOBBERS);
+    if constexpr (MODE == 2) asm volatile(KGE_BANK_SUB_FREE ::: KGE_BANK_CLOBBERS);
+    if constexpr (MODE == 3) asm volatile(KGE_BANK_SUB_SAME ::: KGE_BANK_CLOBBERS);
+    if constexpr (MODE == 4) asm volatile(KGE_BANK_FMA_TWO_SAME ::: KGE_BANK_CLOBBERS);
+  }
+  if (iters < 0) out[threadIdx.x] = 0.f;
+}
+
+extern "C" int64_t kge_probe_valu_bank(int mode, int waves_per_simd, int iters, float* out, int64_t out_elems,
+                                       void* stream) {
+  const int cus = num_cus();
+  if (cus <= 0 || !out || iters <= 0 || waves_per_simd < 1 || waves_per_simd > 8 || out_elems < 256) return 0;
+  const dim3 grid(cus * waves_per_simd), block(256);
+  hipStream_t st = (hipStream_t)stream;
+  switch (mode) {
+    case 0: valu_bank_kernel<0><<<grid, block, 0, st>>>(iters, out); break;
+    case 1: valu_bank_kernel<1><<<grid, block, 0, st>>>(iters, out); break;
+    case 2: valu_bank_kernel<2><<<grid, block, 0, st>>>(iters, out); break;
+    case 3: valu_bank_kernel<3><<<grid, block, 0, st>>>(iters, out); break;
+    case 4: valu_bank_kernel<4><<<grid, block, 0, st>>>(iters, out); break;
+    default: return 0;
+  }
+  if (hipGetLastError() != hipSuccess) return 0;
+  return (int64_t)cus * waves_per_simd * 256 * iters * 32;
+}
+
+// Single-instruction VALU probe (see valu_op_kernel): returns the instructions issued per lane
+// times the lanes (the two-instruction form 13 counts 2), 0 on error.
+extern "C" int64_t kge_probe_valu_op(int op, int waves_per_simd, int iters, float* out, int64_t out_elems,
+                                     void* stream) {
+  const int cus = num_cus();
+  if (cus <= 0 || !out || iters <= 0 || waves_per_simd < 1 || waves_per_simd > 8 ||
+      out_elems < 1 + (int64_t)cus * waves_per_simd * 256)
+    return 0;
+  const dim3 grid(cus * waves_per_simd), block(256);
+  hipStream_t st = (hipStream_t)stream;
+  switch (op) {
+#define KGE_OP_CASE(N) case N: valu_op_kernel<N><<<grid, block, 0, st>>>(iters, out); break;
+    KGE_OP_CASE(0) KGE_OP_CASE(1) KGE_OP_CASE(2) KGE_OP_CASE(3) KGE_OP_CASE(4) KGE_OP_CASE(5) KGE_OP_CASE(6)
+    KGE_OP_CASE(7) KGE_OP_CASE(8) KGE_OP_CASE(9) KGE_OP_CASE(10) KGE_OP_CASE(11) KGE_OP_CASE(12) KGE_OP_CASE(13)
+    KGE_OP_CASE(14) KGE_OP_CASE(15) KGE_OP_CASE(16) KGE_OP_CASE(17) KGE_OP_CASE(18) KGE_OP_CASE(19) KGE_OP_CASE(20)
+    KGE_OP_CASE(21) KGE_OP_CASE(22) KGE_OP_CASE(23)
+#undef KGE_OP_CASE
+    default: return 0;
+  }
+  if (hipGetLastError() != hipSuccess) return 0;
+  return (int64_t)cus * waves_per_simd * 256 * iters * 32 * (op == 13 ? 2 : 1);
 }
 
 // LDS-fed MFMA loop (see mfma_lds_kernel); returns the floating-point operations issued.

@@ -1,14 +1,15 @@
 #!/bin/bash
-# PMC passes (kernel-trace only) over scripts/dev/dist_one.py: usage pmc_dist.sh [kind]
+# PMC passes (kernel-trace only) over scripts/dev/dist_one.py (or dist_bwd_one.py): usage pmc_dist.sh [kind] [script]
 set -o pipefail
 mkdir -p gpurun_out/pmcd
 export TMPDIR=/tmp
 K=${1:-0}
+SCRIPT=${2:-dist_one.py}
 cd /tmp
 i=0
 for set in "SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES GRBM_GUI_ACTIVE" "SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU" "SQ_INSTS_VALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS" "SQ_ACTIVE_INST_LDS SQ_LDS_IDX_ACTIVE SQ_INSTS_SALU SQ_INSTS_SMEM"; do
   i=$((i+1))
-  timeout -s KILL 90 rocprofv3 --pmc $set --kernel-trace --output-format csv -d $GRAFT_REPO_ROOT/gpurun_out/pmcd/p$i -o run -- python3 $GRAFT_REPO_ROOT/scripts/dev/dist_one.py $K 4 > /dev/null 2> $GRAFT_REPO_ROOT/gpurun_out/pmcd/err$i.txt || { echo "pass $i failed"; tail -3 $GRAFT_REPO_ROOT/gpurun_out/pmcd/err$i.txt; exit 1; }
+  timeout -s KILL 90 rocprofv3 --pmc $set --kernel-trace --output-format csv -d $GRAFT_REPO_ROOT/gpurun_out/pmcd/p$i -o run -- python3 $GRAFT_REPO_ROOT/scripts/dev/$SCRIPT $K 2 > /dev/null 2> $GRAFT_REPO_ROOT/gpurun_out/pmcd/err$i.txt || { echo "pass $i failed"; tail -3 $GRAFT_REPO_ROOT/gpurun_out/pmcd/err$i.txt; exit 1; }
 done
 cd $GRAFT_REPO_ROOT
 python3 - <<'PY'

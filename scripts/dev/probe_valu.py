@@ -9,8 +9,10 @@ lib.kge_probe_valu.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.
 cus = lib.kge_probe_cus()
 out = torch.zeros(1 + cus * 8 * 256, device="cuda")
 st = torch.cuda.current_stream().cuda_stream
-names = {0: "L1 sub + add|.| (registers)", 1: "independent v_fma_f32 chains", 2: "L1 loop fed from LDS"}
-for variant in (0, 1, 2):
+names = {0: "L1 sub + add|.| (registers)", 1: "independent v_fma_f32 chains", 2: "L1 loop fed from LDS",
+         3: "L1 bwd: sub, med3(VGPR u), fmac(SGPR w)", 4: "L1 bwd: sub, med3(SGPR u), fmac(SGPR w)"}
+only = [int(a) for a in sys.argv[1:]]
+for variant in (only or (0, 1, 2, 3, 4)):
     for w in (1, 2, 3, 4):
         iters = 20000
         ops = lib.kge_probe_valu(variant, w, iters, out.data_ptr(), out.numel(), st)  # warm-up
