@@ -322,6 +322,21 @@ class TrainingJob(Job):
         return True
 
 
+class _LazyBatch(dict):
+    """A batch dict whose entries are made by a callable the first time they are read."""
+
+    def __init__(self, **makers):
+        super().__init__()
+        self._makers = makers
+
+    def __missing__(self, key):
+        value = self[key] = self._makers[key]()
+        return value
+
+    def __contains__(self, key):
+        return dict.__contains__(self, key) or key in self._makers
+
+
 class _GraphStep:
     """A training step recorded once as a HIP graph and replayed per batch (engine.graph_step).
 
@@ -382,7 +397,9 @@ class _GraphStep:
         """The batch the penalty terms are recorded with: the triples as columns of the block."""
         cols = self._recorded_batch()["cols"]
         s_row, o_row, p_row = (TrainingJob1vsAll.INDEX_BLOCK.index(c) for c in (S, O, P))
-        return {"triples": torch.stack((cols[s_row], cols[p_row], cols[o_row]), 1)}
+        # built on first use: only weighted penalties read the triples, and the stack is a kernel
+        # that would otherwise be recorded into every step
+        return _LazyBatch(triples=lambda: torch.stack((cols[s_row], cols[p_row], cols[o_row]), 1))
 
     # ---- the step
     def run(self, batch_index, batch):

@@ -25,6 +25,13 @@ class KgeLoss:
             return BCEWithLogitsKgeLoss(config)
         if name == "bce_mean":
             return BCEWithLogitsKgeLoss(config, mean=True)
+        if name == "bce_self_adversarial":
+            # the temperature is a user option (loss.py:64-67); 1 when it is not set
+            try:
+                temperature = float(config.get("user.bce_self_adversarial_temperature"))
+            except KeyError:
+                temperature = 1.0
+            return BCEWithLogitsKgeLoss(config, mean=True, temperature=temperature)
         if name == "margin_ranking":
             return MarginRankingKgeLoss(config)
         if name == "soft_margin":
@@ -73,12 +80,15 @@ def _loss_arg(config, default):
 
 class BCEWithLogitsKgeLoss(KgeLoss):
     """bce: sum of BCE over all scores; bce_mean: (sum over positives + mean over each
-    row's negatives) / 2 (loss.py:137-189).  loss_arg = offset added to the scores."""
+    row's negatives) / 2; bce_self_adversarial: the negatives of a row averaged with the
+    softmax of their own (detached) scores times a temperature instead of uniformly
+    (loss.py:137-189).  loss_arg = offset added to the scores."""
 
-    def __init__(self, config, mean=False):
+    def __init__(self, config, mean=False, temperature=None):
         super().__init__(config)
         self._offset = _loss_arg(config, 0.0)
         self._mean = mean
+        self._temperature = temperature  # None: uniform mean over the negatives
         self._loss = torch.nn.BCEWithLogitsLoss(reduction="none" if mean else "sum")
 
     def __call__(self, scores, labels, **kwargs):
@@ -89,10 +99,17 @@ class BCEWithLogitsKgeLoss(KgeLoss):
         if not self._mean:
             return losses
         idx = self._labels_as_indexes(scores, labels)
-        losses = losses.view(scores.shape)
-        pos = losses[torch.arange(len(scores), device=scores.device), idx]
-        neg = losses.sum(dim=1) - pos
-        return (pos.sum() + neg.sum() / (scores.shape[1] - 1)) / 2.0
+        n, k = scores.shape
+        losses = losses.view(n, k)
+        pos = losses.gather(1, idx.view(-1, 1)).sum()
+        if self._temperature is None:
+            neg = (losses.sum() - pos) / (k - 1)
+        else:
+            # every row has exactly one positive: its k - 1 negatives in column order
+            keep = lm.reshape(n, k) == 0
+            neg_scores = scores.detach()[keep].view(n, k - 1)  # the adversarial weights carry no gradient
+            neg = (F.softmax(neg_scores * self._temperature, dim=1) * losses[keep].view(n, k - 1)).sum()
+        return (pos + neg) / 2.0
 
 
 class MarginRankingKgeLoss(KgeLoss):

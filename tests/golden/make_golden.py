@@ -689,7 +689,7 @@ def gen_kvsall_fixture(with_so=False, loss="kl", loss_arg=float("nan")):
     return fn
 
 
-def gen_ns_fixture(model_key, loss="kl", loss_arg=float("nan")):
+def gen_ns_fixture(model_key, loss="kl", loss_arg=float("nan"), extra=None):
     from kge.job import TrainingJob
 
     E, R, splits = make_dataset_splits()
@@ -703,6 +703,8 @@ def gen_ns_fixture(model_key, loss="kl", loss_arg=float("nan")):
         "negative_sampling.num_samples.o": -1, "negative_sampling.num_samples.p": 0,
         "negative_sampling.implementation": "triple", "negative_sampling.filtering.implementation": "standard",
     })
+    for k, v in (extra or {}).items():
+        config.set(k, v, create=True)
     ds = Dataset.create(config, folder=folder)
     gen = torch.Generator().manual_seed(13)
     job = TrainingJob.create(config, ds)
@@ -739,7 +741,7 @@ def gen_ns_fixture(model_key, loss="kl", loss_arg=float("nan")):
         E=E, R=R, dim=dim, d_e=d_e, d_r=d_r, model=model_key, lr=0.1, optimizer="Adagrad", loss=loss,
         loss_arg=None if math.isnan(loss_arg) else loss_arg, batch_size=bs, num_negatives=nneg, implementation="triple", num_batches=nb,
         l_norm=config.get(model_key + ".l_norm") if model_key in ("rotate", "transe") else None,
-        torch=torch.__version__)))
+        extra=extra or {}, torch=torch.__version__)))
     fn = os.path.join(OUT, f"train_ns_{model_key}{'' if loss == 'kl' else '_' + loss}.npz")
     np.savez_compressed(fn, **out)
     return fn
@@ -1043,6 +1045,11 @@ def main():
              "kvsall_bce": lambda: gen_kvsall_fixture(loss="bce", loss_arg=0.5),
              "ns_complex_margin": lambda: gen_ns_fixture("complex", "margin_ranking", 2.0),
              "ns_rotate_bce": lambda: gen_ns_fixture("rotate", "bce", -3.0),
+             "ns_transe_bce_self_adv": lambda: gen_ns_fixture("transe", "bce_self_adversarial", 6.0,
+                                                              {"user.bce_self_adversarial_temperature": 0.5}),
+             "ns_distmult_bce_mean": lambda: gen_ns_fixture("distmult", "bce_mean", 0.5),
+             "ns_complex_soft_margin": lambda: gen_ns_fixture("complex", "soft_margin"),
+             "ns_simple_se": lambda: gen_ns_fixture("simple", "se"),
              "onevsall_bce": gen_1vsall_bce_fixture,
              "penalties": gen_penalty_fixture, "eval_rescal128": gen_eval_rescal128,
              "train_large": gen_train_fixture_large}

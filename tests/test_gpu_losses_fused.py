@@ -243,3 +243,48 @@ def test_negative_sampling_margin_and_bce_steps_vs_reference(name, model, impl, 
     for got, want in zip(tables(job.model), (f["ent1"], f["rel1"])):
         diff = np.abs(got - want)
         assert int((diff > 2e-4).sum()) <= max(4, 1e-3 * diff.size) and float(diff.mean()) < 1e-5
+
+
+@pytest.mark.parametrize("impl", ["triple", "batch"])
+@pytest.mark.parametrize("name,model", [("train_ns_transe_bce_self_adversarial.npz", "transe"),
+                                        ("train_ns_distmult_bce_mean.npz", "distmult"),
+                                        ("train_ns_complex_soft_margin.npz", "complex"),
+                                        ("train_ns_simple_se.npz", "simple")])
+def test_negative_sampling_other_losses_vs_reference(name, model, impl):
+    """The losses the engine does not fuse -- bce_self_adversarial (temperature 0.5 from the user
+    section, offset 6; loss.py:169-187), bce_mean, soft_margin, se -- on reference negative-sampling
+    batches: torch's loss chain on the engine's score block, loss and gradients per batch."""
+    from kge.job import TrainingJob
+
+    f = np.load(os.path.join(GOLDEN, name))
+    meta = json.loads(str(f["meta"]))
+    extra = {"train.type": "negative_sampling", "train.optimizer": "Adagrad",
+             "train.optimizer_args": {"lr": meta["lr"]}, "train.batch_size": meta["batch_size"],
+             "train.loss": meta["loss"],
+             "negative_sampling.num_samples.s": meta["num_negatives"], "negative_sampling.num_samples.o": -1,
+             "negative_sampling.num_samples.p": 0, "negative_sampling.implementation": impl,
+             "engine.precision": "fp32"}
+    if meta["loss_arg"] is not None:
+        extra["train.loss_arg"] = meta["loss_arg"]
+    extra.update(meta["extra"])
+    if meta["l_norm"] is not None:
+        extra[f"{model}.l_norm"] = float(meta["l_norm"])
+    c = base_config(model, meta["dim"], meta["E"], meta["R"], extra)
+    ds = dataset_from(c, f)
+    job = TrainingJob.create(c, ds)
+    set_tables(job.model, f["ent0"], f["rel0"])
+    job._prepare()
+    assert job._fused_loss is None
+    ent_w = job.model._entity_embedder._embeddings.weight
+    rel_w = job.model._relation_embedder._embeddings.weight
+    for b in range(meta["num_batches"]):
+        neg_s, neg_o = torch.from_numpy(f[f"neg_s_{b}"]), torch.from_numpy(f[f"neg_o_{b}"])
+        batch = {"triples": torch.from_numpy(f[f"triples_{b}"]),
+                 "negative_samples": [neg_s, torch.zeros(len(neg_s), 0, dtype=torch.int64), neg_o]}
+        set_tables(job.model, f[f"ent_before_{b}"], f[f"rel_before_{b}"])
+        job.optimizer.zero_grad()
+        res = job.process_batch(b, batch)
+        assert float(res.avg_loss) == pytest.approx(float(f["losses"][b]), rel=2e-5)
+        for w, key in ((ent_w, f"g_ent_{b}"), (rel_w, f"g_rel_{b}")):
+            err = np.abs(w.grad.cpu().numpy() - f[key]).max() / np.abs(f[key]).max()
+            assert err < 2e-5, (b, key, err)

@@ -285,3 +285,45 @@ def test_dataset_relation_types_and_frequency_percentiles():
     assert ds.index("relation_types") == types and types[R - 1] == "1-1"
     assert ds.index("relations_per_type") == K.relations_per_type(types)
     assert ds.index("frequency_percentiles") == K.frequency_percentiles(t, E, R)
+
+
+def test_bce_losses_on_cpu_vs_numpy():
+    """bce / bce_mean / bce_self_adversarial (kge/util/loss.py:137-189) on a small score block with
+    the positive in column 0, against the formulas written out in float64 numpy; the temperature
+    comes from the user section of the configuration."""
+    import numpy as np
+    import torch
+
+    from kge import Config
+    from kge.util.loss import KgeLoss
+
+    rng = np.random.default_rng(3)
+    sc = rng.standard_normal((5, 7)).astype(np.float32) * 2
+    labels = np.zeros((5, 7), np.float32)
+    labels[:, 0] = 1.0
+    x = sc.astype(np.float64) + 0.75
+    bce = np.maximum(x, 0) - x * labels + np.log1p(np.exp(-np.abs(x)))
+    pos, neg = bce[:, 0], bce[:, 1:]
+    w = np.exp(x[:, 1:] * 0.5)
+    w /= w.sum(1, keepdims=True)
+    want = {"bce": bce.sum(), "bce_mean": (pos.sum() + neg.sum() / 6) / 2,
+            "bce_self_adversarial": (pos.sum() + (w * neg).sum()) / 2}
+    for name, ref in want.items():
+        c = Config()
+        c.set("train.type", "negative_sampling")
+        c.set("train.loss", name)
+        c.set("train.loss_arg", 0.75)
+        c.set("user.bce_self_adversarial_temperature", 0.5)
+        s = torch.from_numpy(sc).requires_grad_()
+        got = KgeLoss.create(c)(s, torch.from_numpy(labels), num_negatives=6)
+        assert float(got.detach()) == pytest.approx(float(ref), rel=1e-5), name
+        got.backward()
+        if name == "bce_self_adversarial":
+            # the adversarial weights are constants of the backward pass
+            sig = 1 / (1 + np.exp(-x))
+            g = np.concatenate([(sig[:, :1] - 1), w * sig[:, 1:]], 1) / 2
+            np.testing.assert_allclose(s.grad.numpy(), g, rtol=2e-5, atol=1e-7)
+    # without the user option the temperature is 1
+    c = Config()
+    c.set("train.loss", "bce_self_adversarial")
+    assert KgeLoss.create(c)._temperature == 1.0
