@@ -689,7 +689,7 @@ def gen_kvsall_fixture(with_so=False, loss="kl", loss_arg=float("nan")):
     return fn
 
 
-def gen_ns_fixture(model_key, loss="kl", loss_arg=float("nan"), extra=None):
+def gen_ns_fixture(model_key, loss="kl", loss_arg=float("nan"), extra=None, tag=""):
     from kge.job import TrainingJob
 
     E, R, splits = make_dataset_splits()
@@ -730,8 +730,9 @@ def gen_ns_fixture(model_key, loss="kl", loss_arg=float("nan"), extra=None):
         out[f"rel_before_{b}"] = job.model._relation_embedder._embeddings.weight.detach().clone().numpy()
         job.optimizer.zero_grad()
         res = job._process_batch(b, batch)
-        out[f"g_ent_{b}"] = job.model._entity_embedder._embeddings.weight.grad.detach().clone().numpy()
-        out[f"g_rel_{b}"] = job.model._relation_embedder._embeddings.weight.grad.detach().clone().numpy()
+        for key, emb in (("g_ent", job.model._entity_embedder), ("g_rel", job.model._relation_embedder)):
+            g = emb._embeddings.weight.grad.detach()
+            out[f"{key}_{b}"] = (g.to_dense() if g.is_sparse else g).clone().numpy()  # lookup_embedder.sparse
         job.optimizer.step()
         losses.append(res.avg_loss)
     out["losses"] = np.array(losses, dtype=np.float64)
@@ -742,7 +743,7 @@ def gen_ns_fixture(model_key, loss="kl", loss_arg=float("nan"), extra=None):
         loss_arg=None if math.isnan(loss_arg) else loss_arg, batch_size=bs, num_negatives=nneg, implementation="triple", num_batches=nb,
         l_norm=config.get(model_key + ".l_norm") if model_key in ("rotate", "transe") else None,
         extra=extra or {}, torch=torch.__version__)))
-    fn = os.path.join(OUT, f"train_ns_{model_key}{'' if loss == 'kl' else '_' + loss}.npz")
+    fn = os.path.join(OUT, f"train_ns_{model_key}{'' if loss == 'kl' else '_' + loss}{tag}.npz")
     np.savez_compressed(fn, **out)
     return fn
 
@@ -1050,6 +1051,8 @@ def main():
              "ns_distmult_bce_mean": lambda: gen_ns_fixture("distmult", "bce_mean", 0.5),
              "ns_complex_soft_margin": lambda: gen_ns_fixture("complex", "soft_margin"),
              "ns_simple_se": lambda: gen_ns_fixture("simple", "se"),
+             "ns_complex_sparse": lambda: gen_ns_fixture("complex", extra={"lookup_embedder.sparse": True},
+                                                         tag="_sparse"),
              "onevsall_bce": gen_1vsall_bce_fixture,
              "penalties": gen_penalty_fixture, "eval_rescal128": gen_eval_rescal128,
              "train_large": gen_train_fixture_large}

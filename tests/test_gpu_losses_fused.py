@@ -288,3 +288,52 @@ def test_negative_sampling_other_losses_vs_reference(name, model, impl):
         for w, key in ((ent_w, f"g_ent_{b}"), (rel_w, f"g_rel_{b}")):
             err = np.abs(w.grad.cpu().numpy() - f[key]).max() / np.abs(f[key]).max()
             assert err < 2e-5, (b, key, err)
+
+
+@pytest.mark.parametrize("impl", ["triple", "all", "batch"])
+def test_sparse_embeddings_negative_sampling_vs_reference(impl):
+    """lookup_embedder.sparse: True (lookup_embedder.py:30-45: the reference's nn.Embedding then hands the
+    optimizer row-sparse gradients): two reference negative-sampling batches captured with the
+    option on -- losses, densified gradients, and the tables after two Adagrad steps."""
+    from kge.job import TrainingJob
+
+    f = np.load(os.path.join(GOLDEN, "train_ns_complex_sparse.npz"))
+    meta = json.loads(str(f["meta"]))
+    extra = {"train.type": "negative_sampling", "train.optimizer": "Adagrad",
+             "train.optimizer_args": {"lr": meta["lr"]}, "train.batch_size": meta["batch_size"],
+             "negative_sampling.num_samples.s": meta["num_negatives"], "negative_sampling.num_samples.o": -1,
+             "negative_sampling.num_samples.p": 0, "negative_sampling.implementation": impl,
+             "engine.precision": "fp32"}
+    extra.update(meta["extra"])
+    assert extra["lookup_embedder.sparse"] is True
+    c = base_config("complex", meta["dim"], meta["E"], meta["R"], extra)
+    ds = dataset_from(c, f)
+    job = TrainingJob.create(c, ds)
+    assert job.model._entity_embedder.sparse and job.model._entity_embedder._embeddings.sparse
+    set_tables(job.model, f["ent0"], f["rel0"])
+    job._prepare()
+    ent_w = job.model._entity_embedder._embeddings.weight
+    rel_w = job.model._relation_embedder._embeddings.weight
+    batches = []
+    for b in range(meta["num_batches"]):
+        neg_s, neg_o = torch.from_numpy(f[f"neg_s_{b}"]), torch.from_numpy(f[f"neg_o_{b}"])
+        batch = {"triples": torch.from_numpy(f[f"triples_{b}"]),
+                 "negative_samples": [neg_s, torch.zeros(len(neg_s), 0, dtype=torch.int64), neg_o]}
+        batches.append(batch)
+        set_tables(job.model, f[f"ent_before_{b}"], f[f"rel_before_{b}"])
+        job.optimizer.zero_grad()
+        res = job.process_batch(b, batch)
+        assert float(res.avg_loss) == pytest.approx(float(f["losses"][b]), rel=2e-5)
+        for w, key in ((ent_w, f"g_ent_{b}"), (rel_w, f"g_rel_{b}")):
+            g = w.grad.to_dense() if w.grad.is_sparse else w.grad
+            err = np.abs(g.cpu().numpy() - f[key]).max() / np.abs(f[key]).max()
+            assert err < 1e-5, (b, key, err)
+    set_tables(job.model, f["ent0"], f["rel0"])
+    job.optimizer = type(job.optimizer)(job.optimizer.param_groups[0]["params"], lr=meta["lr"])
+    for b, batch in enumerate(batches):
+        job.optimizer.zero_grad()
+        job.process_batch(b, batch)
+        job.optimizer.step()
+    for got, want in zip(tables(job.model), (f["ent1"], f["rel1"])):
+        diff = np.abs(got - want)
+        assert int((diff > 2e-4).sum()) <= max(4, 1e-3 * diff.size) and float(diff.mean()) < 1e-5
