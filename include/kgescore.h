@@ -435,6 +435,14 @@ int kge_rank_hist(const int64_t* greater, const int64_t* ties, int64_t n,
                   int tie_handling, int64_t* ranks, float* hist, int64_t hist_len,
                   void* stream);
 
+/* Metrics of K rank histograms in one launch (kge/job/entity_ranking.py:553-577: mean rank,
+ * mean reciprocal rank, hits@k from a histogram of ranks).  hists: [k, e] fp32 counts with
+ * leading dimension ld, hists[i][j] = how many triples got rank j + 1.  out: [k, 3 + kmax]
+ * doubles per histogram: the count n, sum_j h[j] (j + 1), sum_j h[j] * fl32(1 / (j + 1)), then
+ * hits@1 .. hits@kmax = fl32(cumulative count / n) (0 when n = 0).  The weighted sums use the
+ * reference's fp32 operands and accumulate in fp64 in a fixed order. */
+int kge_rank_metrics(const float* hists, int64_t ld, int64_t k, int64_t e, int kmax, double* out, void* stream);
+
 /* The same for several rankings in one launch: row i counts into histogram
  * i / rows_per_hist of hist[(n / rows_per_hist) x hist_len] (the raw / filtered /
  * filtered-with-test histograms of one eval batch direction, eval.py:148-171). */

@@ -506,6 +506,58 @@ extern "C" int kge_rank_hist_multi(const int64_t* greater, const int64_t* ties, 
   return 0;
 }
 
+namespace {
+
+// One workgroup per rank histogram: out[k] = (n, sum_j h[j] (j + 1), sum_j h[j] / (j + 1),
+// hits@1 .. hits@kmax) with the operands of entity_ranking.py:553-577 -- fp32 counts, fp32 ranks,
+// fp32 reciprocals, fp32 hits quotients -- and the two weighted sums accumulated in fp64 in a
+// fixed order (thread-strided partial sums, then a tree over the 256 threads).
+__global__ void __launch_bounds__(256) rank_metrics_kernel(const float* __restrict__ hists, int64_t ld, int64_t e,
+                                                           int kmax, double* __restrict__ out) {
+  __shared__ double red[3][256];
+  const int tid = threadIdx.x;
+  const float* h = hists + (int64_t)blockIdx.x * ld;
+  double n = 0.0, s1 = 0.0, s2 = 0.0;
+  for (int64_t j = tid; j < e; j += 256) {
+    const double c = (double)h[j];
+    const float rank = (float)(j + 1);
+    n += c;
+    s1 += c * (double)rank;
+    s2 += c * (double)(1.0f / rank);
+  }
+  red[0][tid] = n, red[1][tid] = s1, red[2][tid] = s2;
+  __syncthreads();
+  for (int off = 128; off > 0; off >>= 1) {
+    if (tid < off) {
+#pragma unroll
+      for (int q = 0; q < 3; ++q) red[q][tid] += red[q][tid + off];
+    }
+    __syncthreads();
+  }
+  double* o = out + (int64_t)blockIdx.x * (3 + kmax);
+  if (tid < 3) o[tid] = red[tid][0];
+  if (tid == 0) {
+    const float nf = (float)red[0][0];  // exact: integer counts far below 2^24
+    float cum = 0.f;
+    for (int k = 0; k < kmax; ++k) {
+      if (k < e) cum += h[k];
+      o[3 + k] = nf > 0.f ? (double)(cum / nf) : 0.0;
+    }
+  }
+}
+
+}  // namespace
+
+extern "C" int kge_rank_metrics(const float* hists, int64_t ld, int64_t k, int64_t e, int kmax, double* out,
+                                void* stream) {
+  KGE_REQUIRE(k >= 0 && e > 0 && kmax >= 0 && ld >= e && (hists || k == 0) && (out || k == 0));
+  if (k == 0) return 0;
+  KGE_REQUIRE(k < (1LL << 31));
+  rank_metrics_kernel<<<dim3((unsigned)k), dim3(256), 0, as_stream(stream)>>>(hists, ld, e, kmax, out);
+  KGE_CHECK_LAUNCH();
+  return 0;
+}
+
 extern "C" int kge_row_norm_max(const float* t, int64_t ldt, int64_t m, int d, float* out, void* stream) {
   KGE_REQUIRE(m >= 0 && d > 0 && (t || m == 0) && out && ldt >= d);
   hipStream_t st = as_stream(stream);

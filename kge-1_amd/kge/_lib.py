@@ -74,6 +74,7 @@ SIGNATURES = {
     "kge_bucket_scatter": ([_P, _I64, _P, _P, _P], _I),
     "kge_stage_i64": ([_P, _P, _I64, _P], _I),
     "kge_rank_hist_multi": ([_P, _P, _I64, _I64, _I, _P, _P, _I64, _P], _I),
+    "kge_rank_metrics": ([_P, _I64, _I64, _I64, _I, _P, _P], _I),
     "kge_rank_rows": ([_P, _I64, _I64, _I64, _I64, _I64, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _P, _P,
                        _I64, _I64, _P, _I64, _P, _I64, _I, _F, _P, _P], _I),
     "kge_row_norm_max": ([_P, _I64, _I64, _I, _P, _P], _I),
@@ -797,6 +798,18 @@ def loss_sums(loss_rows, n_first, scale, n_first_dev=None):
     _check(lib().kge_loss_sums(ptr(loss_rows), loss_rows.numel(), int(n_first), ptr(n_first_dev), float(scale),
                                ptr(parts), ptr(total), stream()), "kge_loss_sums")
     return total, parts
+
+
+def rank_metrics(hists: torch.Tensor, kmax: int) -> torch.Tensor:
+    """kge_rank_metrics: [K, 3 + kmax] float64 rows (count, sum of ranks, sum of reciprocal ranks,
+    hits@1..kmax) of K fp32 rank histograms [K, E]."""
+    require_device(hists)
+    if hists.dtype != torch.float32 or hists.dim() != 2 or hists.stride(1) != 1:
+        hists = hists.float().contiguous()
+    k, e = hists.shape
+    out = torch.empty(k, 3 + kmax, device=hists.device, dtype=torch.float64)
+    _check(lib().kge_rank_metrics(ptr(hists), hists.stride(0), k, e, int(kmax), ptr(out), stream()), "kge_rank_metrics")
+    return out
 
 
 def adjacent_or_cat(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:

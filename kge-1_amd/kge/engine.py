@@ -80,9 +80,10 @@ class BatchStreams:
 
     def __enter__(self):
         if self.streams:
-            cur = torch.cuda.current_stream(self.device)
+            cur = self._caller = torch.cuda.current_stream(self.device)
             for st in self.streams:
                 st.wait_stream(cur)
+            self._turns = [_StreamTurn(st, cur) for st in self.streams]
         return self
 
     def __exit__(self, *exc):
@@ -90,12 +91,35 @@ class BatchStreams:
             cur = torch.cuda.current_stream(self.device)
             for st in self.streams:
                 cur.wait_stream(st)
+            self._turns = None
         return False
 
     def batch(self, i: int):
         if not self.streams:
             return contextlib.nullcontext()
-        return torch.cuda.stream(self.streams[i % len(self.streams)])
+        turns = getattr(self, "_turns", None)
+        if turns is None:  # used without the outer `with`: torch's own (slower) stream context
+            return torch.cuda.stream(self.streams[i % len(self.streams)])
+        return turns[i % len(turns)]
+
+
+class _StreamTurn:
+    """Makes one stream of a BatchStreams current for a block and the caller's stream current
+    again afterwards: two set_stream calls, where torch.cuda.stream() also looks the current
+    stream and device up on every entry (about 10 us per batch)."""
+
+    __slots__ = ("stream", "caller")
+
+    def __init__(self, stream, caller):
+        self.stream, self.caller = stream, caller
+
+    def __enter__(self):
+        torch.cuda.set_stream(self.stream)
+        return self.stream
+
+    def __exit__(self, *exc):
+        torch.cuda.set_stream(self.caller)
+        return False
 
 
 def dist_kind(kind: int, l_norm: float):
@@ -636,6 +660,11 @@ class _ScoreSpo(torch.autograd.Function):
 
 def score_spo(kind: int, l_norm: float, ent, sidx, rel, pidx, oidx) -> torch.Tensor:
     L.require_device(ent, rel)
+    if not torch.is_grad_enabled() or not (ent.requires_grad or rel.requires_grad):
+        # evaluation: no autograd node to build (about 10 us of host time per call)
+        ent, rel = _rows(ent), _rows(rel)
+        return L.score_spo(kind, float(l_norm), ent, L.idx64(sidx), rel, L.idx64(pidx), L.idx64(oidx), ent.shape[1],
+                           rel.shape[1])
     return _ScoreSpo.apply(kind, float(l_norm), ent, L.idx64(sidx), rel, L.idx64(pidx), L.idx64(oidx))
 
 

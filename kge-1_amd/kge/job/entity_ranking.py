@@ -455,22 +455,26 @@ class EntityRankingJob(EvaluationJob):
 
     def _compute_metrics_stacked(self, rank_hists: torch.Tensor, suffixes: List[str]) -> Dict[str, float]:
         """entity_ranking.py:553-577 for a stack of rank histograms [K, E] (one suffix each):
-        mean rank, mean reciprocal rank and hits@k of every histogram in one device pass and ONE
-        device-to-host copy instead of three host round trips per histogram.  The operands are
+        mean rank, mean reciprocal rank and hits@k of every histogram in one launch
+        (kge_rank_metrics) and ONE device-to-host copy instead of three host round trips per
+        histogram (host histograms, e.g. of a CPU rehearsal, take the same sums through torch).  The operands are
         the reference's fp32 ones (counts, ranks, fp32 reciprocals, fp32 hits quotients); the two
         weighted sums accumulate in fp64, which differs from an fp32 sum only by that sum's own
         rounding."""
         E = self.dataset.num_entities()
         K = rank_hists.shape[0]
         kmax = max(self.hits_at_k_s)
-        if self._rank_weights is None or self._rank_weights.device != rank_hists.device:
-            ranks = torch.arange(1, E + 1, device=rank_hists.device).float()
-            self._rank_weights = torch.stack([ranks.double(), (1.0 / ranks).double()])  # fp32 values
-        h64 = rank_hists.double()
-        n = rank_hists.sum(1, keepdim=True)  # exact: integer counts far below 2^24
-        hits = torch.cumsum(rank_hists[:, :kmax], dim=1) / n  # fp32 quotients
-        table = torch.cat([n.double(), (h64 * self._rank_weights[0]).sum(1, keepdim=True),
-                           (h64 * self._rank_weights[1]).sum(1, keepdim=True), hits.double()], dim=1).tolist()
+        if rank_hists.is_cuda:
+            table = _lib.rank_metrics(rank_hists, kmax).tolist()  # one launch, one copy
+        else:
+            if self._rank_weights is None or self._rank_weights.device != rank_hists.device:
+                ranks = torch.arange(1, E + 1, device=rank_hists.device).float()
+                self._rank_weights = torch.stack([ranks.double(), (1.0 / ranks).double()])  # fp32 values
+            h64 = rank_hists.double()
+            n = rank_hists.sum(1, keepdim=True)  # exact: integer counts far below 2^24
+            hits = torch.cumsum(rank_hists[:, :kmax], dim=1) / n  # fp32 quotients
+            table = torch.cat([n.double(), (h64 * self._rank_weights[0]).sum(1, keepdim=True),
+                               (h64 * self._rank_weights[1]).sum(1, keepdim=True), hits.double()], dim=1).tolist()
         metrics = {}
         for row, suffix in zip(table, suffixes):
             cnt = row[0]

@@ -422,3 +422,32 @@ def test_fused_rank_codes_rows_with_thousands_of_near_ties(L):
                 refine=(qd, td, 1e-4, tmax))
     torch.cuda.synchronize()
     assert np.array_equal(g.cpu().numpy(), exp[0][0]) and np.array_equal(tt.cpu().numpy(), exp[0][1])
+
+
+@pytest.mark.parametrize("k,e,kmax", [(3, 14541, 10), (1, 5, 10), (40, 700, 3)])
+def test_rank_metrics_vs_torch_formula(k, e, kmax):
+    """kge_rank_metrics against the stacked torch arithmetic of entity_ranking.py:553-577 (fp32
+    operands, fp64 sums): counts and hits are exact, the weighted sums agree to 1e-12."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from kge import _lib
+
+    g = torch.Generator().manual_seed(k * e)
+    h = torch.randint(0, 50, (k, e), generator=g).float()
+    h[0] = 0 if k > 1 else h[0]  # an empty histogram: every metric 0 on the host side
+    hd = h.cuda()
+    got = _lib.rank_metrics(hd, kmax).cpu()
+    ranks = torch.arange(1, e + 1).float()
+    n = h.sum(1, keepdim=True)
+    want_s1 = (h.double() * ranks.double()).sum(1)
+    want_s2 = (h.double() * (1.0 / ranks).double()).sum(1)
+    assert torch.equal(got[:, 0], n.double().view(-1))
+    torch.testing.assert_close(got[:, 1], want_s1, rtol=1e-12, atol=0)
+    torch.testing.assert_close(got[:, 2], want_s2, rtol=1e-12, atol=0)
+    cum = torch.cumsum(torch.nn.functional.pad(h, (0, max(0, kmax - e)))[:, :kmax], 1)
+    hits = torch.where(n > 0, cum / n, torch.zeros(()))
+    assert torch.equal(got[:, 3:], hits.double())
+    # a view with a leading dimension of its own
+    wide = torch.zeros(k, e + 7, device="cuda")
+    wide[:, :e] = hd
+    assert torch.equal(_lib.rank_metrics(wide[:, :e], kmax).cpu(), got)
