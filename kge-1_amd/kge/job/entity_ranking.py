@@ -34,14 +34,20 @@ REFINED = "bf16x3_refined"
 
 
 def refine_band(d: int) -> float:
-    """Refinement band of kge_rank_rows relative to |q_i| * max_j |t_j|: a worst-case bound on
-    the error of the bf16x3 contraction of d-wide rows.  Each operand is represented by its
-    bf16 rounding plus the bf16 rounding of the rest (what is left is below 2^-16 of the
-    operand) and the lo * lo term is dropped: at most 3 * 2^-16 of sum_k |q_k t_k|; the 3 d
-    products are accumulated in fp32: at most 3 d * 2^-25 of the same sum on average partial
-    sums; and sum_k |q_k t_k| <= |q| |t|.  (Measured errors on N(0, 0.1) tables at d = 512:
-    below 2e-6 in these units, against a band of 9.2e-5.)"""
-    return 3 * 2.0 ** -16 + 3 * d * 2.0 ** -25
+    """Refinement band of kge_rank_rows relative to |q_i| * max_j |t_j|: a bound on the error of
+    the bf16x3 contraction of d-wide rows.
+
+    Representation: every operand x is split as hi = bf16(x), lo = bf16(x - hi), both rounded to
+    nearest (v_cvt_pk_bf16_f32; x - hi is exact in fp32), so |lo| <= 2^-9 (1 + 2^-9) |x| and the
+    rest r = x - hi - lo has |r| <= 2^-18 |x|.  The contraction sums hi hi + hi lo + lo hi (each
+    product exact in fp32); against the exact product it lacks lo_q lo_t + r_q t + (hi_q + lo_q) r_t,
+    at most (1 + 2^-8 + 1 + 1 + 2^-18) 2^-18 < 0.76 * 2^-16 of |q_k t_k|.  2^-16 covers it with a
+    third to spare (the band's own fp32 arithmetic needs 1e-6 of it).
+    Accumulation: the 3 d products are added in fp32 (inside the MFMA and across K stages): at
+    most 3 d * 2^-25 of sum_k |q_k t_k| on average partial sums.
+    And sum_k |q_k t_k| <= |q| |t|.  (Measured errors on N(0, 0.1) tables at d = 512: below 2e-6
+    in these units, against a band of 6.1e-5.)"""
+    return 2.0 ** -16 + 3 * d * 2.0 ** -25
 
 
 RANKING_SUFFIX = {"_raw": "", "_filt": "_filtered", "_filt_test": "_filtered_with_test"}
