@@ -988,6 +988,10 @@ def other_configs(device):
     }) * 1e3, 3)
     res["transe512_1vsall_fb15k237_b1024_step_ms"] = round(c2("transe", {}) * 1e3, 3)
     res["rotate512_1vsall_fb15k237_b1024_step_ms"] = round(c2("rotate", {}) * 1e3, 3)
+    # train.loss bce on the all-entities block (the usual KvsAll loss of LibKGE configurations): the
+    # engine's plane pass (kge_bce_planes, recorded with the step) beside torch's loss on the score matrix
+    res["c2_1vsall_bce_step_ms"] = round(c2("complex", {"train.loss": "bce"}) * 1e3, 3)
+    res["c2_1vsall_bce_torch_loss_step_ms"] = round(c2("complex", {"train.loss": "bce", "engine.fused_loss": False}) * 1e3, 3)
     return res
 
 
