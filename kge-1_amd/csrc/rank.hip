@@ -432,8 +432,10 @@ __global__ void __launch_bounds__(NT) rank_rows_kernel(const RankRowsArgs a) {
 }
 
 // out[0] = max over rows of the Euclidean row norm (out[0] must hold 0 on entry): a wave per
-// row, 16 rows per wave, one atomic per workgroup
-constexpr int NORM_ROWS = 64;
+// row, 2 rows per wave (a wave's rows are read one after the other, each a chain of dependent
+// loads: many short workgroups hide that latency, few long ones do not -- 43 us at 16 rows per
+// wave for a 30-MB table), one atomic per workgroup
+constexpr int NORM_ROWS = 8;
 __global__ void __launch_bounds__(256) row_norm_max_kernel(const float* __restrict__ t, int64_t ldt, int64_t m, int d,
                                                            float* out) {
   __shared__ float wmax[4];
@@ -511,23 +513,35 @@ namespace {
 // One workgroup per rank histogram: out[k] = (n, sum_j h[j] (j + 1), sum_j h[j] / (j + 1),
 // hits@1 .. hits@kmax) with the operands of entity_ranking.py:553-577 -- fp32 counts, fp32 ranks,
 // fp32 reciprocals, fp32 hits quotients -- and the two weighted sums accumulated in fp64 in a
-// fixed order (thread-strided partial sums, then a tree over the 256 threads).
-__global__ void __launch_bounds__(256) rank_metrics_kernel(const float* __restrict__ hists, int64_t ld, int64_t e,
-                                                           int kmax, double* __restrict__ out) {
-  __shared__ double red[3][256];
+// fixed order (thread-strided partial sums, then a tree over the 1,024 threads).
+__global__ void __launch_bounds__(1024) rank_metrics_kernel(const float* __restrict__ hists, int64_t ld, int64_t e,
+                                                            int kmax, double* __restrict__ out) {
+  constexpr int NT = 1024, UNROLL = 8;
+  __shared__ double red[3][NT];
   const int tid = threadIdx.x;
   const float* h = hists + (int64_t)blockIdx.x * ld;
   double n = 0.0, s1 = 0.0, s2 = 0.0;
-  for (int64_t j = tid; j < e; j += 256) {
-    const double c = (double)h[j];
-    const float rank = (float)(j + 1);
-    n += c;
-    s1 += c * (double)rank;
-    s2 += c * (double)(1.0f / rank);
+  // few workgroups run (one per histogram), so nothing hides a load's latency but the loads of the
+  // same thread: UNROLL of them are in flight at a time
+  for (int64_t j0 = tid; j0 < e; j0 += (int64_t)NT * UNROLL) {
+    float c[UNROLL];
+#pragma unroll
+    for (int u = 0; u < UNROLL; ++u) {
+      const int64_t j = j0 + (int64_t)u * NT;
+      c[u] = j < e ? h[j] : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < UNROLL; ++u) {
+      const float rank = (float)(j0 + (int64_t)u * NT + 1);
+      const double cd = (double)c[u];
+      n += cd;
+      s1 += cd * (double)rank;
+      s2 += cd * (double)(1.0f / rank);
+    }
   }
   red[0][tid] = n, red[1][tid] = s1, red[2][tid] = s2;
   __syncthreads();
-  for (int off = 128; off > 0; off >>= 1) {
+  for (int off = NT / 2; off > 0; off >>= 1) {
     if (tid < off) {
 #pragma unroll
       for (int q = 0; q < 3; ++q) red[q][tid] += red[q][tid + off];
@@ -536,13 +550,12 @@ __global__ void __launch_bounds__(256) rank_metrics_kernel(const float* __restri
   }
   double* o = out + (int64_t)blockIdx.x * (3 + kmax);
   if (tid < 3) o[tid] = red[tid][0];
-  if (tid == 0) {
+  if (tid < kmax) {
+    // hits@(tid + 1): the cumulative count summed in fp32 in index order, as torch.cumsum does
     const float nf = (float)red[0][0];  // exact: integer counts far below 2^24
     float cum = 0.f;
-    for (int k = 0; k < kmax; ++k) {
-      if (k < e) cum += h[k];
-      o[3 + k] = nf > 0.f ? (double)(cum / nf) : 0.0;
-    }
+    for (int k = 0; k <= tid && k < e; ++k) cum += h[k];
+    o[3 + tid] = nf > 0.f ? (double)(cum / nf) : 0.0;
   }
 }
 
@@ -553,7 +566,8 @@ extern "C" int kge_rank_metrics(const float* hists, int64_t ld, int64_t k, int64
   KGE_REQUIRE(k >= 0 && e > 0 && kmax >= 0 && ld >= e && (hists || k == 0) && (out || k == 0));
   if (k == 0) return 0;
   KGE_REQUIRE(k < (1LL << 31));
-  rank_metrics_kernel<<<dim3((unsigned)k), dim3(256), 0, as_stream(stream)>>>(hists, ld, e, kmax, out);
+  KGE_REQUIRE(kmax <= 1024);
+  rank_metrics_kernel<<<dim3((unsigned)k), dim3(1024), 0, as_stream(stream)>>>(hists, ld, e, kmax, out);
   KGE_CHECK_LAUNCH();
   return 0;
 }
