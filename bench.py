@@ -565,6 +565,11 @@ def main():
            "roofline": roofline}
     out.update(extra_n)
 
+    if world > 1 and not args.no_extras:
+        try:
+            out["eval_row_sharded"] = sharded_eval(args, world, rank, device, model, c)
+        except Exception as e:  # reported, never fatal for the headline (every rank runs the same code)
+            out["eval_row_sharded"] = {"error": f"{type(e).__name__}: {e}"[:300]}
     if rank == 0 and world == 1 and not args.no_extras:
         out["extras"], eval_ctx = extras(args, model, c, E, R, device)
     else:
@@ -686,6 +691,47 @@ def sharded_headline(args, world, rank, device, ent, rel, prec, s_all, p_all, st
     if not args.no_c5:
         extra["row_sharded_c5"] = sharded_c5(args, world, rank, device, prec)
     return sec_head, world * B, hi - lo, extra
+
+
+def sharded_eval(args, world, rank, device, model, c):
+    """N > 1: the metric's second half -- filtered MRR of the synthetic test split from the
+    ROW-SHARDED EntityRankingJob (each rank ranks against its ceil(E / N) entity rows at the
+    default refined precision, counts summed by one all_reduce per batch), with its wall time, and
+    the same job unsharded on every rank's full replica of the table as the check: the metrics
+    must be equal (every rank built the same tables from the same seed)."""
+    from kge import Dataset
+    from kge.job import EntityRankingJob
+
+    res = {}
+    model.eval()
+    for name, mode in (("row_sharded", "on"), ("unsharded_same_tables", "off")):
+        ce = c.clone()
+        ce.set("eval.split", "test")
+        ce.set("eval.batch_size", args.batch)
+        ce.set("engine.row_sharded", mode)
+        ds = Dataset.synthetic(ce, args.dataset, seed=0)
+        ej = EntityRankingJob(ce, ds, model=model)
+        ej._prepare()
+        ej._run()  # builds the filter indexes, warms the allocator
+        ts = []
+        for _ in range(3):
+            if world > 1:
+                dist.barrier()
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            tr = ej._run()
+            torch.cuda.synchronize()
+            ts.append(time.perf_counter() - t0)
+        (sec,) = max_over_ranks([float(np.median(ts))], device, world)
+        res[name] = {"eval_seconds": round(sec, 4), "eval_test_triples": int(len(ds.split("test"))),
+                     "mrr_filtered": tr["mean_reciprocal_rank_filtered"],
+                     "hits_at_10_filtered": tr["hits_at_10_filtered"], "mean_rank_filtered": tr["mean_rank_filtered"]}
+    a, b = res["row_sharded"], res["unsharded_same_tables"]
+    res["metrics_equal"] = all(a[k] == b[k] for k in ("mrr_filtered", "hits_at_10_filtered", "mean_rank_filtered"))
+    res["what"] = (f"EntityRankingJob over the synthetic FB15K-237 test split, batch {args.batch}, "
+                   f"engine.eval_precision bf16x3_refined: entity rows sharded over {world} ranks vs every rank "
+                   "ranking against its own full replica; seconds = max over ranks of the median of 3 runs")
+    return res
 
 
 def sharded_c5(args, world, rank, device, prec):

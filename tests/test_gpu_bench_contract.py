@@ -66,3 +66,9 @@ def test_bench_gpus_2_launches_its_own_ranks():
     assert d["config"]["global_batch"] == 2 * 1024
     assert d["value"] == pytest.approx(2 * 1024 * d["config"]["entities"] / (d["ms_per_step"] / 1e3), rel=1e-6)
     assert "row_sharded" in d and d["row_sharded"]["headline_schedule"] in ("pipelined", "serial", "grouped")
+    # the metric's second half at N ranks: filtered MRR of the row-sharded evaluation job, equal to
+    # the unsharded job's on the same tables
+    ev = d["eval_row_sharded"]
+    assert "error" not in ev, ev
+    assert ev["metrics_equal"] is True, ev
+    assert ev["row_sharded"]["eval_test_triples"] == 20466 and ev["row_sharded"]["mrr_filtered"] > 0
