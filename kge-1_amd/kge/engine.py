@@ -608,13 +608,16 @@ def rank_codes_applicable(kind: int, precision: int, ent: torch.Tensor) -> bool:
 
 @torch.no_grad()
 def rank_parts(kind: int, ent: torch.Tensor, rel: torch.Tensor, parts, true_parts, c0: int, c1: int, band_rel,
-               t_norm_max):
+               t_norm_max, tab: Optional[torch.Tensor] = None):
     """The evaluation contraction with the ranking fused in (kge_score_dot_split_rank): the
     stacked query batches parts = [(direction, eidx, ridx), ...] (one or two) against entity rows
     [c0, c1), each score compared with its row's true score in the contraction's epilogue;
     true_parts = [(true_idx, true_score), ...] per batch.  band_rel None: plain comparison of
     the bf16x3 scores; else entries within band_rel |q_i| t_norm_max of the true score are marked
-    for exact rescoring.  Returns (codes [n, ldc] int32, fp32 query rows or None, n_a)."""
+    for exact rescoring.  tab: the candidate rows when they are not rows [c0, c1) of ``ent`` -- a
+    row-sharded job builds its queries from gathered rows (``ent``) and ranks them against its
+    shard (``tab``, whose first row is entity c0).  Returns (codes [n, ldc] int32, fp32 query rows
+    or None, n_a)."""
     L.require_device(ent, rel)
     ent, rel = _rows(ent), _rows(rel)
     parts = [(d, L.idx64(e), L.idx64(r)) for d, e, r in parts]
@@ -632,7 +635,7 @@ def rank_parts(kind: int, ent: torch.Tensor, rel: torch.Tensor, parts, true_part
         band = L.rank_band(q, band_rel, t_norm_max)
     else:
         band = torch.full((n,), -1.0, device=ent.device, dtype=torch.float32)
-    codes = _timed(L.score_dot_split_rank, hi, lo, ent[c0:c1], qw, sq.n_a, true_parts[0],
+    codes = _timed(L.score_dot_split_rank, hi, lo, ent[c0:c1] if tab is None else _rows(tab), qw, sq.n_a, true_parts[0],
                    true_parts[1] if len(true_parts) > 1 else None, band, c0)
     return codes, q, sq.n_a
 

@@ -360,6 +360,9 @@ class EntityRankingJob(EvaluationJob):
                       ent_rows, tmax):
         """The batch loop of _run_ranking: adds every batch's ranks to the histograms."""
         dev = self.device
+        if (sharded is not None and getattr(sharded.ops, "rank_rows", None) is not None
+                and sharded.rank_block_applies(self._two_sided)):
+            return self._rank_batches_sharded(N, sharded, nrank, hists_sharded, group_hists, ranks_out)
         for bi, b0 in enumerate(range(0, N, self.batch_size)):
             with (self._streams.batch(bi) if sharded is None else contextlib.nullcontext()):
                 b1 = min(N, b0 + self.batch_size)
@@ -454,6 +457,51 @@ class EntityRankingJob(EvaluationJob):
                     for di, d in enumerate("os"):
                         for ri, r in enumerate(self.rankings):
                             ranks_out[f"{d}{r}"].append(rk[ri, di])
+
+    def _rank_batches_sharded(self, N, sharded, nrank, hists_sharded, group_hists, ranks_out):
+        """The row-sharded batch loop with its exchanges GROUPED over engine.eval_exchange_group
+        batches: one gather of the full rows of a group's subjects and objects (every rank holds
+        the same triples), the stacked local pass per batch against this rank's rows, and one
+        all_reduce of the group's counts -- 2 collectives per group instead of 2 per batch (each
+        costs tens of microseconds of host time whatever it carries).  The counts sum exactly,
+        so the ranks are those of the per-batch exchange (entity_ranking.py:153-216)."""
+        from ..sharded import all_reduce
+
+        G = max(1, int(self.config.get("engine.eval_exchange_group")))
+        bs = self.batch_size
+        (fp_sp, fp_po, f_col), tstack = self._stacked
+        R = self.dataset.num_relations()
+        for g0 in range(0, N, G * bs):
+            g1 = min(N, g0 + G * bs)
+            rows_g = sharded.gather_rows(self._stack_e[2 * g0:2 * g1])  # per batch: its s rows, then its o rows
+            local, spans = [], []
+            for b0 in range(g0, g1, bs):
+                B = min(g1, b0 + bs) - b0
+                s, o = self._stack_e[2 * b0:2 * b0 + B], self._stack_e[2 * b0 + B:2 * b0 + 2 * B]
+                p = self._stack_p[2 * b0:2 * b0 + B]
+                tp = (tstack[0][b0:], tstack[1][b0:]) if tstack is not None else None
+                local.append(sharded.rank_block_local(
+                    rows_g[2 * (b0 - g0):2 * (b0 - g0) + 2 * B], s, p, o, (fp_sp[b0:], fp_po[b0:]), f_col, tp,
+                    tstack[2] if tstack is not None else None, p_inverse=(p + R) if self._two_sided else None,
+                    refinement=self._shard_refinement))
+                spans.append((b0, B))
+            flat = torch.cat([c.view(-1) for c in local]) if len(local) > 1 else local[0].view(-1)
+            all_reduce(flat, group=sharded.group)
+            off = 0
+            for (b0, B), c_loc in zip(spans, local):
+                counts = flat[off:off + c_loc.numel()].view(2, nrank * 2 * B)
+                off += c_loc.numel()
+                # [2, rankings x (2 B)]: ranking-major, then direction -> [.., direction, ranking, B]
+                c = counts.view(2, nrank, 2, B).permute(0, 2, 1, 3).contiguous()
+                rk = torch.empty(2, nrank, B, dtype=torch.int64, device=self.device)
+                for di, d in enumerate("os"):
+                    sharded.ops.rank_hist_multi(c[0, di].view(-1), c[1, di].view(-1), B, self.tie_handling,
+                                                rk[di].view(-1), hists_sharded[di])
+                    if self.capture_ranks:
+                        for ri, r in enumerate(self.rankings):
+                            ranks_out[f"{d}{r}"].append(rk[di, ri])
+                if group_hists:
+                    self._count_groups(group_hists, rk.permute(1, 0, 2), b0, B)
 
     def _compute_metrics(self, rank_hist: torch.Tensor, suffix: str = "") -> Dict[str, float]:
         """entity_ranking.py:553-577 for one rank histogram."""

@@ -222,6 +222,16 @@ class EngineOps:
         so = torch.cat((ent_s, ent_o), 0)
         return self.L.score_spo(self.kind, self.l_norm, so, ar, rel, p, ar + n, so.shape[1], rel.shape[1])
 
+    def spo_stacked(self, rows, rel, p, swap=False):
+        """spo on a block that already holds the n subject rows followed by the n object rows
+        (swap: scored as (o, p, s), the reciprocal model's second direction): no copy, cached indexes."""
+        from .engine import _arange
+
+        n = p.numel()
+        ar = _arange(2 * n, rows.device)
+        a, b = (ar[n:], ar[:n]) if swap else (ar[:n], ar[n:])
+        return self.L.score_spo(self.kind, self.l_norm, rows, a, rel, p, b, rows.shape[1], rel.shape[1])
+
     def rank_counts(self, s, c0, true_idx, true_score, fp, fc, tp, tc, greater, ties):
         self.L.rank_counts(s, c0, true_idx, true_score, fp, fc, tp, tc, greater, ties)
 
@@ -248,6 +258,22 @@ class EngineOps:
         else:
             band = torch.full((q.shape[0],), -1.0, device=q.device, dtype=torch.float32)
         return self.L.score_dot_split_rank(hi, lo, tab, q.shape[1], n_a, true_a, true_b, band, c0)
+
+    def rank_codes_rows(self, rows, rel, p_a, p_b, dir_b, tab, n_a, true_a, true_b, refinement, c0):
+        """rank_codes with the query preparation folded in: the stacked queries (direction 0 from
+        rows[:n_a] with relations p_a, direction dir_b from rows[n_a:] with p_b) are prepared
+        straight into bf16 planes by ONE launch (engine.rank_parts), no fp32 stack / split pass.
+        Returns (codes, fp32 query rows or None) or None when not served."""
+        from . import engine
+
+        if not engine.rank_codes_applicable(self.kind, self.precision, tab) or rows.shape[1] != tab.shape[1]:
+            return None
+        ar = engine._arange(rows.shape[0], rows.device)
+        codes, q, _ = engine.rank_parts(
+            self.kind, rows, rel, [(0, ar[:n_a], p_a), (dir_b, ar[n_a:], p_b)], [true_a, true_b], c0,
+            c0 + tab.shape[0], refinement[0] if refinement is not None else None,
+            refinement[1] if refinement is not None else None, tab=tab)
+        return codes, q
 
     def refinement(self, ent):
         """(band relative to |q_i| max_j |t_j|, device scalar max_j |t_j| over ``ent``) when the
@@ -611,29 +637,54 @@ class RowShardedScorer:
         rows; no exchange).  Returns [2 (greater, ties), rankings x 2 B] global counts, or None
         when the two directions contract with different entity-row windows (the caller then
         takes rank_counts)."""
+        if not self.rank_block_applies(p_inverse is not None):
+            return None
+        rows = self.gather_rows(torch.cat([s, o]))  # full s rows then o rows, on every rank
+        counts = self.rank_block_local(rows, s, p, o, f_ptrs, f_col, t_ptrs, t_col, p_inverse, refinement)
+        all_reduce(counts, group=self.group)
+        return counts
+
+    def rank_block_applies(self, two_sided: bool) -> bool:
+        """Whether both directions contract with the same entity-row window (one stacked pass)."""
+        wa, wb = self._win(0, self.ent), self._win(0 if two_sided else 1, self.ent)
+        return wa.data_ptr() == wb.data_ptr() and wa.shape == wb.shape
+
+    def rank_block_local(self, rows, s, p, o, f_ptrs, f_col, t_ptrs=None, t_col=None, p_inverse=None, refinement=None):
+        """The local part of rank_block: this shard's counts [2, rankings x 2 B] of one batch, NOT
+        yet summed over the shards.  rows: the full entity rows of the batch's subjects followed
+        by its objects ([2 B, d], identical on every rank: gather_rows) -- a caller that gathers
+        the rows of several batches in one exchange and sums the counts of several batches in one
+        all_reduce pays two collectives per GROUP of batches instead of two per batch."""
         B = s.numel()
         dir_b = 1 if p_inverse is None else 0
-        wa, wb = self._win(0, self.ent), self._win(dir_b, self.ent)
-        if wa.data_ptr() != wb.data_ptr() or wa.shape != wb.shape:
-            return None
+        wa = self._win(0, self.ent)
         dev = s.device
-        rows = self.gather_rows(torch.cat([s, o]))  # full s rows then o rows, on every rank
-        ar = torch.arange(B, device=dev)
-        true_o = self.ops.spo(rows[:B], self.rel, p, rows[B:]).view(-1).float().contiguous()
-        if p_inverse is None:
-            true_s, rel_b = true_o, p
+        stacked = getattr(self.ops, "spo_stacked", None)
+        if stacked is not None and rows.is_contiguous():
+            true_o = stacked(rows, self.rel, p).view(-1).float().contiguous()
+            true_s = true_o if p_inverse is None else stacked(rows, self.rel, p_inverse, swap=True).view(-1).float().contiguous()
         else:
-            true_s, rel_b = self.ops.spo(rows[B:], self.rel, p_inverse, rows[:B]).view(-1).float().contiguous(), p_inverse
-        q = torch.cat([self.ops.prep(0, rows, ar, self.rel, p), self.ops.prep(dir_b, rows, ar + B, self.rel, rel_b)])
+            true_o = self.ops.spo(rows[:B], self.rel, p, rows[B:]).view(-1).float().contiguous()
+            true_s = true_o if p_inverse is None else self.ops.spo(rows[B:], self.rel, p_inverse, rows[:B]).view(-1).float().contiguous()
+        rel_b = p if p_inverse is None else p_inverse
         E_k = self.hi - self.lo
         nrank = 1 + (f_ptrs is not None) + (t_ptrs is not None)
         counts = torch.zeros(2, nrank * 2 * B, dtype=torch.int64, device=dev)
         o, s = o.contiguous(), s.contiguous()
         part_a = (o, true_o, f_ptrs[0] if f_ptrs is not None else None, t_ptrs[0] if t_ptrs is not None else None)
         part_b = (s, true_s, f_ptrs[1] if f_ptrs is not None else None, t_ptrs[1] if t_ptrs is not None else None)
+        codes = q = None
+        fused_rows = getattr(self.ops, "rank_codes_rows", None)
+        if fused_rows is not None:  # queries prepared straight into planes, ranking fused into the contraction
+            got = fused_rows(rows, self.rel, p, rel_b, dir_b, wa, B, (o, true_o), (s, true_s), refinement, self.lo)
+            if got is not None:
+                codes, q = got
+        if codes is None:
+            ar = torch.arange(B, device=dev)
+            q = torch.cat([self.ops.prep(0, rows, ar, self.rel, p), self.ops.prep(dir_b, rows, ar + B, self.rel, rel_b)])
+            fused = getattr(self.ops, "rank_codes", None)
+            codes = fused(q, wa, B, (o, true_o), (s, true_s), refinement, self.lo) if fused is not None else None
         refine = (q, self.ent, refinement[0], refinement[1]) if refinement is not None else None
-        fused = getattr(self.ops, "rank_codes", None)
-        codes = fused(q, wa, B, (o, true_o), (s, true_s), refinement, self.lo) if fused is not None else None
         if codes is not None:  # the scores are compared inside the contraction: no score block
             self.ops.rank_rows(None, B, self.lo, part_a, part_b, f_col, t_col, counts[0], counts[1], refine=refine,
                                codes=codes, m=E_k)
@@ -641,7 +692,6 @@ class RowShardedScorer:
             buf = torch.empty(2 * B, (E_k + 3) // 4 * 4, device=dev, dtype=torch.float32)
             scores = self.ops.score(q, wa, out=buf[:, :E_k])
             self.ops.rank_rows(scores, B, self.lo, part_a, part_b, f_col, t_col, counts[0], counts[1], refine=refine)
-        all_reduce(counts, group=self.group)
         return counts
 
     def all_gather_table(self) -> torch.Tensor:
