@@ -519,13 +519,14 @@ def main():
     achieved = alg_flops / k_s / 1e12
     # HBM bytes per launch from the PMC passes of scripts/pmc_traffic.sh (same kernel, same
     # shape, N = 1), committed under profiles/; null when absent or for another shape.
-    traffic, traffic_src = None, None
+    traffic, traffic_src, mfma_pmc = None, None, None
     for rnd in (PROFILE_ROUND, "r01"):
         pmc = os.path.join(ROOT, "profiles", rnd, "pmc_traffic.json")
         if args.precision == "bf16x3" and world == 1 and os.path.exists(pmc):
             with open(pmc) as f:
                 t = json.load(f)
             traffic = int(t["traffic_bytes"])
+            mfma_pmc = t.get("mfma")
             traffic_src = (f"profiles/{rnd}/pmc_traffic.json: 2 x FETCH_SIZE + WRITE_SIZE per dispatch "
                            f"(read {t['read_bytes'] / 1e6:.1f} MB, write {t['write_bytes'] / 1e6:.1f} MB)")
             break
@@ -540,6 +541,7 @@ def main():
                 "hbm_achieved_GBs": round(alg_bytes / k_s / 1e9, 1),
                 "hbm_frac": round(alg_bytes / k_s / 1e9 / HBM_PEAK_GBS, 4),
                 "alg_bytes_per_launch": int(alg_bytes), "alg_flops_per_launch": int(alg_flops), "note": note,
+                "mfma_busy_pmc": mfma_pmc,
                 "exact_fp32_kernel_us": round(k32_ms * 1e3, 2),
                 "exact_fp32_kernel_frac_of_fp32_mfma_peak": round(alg_flops / (k32_ms / 1e3) / 1e12 / FP32_MFMA_TFLOPS, 4)}
 

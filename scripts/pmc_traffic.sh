@@ -1,5 +1,5 @@
 #!/bin/bash
-# HBM traffic of the headline contraction kernel per launch, as MI355X_MICROARCH.md §HBM
+# HBM traffic, MFMA-busy fraction and clock of the headline contraction kernel per launch.  Traffic as MI355X_MICROARCH.md §HBM
 # prescribes: separate --pmc passes for FETCH_SIZE and WRITE_SIZE (kernel-trace only, no
 # sys/runtime trace), FETCH_SIZE doubled for the 16-B-per-lane streaming reads on gfx950.
 # Writes gpurun_out/pmc_traffic/pmc_traffic.json: copy it into the profiles/ directory being collected
@@ -10,7 +10,7 @@ OUT=$GRAFT_REPO_ROOT/gpurun_out/pmc_traffic
 mkdir -p $OUT
 cd /tmp
 i=0
-for ctr in FETCH_SIZE WRITE_SIZE; do
+for ctr in FETCH_SIZE WRITE_SIZE "SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_MFMA GRBM_GUI_ACTIVE"; do
   i=$((i+1))
   timeout -k 10 240 rocprofv3 --pmc $ctr --kernel-trace --output-format csv -d $OUT/p$i -o run -- \
     python3 $GRAFT_REPO_ROOT/bench.py --no-cpu --no-extras --no-probe --streams 1 --steps 10 --warmup 3 > $OUT/bench$i.json 2> $OUT/err$i.txt \
@@ -26,12 +26,31 @@ for fn in sorted(glob.glob(f"{root}/p*/**/*counter_collection.csv", recursive=Tr
         if "score_dot_persist" in row.get("Kernel_Name", ""):
             vals[row["Counter_Name"]].append(float(row["Counter_Value"]))
             name = row["Kernel_Name"]
+# MFMA-busy and clock from the third pass: SQ_VALU_MFMA_BUSY_CYCLES sums the busy cycles of the
+# chip's 1,024 SIMDs, GRBM_GUI_ACTIVE the active cycles of its 8 XCDs; the kernel's duration comes
+# from the same pass's kernel trace
+durs = []
+for fn in sorted(glob.glob(f"{root}/p3/**/*kernel_trace.csv", recursive=True)):
+    for row in csv.DictReader(open(fn)):
+        if "score_dot_persist" in row.get("Kernel_Name", ""):
+            durs.append(float(row["End_Timestamp"]) - float(row["Start_Timestamp"]))
+mean = lambda k: sum(vals[k]) / len(vals[k]) if vals.get(k) else None
+busy, gui, insts = mean("SQ_VALU_MFMA_BUSY_CYCLES"), mean("GRBM_GUI_ACTIVE"), mean("SQ_INSTS_MFMA")
+mfma = None
+if busy and gui and durs:
+    cycles = gui / 8.0
+    dur_us = sum(durs) / len(durs) / 1e3
+    mfma = {"mfma_busy_simd_cycles": busy, "mfma_instructions": insts, "xcd_active_cycles": cycles,
+            "kernel_us_under_pmc": dur_us, "mfma_busy_frac": busy / (cycles * 1024.0),
+            "note": "SQ_VALU_MFMA_BUSY_CYCLES (summed over the 1,024 SIMDs) / (GRBM_GUI_ACTIVE / 8 XCDs x 1,024); "
+                    "GRBM_GUI_ACTIVE also counts the cycles around the kernel's own duration, so the fraction is a "
+                    "lower bound (the MFMA pipe's share of the kernel's own cycles is higher)"}
 fetch_kb = sum(vals["FETCH_SIZE"]) / len(vals["FETCH_SIZE"])
 write_kb = sum(vals["WRITE_SIZE"]) / len(vals["WRITE_SIZE"])
 out = {"kernel": name, "dispatches": {k: len(v) for k, v in vals.items()},
        "fetch_size_kb": fetch_kb, "write_size_kb": write_kb,
        "read_bytes": 2 * fetch_kb * 1024, "write_bytes": write_kb * 1024,
-       "traffic_bytes": 2 * fetch_kb * 1024 + write_kb * 1024,
+       "traffic_bytes": 2 * fetch_kb * 1024 + write_kb * 1024, "mfma": mfma,
        "method": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes, kernel-trace only) over "
                  "bench.py --no-cpu --no-extras --no-probe --streams 1; per-dispatch mean; FETCH_SIZE x2 (gfx950: 16-B/lane "
                  "streaming reads tallied at half, MI355X_MICROARCH.md §HBM); WRITE_SIZE as reported "
