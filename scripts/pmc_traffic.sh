@@ -42,9 +42,9 @@ if busy and gui and durs:
     dur_us = sum(durs) / len(durs) / 1e3
     mfma = {"mfma_busy_simd_cycles": busy, "mfma_instructions": insts, "xcd_active_cycles": cycles,
             "kernel_us_under_pmc": dur_us, "mfma_busy_frac": busy / (cycles * 1024.0),
-            "note": "SQ_VALU_MFMA_BUSY_CYCLES (summed over the 1,024 SIMDs) / (GRBM_GUI_ACTIVE / 8 XCDs x 1,024); "
-                    "GRBM_GUI_ACTIVE also counts the cycles around the kernel's own duration, so the fraction is a "
-                    "lower bound (the MFMA pipe's share of the kernel's own cycles is higher)"}
+            "note": "SQ_VALU_MFMA_BUSY_CYCLES (summed over the 1,024 SIMDs) / (GRBM_GUI_ACTIVE / 8 XCDs x 1,024); when "
+                    "GRBM_GUI_ACTIVE / 8 over the traced duration exceeds the 2.4 GHz maximum clock the counter has run beyond "
+                    "the kernel's own duration and the fraction is a lower bound"}
 fetch_kb = sum(vals["FETCH_SIZE"]) / len(vals["FETCH_SIZE"])
 write_kb = sum(vals["WRITE_SIZE"]) / len(vals["WRITE_SIZE"])
 out = {"kernel": name, "dispatches": {k: len(v) for k, v in vals.items()},
