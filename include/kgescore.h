@@ -105,6 +105,15 @@ int kge_prep_query_split2(int model, int dir_a, int dir_b, int64_t n_a, const in
                           int64_t ld_rel, const int64_t* ridx, int64_t n, int d_e, int d_r, float* q,
                           int64_t ldq, void* q_hi, void* q_lo, int64_t ldp, void* stream);
 
+/* kge_prep_query_split2 for an evaluation batch that will be ranked with near-tie refinement: the
+ * same launch also writes band[i] = band_rel * |q_i|_2 * t_norm_max[0] (see kge_rank_band; a hair
+ * wider, never narrower) -- q, both planes and band are required.  (entity_ranking.py:153-168: the
+ * query side of score_sp_po for one batch.) */
+int kge_prep_query_split2_band(int model, int dir_a, int dir_b, int64_t n_a, const float* ent, int64_t ld_ent,
+                               const int64_t* eidx, const float* rel, int64_t ld_rel, const int64_t* ridx,
+                               int64_t n, int d_e, int d_r, float* q, int64_t ldq, void* q_hi, void* q_lo,
+                               int64_t ldp, float band_rel, const float* t_norm_max, float* band, void* stream);
+
 /* backward of kge_prep_query_split2 (see kge_prep_query_bwd) */
 int kge_prep_query_bwd2(int model, int dir_a, int dir_b, int64_t n_a, const int64_t* n_a_dev,
                         const float* ent, int64_t ld_ent, const int64_t* eidx, const float* rel,

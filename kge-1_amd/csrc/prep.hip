@@ -30,6 +30,11 @@ struct QOut {
   __bf16* lo;
   int64_t ldp;
   int padw;
+  // optional: band[i] = band_rel * |q_i|_2 * tmax[0] (the refinement band of an evaluation row,
+  // kge_rank_band) written by the vectorised kernel, whose wave holds the whole row anyway
+  float* band = nullptr;
+  float band_rel = 0.f;
+  const float* tmax = nullptr;
   __device__ __forceinline__ void put(int64_t i, int k, float v) const {
     if (q) q[i * ldq + k] = v;
     if (hi) {
@@ -122,7 +127,9 @@ __global__ void __launch_bounds__(256) prep_elementwise(const float* __restrict_
 // Needs d_e % 8 == 0 (complex halves % 4) and 16-B aligned rows (checked by the launcher).
 template <int MODEL, int DIR>
 __device__ __forceinline__ void prep_row_vec(const Rows rw, int64_t i, int lane, int d_e, const QOut& out) {
+  float ss = 0.f;  // this lane's share of |q_i|^2
   auto put4 = [&](int k, float4 v) {
+    ss = fmaf(v.x, v.x, fmaf(v.y, v.y, fmaf(v.z, v.z, fmaf(v.w, v.w, ss))));
     if (out.q) *reinterpret_cast<float4*>(out.q + i * out.ldq + k) = v;
     if (out.hi) {
       bf16x4 h, l;
@@ -191,6 +198,11 @@ __device__ __forceinline__ void prep_row_vec(const Rows rw, int64_t i, int lane,
         v = make_float4(a.x - b.x, a.y - b.y, a.z - b.z, a.w - b.w);
       put4(k, v);
     }
+  }
+  if (out.band) {
+    ss = wave_sum(ss);
+    // a hair wider than a band computed in another summation order: never narrower than the bound
+    if (lane == 0) out.band[i] = out.band_rel * sqrtf(ss) * out.tmax[0] * 1.000001f;
   }
 }
 
@@ -387,7 +399,8 @@ __global__ void __launch_bounds__(256) prep_rescal_bwd(
 }
 
 int launch_prep(int model, const float* ent, int64_t ld_ent, const int64_t* eidx, const float* rel,
-                int64_t ld_rel, const int64_t* ridx, int64_t n, int d_e, QOut q, Dirs dirs, hipStream_t st) {
+                int64_t ld_rel, const int64_t* ridx, int64_t n, int d_e, QOut q, Dirs dirs, hipStream_t st,
+                bool* band_written = nullptr) {
   dim3 grid((unsigned)n), block(256);
   const bool halves = model == KGE_COMPLEX || model == KGE_ROTATE || model == KGE_CP || model == KGE_SIMPLE;
   const int unit = halves ? d_e / 2 : d_e;
@@ -395,6 +408,8 @@ int launch_prep(int model, const float* ent, int64_t ld_ent, const int64_t* eidx
                    unit % 4 == 0 && ld_ent % 4 == 0 && ld_rel % 4 == 0 && aligned16(ent) && aligned16(rel) &&
                    (!q.q || (q.ldq % 4 == 0 && aligned16(q.q))) &&
                    (!q.hi || (q.ldp % 8 == 0 && aligned16(q.hi) && aligned16(q.lo)));
+  if (band_written) *band_written = vec && q.band;
+  if (!vec) q.band = nullptr;  // only the vectorised kernel writes it
   if (vec) {
     const dim3 g4((unsigned)((n + 3) / 4));
     switch (model) {
@@ -524,6 +539,32 @@ extern "C" int kge_prep_query_split2(int model, int dir_a, int dir_b, int64_t n_
   QOut out{q, ldq, (__bf16*)q_hi, (__bf16*)q_lo, ldp, (int)std::min<int64_t>(ldp, (qw + 31) / 32 * 32)};
   return launch_prep(model, ent, ld_ent, eidx, rel, ld_rel, ridx, n, d_e, out, Dirs{dir_a, dir_b, n_a, n_a_dev},
                      as_stream(stream));
+}
+
+extern "C" int kge_rank_band(const float* q, int64_t ldq, int64_t n, int d, float band_rel, const float* t_norm_max,
+                             float* band, void* stream);
+
+extern "C" int kge_prep_query_split2_band(int model, int dir_a, int dir_b, int64_t n_a, const float* ent,
+                                          int64_t ld_ent, const int64_t* eidx, const float* rel, int64_t ld_rel,
+                                          const int64_t* ridx, int64_t n, int d_e, int d_r, float* q, int64_t ldq,
+                                          void* q_hi, void* q_lo, int64_t ldp, float band_rel,
+                                          const float* t_norm_max, float* band, void* stream) {
+  if (int e = check_dims(model, d_e, d_r)) return e;
+  KGE_REQUIRE(n >= 0 && ent && rel && q && q_hi && q_lo && band && t_norm_max && band_rel >= 0.f);
+  KGE_REQUIRE(ldq >= query_width(model, d_e) && ldp >= query_width(model, d_e) && ldp % 8 == 0);
+  KGE_REQUIRE((dir_a == KGE_DIR_SP || dir_a == KGE_DIR_PO) && (dir_b == KGE_DIR_SP || dir_b == KGE_DIR_PO));
+  KGE_REQUIRE(n_a >= 0);
+  if (n == 0) return 0;
+  const int qw = query_width(model, d_e);
+  QOut out{q, ldq, (__bf16*)q_hi, (__bf16*)q_lo, ldp, (int)std::min<int64_t>(ldp, (qw + 31) / 32 * 32)};
+  out.band = band;
+  out.band_rel = band_rel;
+  out.tmax = t_norm_max;
+  bool written = false;
+  const int r = launch_prep(model, ent, ld_ent, eidx, rel, ld_rel, ridx, n, d_e, out, Dirs{dir_a, dir_b, n_a, nullptr},
+                            as_stream(stream), &written);
+  if (r != 0 || written) return r;
+  return kge_rank_band(q, ldq, n, qw, band_rel, t_norm_max, band, stream);  // layouts the vector kernel does not take
 }
 
 extern "C" int kge_prep_query_bwd(int model, int dir, const float* ent, int64_t ld_ent, const int64_t* eidx,

@@ -95,6 +95,8 @@ SIGNATURES = {
     "kge_ns_loss": ([_I, _P, _I64, _I64, _I64, _F, _F, _P, _P, _I64, _P], _I),
     "kge_prep_query_split2": ([_I, _I, _I, _I64, _P, _P, _I64, _P, _P, _I64, _P, _I64, _I, _I, _P, _I64, _P, _P, _I64,
                                _P], _I),
+    "kge_prep_query_split2_band": ([_I, _I, _I, _I64, _P, _I64, _P, _P, _I64, _P, _I64, _I, _I, _P, _I64, _P, _P, _I64,
+                                    _F, _P, _P, _P], _I),
     "kge_prep_query_bwd2": ([_I, _I, _I, _I64, _P, _P, _I64, _P, _P, _I64, _P, _I64, _I, _I, _P, _I64, _P, _I64, _P,
                              _I64, _P], _I),
     "kge_softmax_row_stats": ([_P, _I64, _I64, _I64, _I64, _P, _P, _P, _P, _P], _I),
@@ -289,6 +291,22 @@ def prep_query_split2(model, dir_a, dir_b, n_a, n_a_dev, ent, eidx, rel, ridx, d
                                        rows(q) if q is not None else 0, ptr(hi), ptr(lo), hi.stride(0), stream()),
            "kge_prep_query_split2")
     return q, hi, lo
+
+
+def prep_query_split2_band(model, dir_a, dir_b, n_a, ent, eidx, rel, ridx, d_e, d_r, out, band_rel, t_norm_max):
+    """kge_prep_query_split2_band: prep_query_split2 into out = (q, hi, lo) plus the rows' refinement
+    bands band_rel * |q_i| * t_norm_max[0] from the same launch.  Returns (q, hi, lo, band)."""
+    require_device(ent, rel)
+    eidx, ridx = idx64(eidx), idx64(ridx)
+    check_index(eidx, ent.shape[0], "entity index")
+    check_index(ridx, rel.shape[0], "relation index")
+    q, hi, lo = out
+    band = torch.empty(eidx.numel(), device=ent.device, dtype=torch.float32)
+    _check(lib().kge_prep_query_split2_band(model, dir_a, dir_b, int(n_a), ptr(ent), rows(ent), ptr(eidx), ptr(rel),
+                                            rows(rel), ptr(ridx), eidx.numel(), d_e, d_r, ptr(q), rows(q), ptr(hi),
+                                            ptr(lo), hi.stride(0), float(band_rel), ptr(t_norm_max), ptr(band),
+                                            stream()), "kge_prep_query_split2_band")
+    return q, hi, lo, band
 
 
 def prep_query_bwd2(model, dir_a, dir_b, n_a, n_a_dev, ent, eidx, rel, ridx, d_e, d_r, dq, d_ent, d_rel):

@@ -630,10 +630,12 @@ def rank_parts(kind: int, ent: torch.Tensor, rel: torch.Tensor, parts, true_part
     hi = torch.empty(n, ldp, device=ent.device, dtype=torch.bfloat16)
     lo = torch.empty_like(hi)
     sq = StackedQueries.of(parts)
-    L.prep_query_split2(kind, sq.dir_a, sq.dir_b, sq.n_a, None, ent, sq.eidx, rel, sq.ridx, d_e, d_r, out=(q, hi, lo))
-    if refine:
-        band = L.rank_band(q, band_rel, t_norm_max)
+    if refine:  # the bands come out of the preparation launch
+        _, _, _, band = L.prep_query_split2_band(kind, sq.dir_a, sq.dir_b, sq.n_a, ent, sq.eidx, rel, sq.ridx, d_e, d_r,
+                                                 (q, hi, lo), band_rel, t_norm_max)
     else:
+        L.prep_query_split2(kind, sq.dir_a, sq.dir_b, sq.n_a, None, ent, sq.eidx, rel, sq.ridx, d_e, d_r,
+                            out=(q, hi, lo))
         band = torch.full((n,), -1.0, device=ent.device, dtype=torch.float32)
     codes = _timed(L.score_dot_split_rank, hi, lo, ent[c0:c1] if tab is None else _rows(tab), qw, sq.n_a, true_parts[0],
                    true_parts[1] if len(true_parts) > 1 else None, band, c0)

@@ -451,3 +451,37 @@ def test_rank_metrics_vs_torch_formula(k, e, kmax):
     wide = torch.zeros(k, e + 7, device="cuda")
     wide[:, :e] = hd
     assert torch.equal(_lib.rank_metrics(wide[:, :e], kmax).cpu(), got)
+
+
+@pytest.mark.parametrize("model,d", [("complex", 512), ("distmult", 64), ("simple", 128), ("rescal", 16)])
+def test_prep_split2_band_matches_separate_launches(L, model, d):
+    """kge_prep_query_split2_band = kge_prep_query_split2 + kge_rank_band: identical query rows and
+    planes, bands equal to the separate launch's up to summation order (RESCAL takes the separate
+    launches inside the entry point)."""
+    kind = {"complex": L.COMPLEX, "distmult": L.DISTMULT, "simple": L.SIMPLE, "rescal": L.RESCAL}[model]
+    g = torch.Generator(device="cuda").manual_seed(d)
+    E, R, n, n_a = 300, 7, 37, 20
+    d_r = d * d if model == "rescal" else d
+    ent = torch.randn(E, d, device="cuda", generator=g) * 0.1
+    rel = torch.randn(R, d_r, device="cuda", generator=g) * 0.1
+    eidx = torch.randint(0, E, (n,), device="cuda", generator=g)
+    ridx = torch.randint(0, R, (n,), device="cuda", generator=g)
+    qw = L.query_width(kind, d)
+    ldp = (qw + 31) // 32 * 32
+
+    def bufs():
+        return (torch.empty(n, qw, device="cuda"), torch.empty(n, ldp, device="cuda", dtype=torch.bfloat16),
+                torch.empty(n, ldp, device="cuda", dtype=torch.bfloat16))
+
+    tmax = L.row_norm_max(ent)
+    q0, h0, l0 = L.prep_query_split2(kind, L.DIR_SP, L.DIR_PO, n_a, None, ent, eidx, rel, ridx, d, d_r, out=bufs())
+    b0 = L.rank_band(q0, 7e-5, tmax)
+    q1, h1, l1, b1 = L.prep_query_split2_band(kind, L.DIR_SP, L.DIR_PO, n_a, ent, eidx, rel, ridx, d, d_r, bufs(), 7e-5,
+                                              tmax)
+    torch.cuda.synchronize()
+    assert torch.equal(q0, q1) and torch.equal(h0.view(torch.int16), h1.view(torch.int16))
+    assert torch.equal(l0.view(torch.int16), l1.view(torch.int16))
+    torch.testing.assert_close(b1, b0, rtol=2e-6, atol=0)
+    # and against float64: the band is never narrower than band_rel |q| tmax
+    exact = 7e-5 * q0.double().norm(dim=1) * float(tmax)
+    assert bool((b1.double() >= exact * (1 - 1e-7)).all())
