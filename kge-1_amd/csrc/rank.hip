@@ -206,15 +206,19 @@ __global__ void __launch_bounds__(NT) rank_rows_kernel(const RankRowsArgs a) {
   if (REFINE) {
     qrow = a.q + i * a.ldq;
     float ss = 0.f;
-    for (int k = threadIdx.x; k < a.d; k += NT) ss += qrow[k] * qrow[k];
+    if (!CODES) {  // the codes already say which entries lie inside the band
+      for (int k = threadIdx.x; k < a.d; k += NT) ss += qrow[k] * qrow[k];
 #pragma unroll
-    for (int off = 32; off > 0; off >>= 1) ss += __shfl_xor(ss, off, 64);
-    if (lane == 0) fsm[wave] = ss;
+      for (int off = 32; off > 0; off >>= 1) ss += __shfl_xor(ss, off, 64);
+      if (lane == 0) fsm[wave] = ss;
+    }
     if (threadIdx.x == 0) ev_total = 0;
     __syncthreads();
-    ss = 0.f;
-    for (int w = 0; w < NT / 64; ++w) ss += fsm[w];
-    band = a.band_rel * sqrtf(ss) * a.t_norm_max[0];
+    if (!CODES) {
+      ss = 0.f;
+      for (int w = 0; w < NT / 64; ++w) ss += fsm[w];
+      band = a.band_rel * sqrtf(ss) * a.t_norm_max[0];
+    }
   }
 
   // Counting one entry: the true column takes the true score; a score inside the band is
