@@ -119,6 +119,7 @@ struct RankRowsArgs {
   const float* s;
   const unsigned* codes;  // CODES kernels: the contraction's 2-bit codes instead of scores
   int64_t ldc;
+  int codes_vec;  // code rows start on 16-byte boundaries: a row is read four words at a time
   int64_t lds, n_a, n, m, c0;
   RankPart part[2];
   const int64_t* f_col;
@@ -355,13 +356,72 @@ __global__ void __launch_bounds__(NT) rank_rows_kernel(const RankRowsArgs a) {
     }
     return done;
   };
+  // CODES with 16-byte aligned rows.  The kernel is a chain of dependent loads (words of the row,
+  // then per filter list: its bounds, its columns, their codes, then the rescored table rows), far
+  // too short in bytes for bandwidth to matter: here every load that does not depend on a count is
+  // requested before the first word is looked at -- the row four words per thread and round, the
+  // first NT columns of each filter list and their codes -- which leaves three round trips.
+  const int nfilt = P.t_ptr ? 2 : (P.f_ptr ? 1 : 0);
+  const bool pre = CODES && a.codes_vec;
+  int64_t fb[2] = {0, 0}, fe[2] = {0, 0}, fj[2] = {-1, -1};
+  unsigned fcode[2] = {0u, 0u};
+  auto scan_code_quads = [&]() {
+    const int64_t nquads = (m + 63) >> 6;
+    const uint4* c4 = reinterpret_cast<const uint4*>(crow);
+    auto words = [&](int64_t qi, const uint4& w4) {
+      const unsigned ws[4] = {w4.x, w4.y, w4.z, w4.w};
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const unsigned w = ws[k];
+        if (!w) continue;
+        const unsigned lo = w & 0x55555555u, hi = (w >> 1) & 0x55555555u;
+        gt += __popc(lo & ~hi);
+        eq += __popc(hi & ~lo);
+        unsigned near = lo & hi;
+        const int64_t jw = qi * 64 + k * 4;
+        while (REFINE && near) {
+          const int b = __ffs(near) - 1;
+          near &= near - 1;
+          count_code(jw + (b >> 3) * 16 + ((b >> 1) & 3), 3u, 1);
+        }
+      }
+    };
+    uint4 w4 = make_uint4(0u, 0u, 0u, 0u);
+    if (threadIdx.x < nquads) w4 = c4[threadIdx.x];
+    for (int r = 0; r < nfilt; ++r) {
+      const int64_t* ptr = r == 0 ? P.f_ptr : P.t_ptr;
+      fb[r] = ptr[li];
+      fe[r] = ptr[li + 1];
+    }
+    for (int r = 0; r < nfilt; ++r) {
+      const int64_t x = fb[r] + threadIdx.x;
+      if (x < fe[r]) {
+        const int64_t j = (r == 0 ? a.f_col : a.t_col)[x] - a.c0;
+        if (j >= 0 && j < m && j != tj) {
+          fj[r] = j;
+          fcode[r] = kge_rank_code_of(crow, j);
+        }
+      }
+    }
+    words(threadIdx.x, w4);
+    for (int64_t base = NT; base < nquads; base += 2 * NT) {  // uniform trip count
+      const int64_t q0 = base + threadIdx.x, q1 = q0 + NT;
+      uint4 u0 = make_uint4(0u, 0u, 0u, 0u), u1 = u0;
+      if (q0 < nquads) u0 = c4[q0];
+      if (q1 < nquads) u1 = c4[q1];
+      words(q0, u0);
+      words(q1, u1);
+    }
+    if (threadIdx.x == 0 && tj >= 0 && tj < m) eq += 1;  // the true entry ties with itself
+  };
   unsigned done = 0;  // ring entries rescored so far
   if (REFINE) {
     // Rows with at most EV_CAP entries inside the band (all but degenerate ones: thousands of
     // candidates tied with the true score) are scanned without a barrier and drained once.  A
     // row with more has overwritten ring slots: its counts are discarded and the row is scanned
     // again, draining after every step.
-    scan(false);
+    if (pre) scan_code_quads();
+    else scan(false);
     __syncthreads();  // every push is visible; nobody pushes again before the next barrier
     const bool overflow = ev_total > (unsigned)EV_CAP;
     if (!overflow) {
@@ -376,6 +436,8 @@ __global__ void __launch_bounds__(NT) rank_rows_kernel(const RankRowsArgs a) {
       __syncthreads();
       done = scan(true);
     }
+  } else if (pre) {
+    scan_code_quads();
   } else {
     scan(false);
   }
@@ -404,16 +466,20 @@ __global__ void __launch_bounds__(NT) rank_rows_kernel(const RankRowsArgs a) {
   }
   __syncthreads();
 
-  const int nfilt = P.t_ptr ? 2 : (P.f_ptr ? 1 : 0);
   for (int r = 0; r < nfilt; ++r) {
     const int64_t* ptr = r == 0 ? P.f_ptr : P.t_ptr;
     const int64_t* col = r == 0 ? a.f_col : a.t_col;
     gt = 0;
     eq = 0;
-    const int64_t b = ptr[li], e = ptr[li + 1];
+    const int64_t b = pre ? fb[r] : ptr[li], e = pre ? fe[r] : ptr[li + 1];
     for (int64_t x0 = b; x0 < e; x0 += NT) {  // uniform trip count
       const int64_t x = x0 + threadIdx.x;
-      if (x < e) {
+      if (pre && x0 == b) {  // columns and codes are in registers already
+        if (fj[r] >= 0) {
+          count_code(fj[r], fcode[r], -1);
+          eq += (t == -INFINITY);
+        }
+      } else if (x < e) {
         const int64_t j = col[x] - a.c0;
         if (j >= 0 && j < m && j != tj) {
           if (CODES)
@@ -664,6 +730,7 @@ static int rank_rows_common(const float* s, int64_t lds, const unsigned* codes, 
   }
   if (n == 0) return 0;
   RankRowsArgs a;
+  a.codes_vec = codes && ldc % 4 == 0 && aligned16(codes);
   a.s = s; a.codes = codes; a.ldc = ldc; a.lds = lds; a.n_a = n_a; a.n = n; a.m = m; a.c0 = c0;
   a.part[0] = RankPart{true_idx_a, true_score_a, f_ptr_a, t_ptr_a};
   a.part[1] = RankPart{true_idx_b, true_score_b, f_ptr_b, t_ptr_b};

@@ -326,13 +326,17 @@ def _near_tie_tables(rng, n, m, d, copies):
     return q, t, true_idx
 
 
-@pytest.mark.parametrize("n_a,n_b,m,c0,d,with_test,refined", [
-    (300, 300, 3001, 0, 512, True, True),     # two 256-row tiles per batch, a ragged last entity panel
-    (100, 100, 1000, 700, 128, True, True),   # 128-row tiles; a chunk starting at column 700
-    (64, 0, 257, 0, 64, False, True),         # one batch; one column past a panel
-    (300, 211, 2050, 0, 256, True, False),    # no refinement: the bf16x3 scores compared as they are
+@pytest.mark.parametrize("n_a,n_b,m,c0,d,with_test,refined,max_filt,ld_pad", [
+    (300, 300, 3001, 0, 512, True, True, 30, 0),     # two 256-row tiles per batch, a ragged last entity panel
+    (100, 100, 1000, 700, 128, True, True, 30, 0),   # 128-row tiles; a chunk starting at column 700
+    (64, 0, 257, 0, 64, False, True, 30, 0),         # one batch; one column past a panel
+    (300, 211, 2050, 0, 256, True, False, 30, 0),    # no refinement: the bf16x3 scores compared as they are
+    (40, 40, 40000, 0, 64, True, True, 700, 0),      # rows of more than 256 word quads, filter lists of more
+                                                     # than 256 columns: the ranking kernel's later rounds
+    (40, 40, 40000, 300, 64, True, False, 700, 0),
+    (100, 100, 1000, 700, 128, True, True, 400, 3),  # code rows off 16-byte boundaries: read word by word
 ])
-def test_fused_rank_codes_give_the_score_block_counts(L, n_a, n_b, m, c0, d, with_test, refined):
+def test_fused_rank_codes_give_the_score_block_counts(L, n_a, n_b, m, c0, d, with_test, refined, max_filt, ld_pad):
     """kge_score_dot_split_rank + kge_rank_rows_codes (the scores never written: compared with
     the true score in the contraction's epilogue, 2-bit codes out) against kge_score_dot_split +
     kge_rank_rows on the score block: the same contraction, the same band, the same exact
@@ -348,10 +352,11 @@ def test_fused_rank_codes_give_the_score_block_counts(L, n_a, n_b, m, c0, d, wit
     true_score = exact[np.arange(n), true_local].copy()
     true_score[2] = np.nan
     true_score[4] = -np.inf
-    f_ptr_a, f_col_a = _csr(rng, n_a, E, 30)
-    f_ptr_b, f_col_b = _csr(rng, n_b, E, 30) if n_b else (np.zeros(1, np.int64), np.zeros(0, np.int64))
-    t_a = _minus(*_csr(rng, n_a, E, 20), f_ptr_a, f_col_a)
-    t_b = _minus(*_csr(rng, n_b, E, 20), f_ptr_b, f_col_b) if n_b else (np.zeros(1, np.int64), np.zeros(0, np.int64))
+    f_ptr_a, f_col_a = _csr(rng, n_a, E, max_filt)
+    f_ptr_b, f_col_b = _csr(rng, n_b, E, max_filt) if n_b else (np.zeros(1, np.int64), np.zeros(0, np.int64))
+    n_test = max_filt * 2 // 3
+    t_a = _minus(*_csr(rng, n_a, E, n_test), f_ptr_a, f_col_a)
+    t_b = _minus(*_csr(rng, n_b, E, n_test), f_ptr_b, f_col_b) if n_b else (np.zeros(1, np.int64), np.zeros(0, np.int64))
     nrank = 3 if with_test else 2
     qd, td = _dev(q), _dev(t)
     hi, lo = L.split_rows(qd)
@@ -376,9 +381,11 @@ def test_fused_rank_codes_give_the_score_block_counts(L, n_a, n_b, m, c0, d, wit
                   rows_per_hist=rows_per_hist, refine=refine)
         if codes_path:
             band = L.rank_band(qd, band_rel, tmax) if refined else torch.full((n,), -1.0, device="cuda")
+            ldc = L.rank_codes_ld(m)
+            codes = torch.empty(n, ldc + ld_pad, dtype=torch.int32, device="cuda")[:, :ldc] if ld_pad else None
             codes = L.score_dot_split_rank(hi, lo, td, d, n_a, (ti[:n_a], ts[:n_a]),
-                                           (ti[n_a:], ts[n_a:]) if n_b else None, band, c0)
-            assert codes.shape == (n, L.rank_codes_ld(m)) and L.lib().kge_rank_codes_ld(m) == codes.shape[1]
+                                           (ti[n_a:], ts[n_a:]) if n_b else None, band, c0, codes=codes)
+            assert codes.shape == (n, ldc) and L.lib().kge_rank_codes_ld(m) == ldc
             L.rank_rows(None, n_a, c0, part_a, part_b, f_col, t_col, g, tt, codes=codes, m=m, **kw)
         else:
             buf = torch.empty(n, (m + 3) // 4 * 4, device="cuda")
