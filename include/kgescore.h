@@ -366,6 +366,24 @@ int kge_score_cand_bwd(int model, float l_norm, int dir, const float* q, int64_t
                        int64_t ldg, float* dq, int64_t lddq, float* d_ent, int64_t ld_dent,
                        void* stream);
 
+/* The same two passes for candidate lists given in a caller-chosen ORDER: position c of row i
+ * holds candidate cand[i, c] whose score belongs to column col[i, c] of out / g / s (col[i, :] a
+ * permutation of 0 .. k-1).  With every row in ascending candidate order the workgroups of an XCD
+ * sweep the entity table together and find most rows in that XCD's L2 (same result, same
+ * reference code: kge/job/train.py:868-892; the order of a row's candidates carries no meaning
+ * there).  kge_score_cand_bwd_q_ordered writes dq only and needs the vector layout of
+ * kge_score_cand_bwd's fast path ((d or d/2 for RotatE) % 4 == 0, 16-B aligned rows, at most
+ * 2048 such elements; else KGE_ERR_ALIGN). */
+int kge_score_cand_ordered(int model, float l_norm, int dir, const float* q, int64_t ldq,
+                           const float* ent, int64_t ld_ent, const int64_t* cand, int64_t ldc,
+                           const int64_t* col, int64_t ldcol, int64_t n, int64_t k, int d,
+                           float* out, int64_t ldo, void* stream);
+int kge_score_cand_bwd_q_ordered(int model, float l_norm, int dir, const float* q, int64_t ldq,
+                                 const float* ent, int64_t ld_ent, const int64_t* cand,
+                                 int64_t ldc, const int64_t* col, int64_t ldcol, int64_t n,
+                                 int64_t k, int d, const float* s, int64_t lds, const float* g,
+                                 int64_t ldg, float* dq, int64_t lddq, void* stream);
+
 /* d_ent part of kge_score_cand_bwd without atomics, for candidate lists with many repeats:
  * the caller groups the n*k pairs by entity -- order[] = the flattened pair indexes
  * (i*k + c; cand contiguous [n][k]) sorted by cand value, seg_ptr[nseg+1] the group
@@ -383,6 +401,11 @@ int kge_score_cand_bwd_ent(int model, float l_norm, int dir, const float* q, int
  * kge_score_cand_bwd_ent. */
 int kge_bucket_scatter(const int64_t* idx, int64_t n, int64_t* cursor, int64_t* order,
                        void* stream);
+
+/* The bucket counts that go with it: counts[idx[t]] += 1 for t in [0, n) (int64 atomics; the
+ * caller zeroes counts; indexes outside [0, nbuckets) are skipped) -- torch.bincount without its
+ * host round trip for the maximum. */
+int kge_bucket_count(const int64_t* idx, int64_t n, int64_t nbuckets, int64_t* counts, void* stream);
 
 /* ---- optimizer ------------------------------------------------------------------------
  * One fused Adagrad step over n contiguous fp32 elements (an embedding table, its dense

@@ -41,9 +41,11 @@ __device__ __forceinline__ float elem(float q, float e, float sigma, bool l1) {
   return l1 ? fabsf(df) : df * df;
 }
 
+// |dr + i di| (p = 1) or its square: the hardware square root (1 ulp), as the all-entities
+// distance kernels take it -- sqrtf's correctly rounded expansion is ten instructions per element
 __device__ __forceinline__ float cabs_term(float dr, float di, bool l1) {
   const float sq = fmaf(di, di, dr * dr);
-  return l1 ? sqrtf(sq) : sq;
+  return l1 ? __builtin_amdgcn_sqrtf(sq) : sq;
 }
 
 template <int KIND>
@@ -87,7 +89,8 @@ __device__ __forceinline__ float row_reduce(const float* qs, const float* e, int
 template <int KIND, bool VEC>
 __global__ void __launch_bounds__(NT) cand_kernel(bool l1, float sigma, const float* __restrict__ q, int64_t ldq,
                                                   const float* __restrict__ ent, int64_t ld_ent,
-                                                  const int64_t* __restrict__ cand, int64_t ldc, int k, int d,
+                                                  const int64_t* __restrict__ cand, int64_t ldc,
+                                                  const int64_t* __restrict__ col, int64_t ldcol, int k, int d,
                                                   float* __restrict__ out, int64_t ldo) {
   extern __shared__ __attribute__((aligned(16))) float qs[];
   const int64_t i = blockIdx.x;
@@ -104,10 +107,77 @@ __global__ void __launch_bounds__(NT) cand_kernel(bool l1, float sigma, const fl
     float a2 = row_reduce<KIND, VEC>(qs, e2, d, lane, sigma, l1);
     a1 = wave_sum(a1);
     a2 = wave_sum(a2);
-    if (lane == 0) {
-      out[i * ldo + c] = finish<KIND>(a1, l1);
-      if (c2 < k) out[i * ldo + c2] = finish<KIND>(a2, l1);
+    if (lane == 0) {  // col: the output column of the candidate at position c (ordered lists)
+      out[i * ldo + (col ? col[i * ldcol + c] : c)] = finish<KIND>(a1, l1);
+      if (c2 < k) out[i * ldo + (col ? col[i * ldcol + c2] : c2)] = finish<KIND>(a2, l1);
     }
+  }
+}
+
+// The same scores with the query's slice in registers (lane owns elements ch*256 + lane*4 .. +3,
+// as the backward kernels) and a whole candidate row requested at once.  Per lane the partial
+// sums are formed in the same order as cand_kernel<KIND, true> forms them: the same bits.
+template <int KIND, int NCH>
+__global__ void __launch_bounds__(NT) cand_fwd_kernel(bool l1, float sigma, const float* __restrict__ q, int64_t ldq,
+                                                      const float* __restrict__ ent, int64_t ld_ent,
+                                                      const int64_t* __restrict__ cand, int64_t ldc,
+                                                      const int64_t* __restrict__ col, int64_t ldcol, int k, int d,
+                                                      float* __restrict__ out, int64_t ldo) {
+  constexpr int P = KIND == K_ROTATE ? 2 : 1;
+  const int64_t i = blockIdx.x;
+  const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  const int unit = KIND == K_ROTATE ? d / 2 : d;
+  const float* qi = q + i * ldq;
+  float4 qv[NCH][P];
+  int off[NCH];
+  bool own[NCH];  // lanes past the row's end re-read its last elements and count nothing
+#pragma unroll
+  for (int ch = 0; ch < NCH; ++ch) {
+    own[ch] = ch * 256 + lane * 4 < unit;
+    off[ch] = min(ch * 256 + lane * 4, unit - 4);
+#pragma unroll
+    for (int pl = 0; pl < P; ++pl) qv[ch][pl] = ld4(qi + off[ch] + pl * unit);
+  }
+  const int64_t* ci = cand + i * ldc;
+  const int64_t* coli = col ? col + i * ldcol : nullptr;
+  auto rows = [&](float4 (&ev)[NCH][P], int64_t id) {
+    const float* e = ent + id * ld_ent;
+#pragma unroll
+    for (int ch = 0; ch < NCH; ++ch)
+#pragma unroll
+      for (int pl = 0; pl < P; ++pl) ev[ch][pl] = ld4(e + off[ch] + pl * unit);
+  };
+  auto reduce = [&](const float4 (&ev)[NCH][P]) {
+    float acc = 0.f;
+#pragma unroll
+    for (int ch = 0; ch < NCH; ++ch) {
+      const float4 a = qv[ch][0], b = ev[ch][0];
+      float t;
+      if (KIND == K_ROTATE) {
+        const float4 ai = qv[ch][P - 1], bi = ev[ch][P - 1];
+        t = cabs_term(a.x - b.x, ai.x - bi.x, l1) + cabs_term(a.y - b.y, ai.y - bi.y, l1) +
+            cabs_term(a.z - b.z, ai.z - bi.z, l1) + cabs_term(a.w - b.w, ai.w - bi.w, l1);
+      } else {
+        t = elem<KIND>(a.x, b.x, sigma, l1) + elem<KIND>(a.y, b.y, sigma, l1) + elem<KIND>(a.z, b.z, sigma, l1) +
+            elem<KIND>(a.w, b.w, sigma, l1);
+      }
+      if (own[ch]) acc += t;
+    }
+    return wave_sum(acc);
+  };
+  auto put = [&](int c, float a) {
+    if (lane == 0 && c < k) out[i * ldo + (coli ? coli[c] : c)] = finish<KIND>(a, l1);
+  };
+  // ONE row per wave on its way at a time: the candidate lists of the queries resident on an XCD
+  // are swept together (ascending lists), and the rows they share are found in that XCD's L2 only
+  // while everything in flight plus the spread between the workgroups fits into it -- at 4-KB rows
+  // two rows per wave in flight cost 15 % and four 50 % (measured at 512 x 1,025 x 1,024 floats).
+  int64_t id = ci[w < k ? w : 0];
+  for (int c = w; c < k; c += NW) {
+    float4 a[NCH][P];
+    rows(a, id);
+    id = ci[min(c + NW, k - 1)];
+    put(c, reduce(a));
   }
 }
 
@@ -121,17 +191,19 @@ __device__ __forceinline__ void grad_q(bool l1, float sigma, float inv, float gc
     gr = gc * er;
   } else if (KIND == K_TRANSE) {  // score = -||diff||, diff = sigma (q - e) + eps
     const float df = sigma * (qr - er) + 1e-6f;
-    const float dn = l1 ? (df > 0.f ? 1.f : (df < 0.f ? -1.f : 0.f)) : df * inv;
+    // p = 1: sign(df) as the median of (df * 2^126, -1, 1) -- every normal df saturates, 0 stays 0
+    const float dn = l1 ? __builtin_amdgcn_fmed3f(df * 0x1p126f, -1.f, 1.f) : df * inv;
     gr = -gc * sigma * dn;
   } else {  // score = sum |q - e|_C or its L2 form
     const float dr = qr - er, di = qi - ei;
     float f = inv;
-    if (l1) {
-      const float a = sqrtf(fmaf(di, di, dr * dr));
-      f = a > 0.f ? 1.f / a : 0.f;
+    if (l1) {  // 1 / |dr + i di| by the hardware reciprocal square root (1 ulp); 0 at 0
+      const float sq = fmaf(di, di, dr * dr);
+      f = sq > 0.f ? __builtin_amdgcn_rsqf(sq) : 0.f;
     }
-    gr = gc * dr * f;
-    gi = gc * di * f;
+    f *= gc;
+    gr = dr * f;
+    gi = di * f;
   }
 }
 
@@ -147,14 +219,15 @@ __device__ __forceinline__ float inv_norm(bool l1, const float* s, int64_t idx) 
 template <int KIND, int NCH>
 __global__ void __launch_bounds__(NT) cand_bwd_q_kernel(bool l1, float sigma, const float* __restrict__ q,
                                                         int64_t ldq, const float* __restrict__ ent, int64_t ld_ent,
-                                                        const int64_t* __restrict__ cand, int64_t ldc, int k, int d,
+                                                        const int64_t* __restrict__ cand, int64_t ldc,
+                                                        const int64_t* __restrict__ col, int64_t ldcol, int k, int d,
                                                         const float* __restrict__ s, int64_t lds,
                                                         const float* __restrict__ g, int64_t ldg, float* __restrict__ dq,
                                                         int64_t lddq) {
   constexpr int P = KIND == K_ROTATE ? 2 : 1;  // float4 planes per chunk
   extern __shared__ __attribute__((aligned(16))) float red[];  // NW x d
   const int64_t i = blockIdx.x;
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
   const int unit = KIND == K_ROTATE ? d / 2 : d;
   const float* qi = q + i * ldq;
   float4 qv[NCH][P], acc[NCH][P];
@@ -168,16 +241,21 @@ __global__ void __launch_bounds__(NT) cand_bwd_q_kernel(bool l1, float sigma, co
     }
   }
   const int64_t* ci = cand + i * ldc;
-  for (int c = w; c < k; c += NW) {
-    const float gc = g[i * ldg + c];
-    if (gc == 0.f) continue;
-    const float inv = inv_norm<KIND>(l1, s, i * lds + c);
-    const float* e = ent + ci[c] * ld_ent;
-    float4 ev[NCH][P];
+  const int64_t* coli = col ? col + i * ldcol : nullptr;
+  // gradient and inverse norm of the candidate at position c (its column in g and s: col)
+  auto meta = [&](int c, float& gc, float& inv) {
+    const int64_t cc = coli ? coli[c] : c;
+    gc = g[i * ldg + cc];
+    inv = inv_norm<KIND>(l1, s, i * lds + cc);
+  };
+  auto rows = [&](float4 (&ev)[NCH][P], int64_t id) {
+    const float* e = ent + id * ld_ent;
 #pragma unroll
     for (int ch = 0; ch < NCH; ++ch)
 #pragma unroll
       for (int pl = 0; pl < P; ++pl) ev[ch][pl] = ld4(e + min(ch * 256 + lane * 4, unit - 4) + pl * unit);
+  };
+  auto accumulate = [&](const float4 (&ev)[NCH][P], float gc, float inv) {
 #pragma unroll
     for (int ch = 0; ch < NCH; ++ch) {
       const float4 a = qv[ch][0], b = ev[ch][0];
@@ -191,6 +269,25 @@ __global__ void __launch_bounds__(NT) cand_bwd_q_kernel(bool l1, float sigma, co
       if (P > 1) {
         acc[ch][P - 1].x += gi[0]; acc[ch][P - 1].y += gi[1]; acc[ch][P - 1].z += gi[2]; acc[ch][P - 1].w += gi[3];
       }
+    }
+  };
+  // A candidate is a chain of dependent loads (column -> gradient / norm, id -> row): the next
+  // candidate's gradient, norm and id are fetched while this one's row is on its way.  One row
+  // per wave in flight, no more (see cand_fwd_kernel).
+  int c = w;
+  if (c < k) {
+    float gc_n, inv_n;
+    meta(c, gc_n, inv_n);
+    int64_t id_n = ci[c];
+    for (; c < k; c += NW) {
+      const float gc = gc_n, inv = inv_n;
+      float4 ev[NCH][P];
+      rows(ev, id_n);
+      if (c + NW < k) {
+        meta(c + NW, gc_n, inv_n);
+        id_n = ci[c + NW];
+      }
+      if (gc != 0.f) accumulate(ev, gc, inv);
     }
   }
   // cross-wave reduction through LDS (each wave's partial row), then one store of dq_i
@@ -210,7 +307,10 @@ __global__ void __launch_bounds__(NT) cand_bwd_q_kernel(bool l1, float sigma, co
   }
 }
 
-// d_ent, vectorised, one wave per entity group (pairs of order[seg_ptr[u] .. seg_ptr[u+1]))
+// d_ent, vectorised, one wave per entity group (pairs of order[seg_ptr[u] .. seg_ptr[u+1])).
+// The group is a chain of dependent loads per pair (pair index -> gradient / norm -> query row);
+// the loop keeps the NEXT pair's query row in flight while the current one is accumulated and
+// fetches the pair index two ahead, so that a pair costs one L2 round trip instead of three.
 template <int KIND, int NCH>
 __global__ void __launch_bounds__(256) cand_bwd_ent_kernel(bool l1, float sigma, const float* __restrict__ q,
                                                            int64_t ldq, const float* __restrict__ ent,
@@ -222,33 +322,51 @@ __global__ void __launch_bounds__(256) cand_bwd_ent_kernel(bool l1, float sigma,
                                                            int64_t ld_dent) {
   constexpr int P = KIND == K_ROTATE ? 2 : 1;
   const int lane = threadIdx.x & 63;
-  const int64_t u = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  // the wave's group, known to be the same in every lane: its bookkeeping goes to the scalar unit
+  const int64_t u = (int64_t)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
   if (u >= nseg) return;
   const int64_t p0 = seg_ptr[u], p1 = seg_ptr[u + 1];
   if (p0 >= p1) return;  // entity without pairs (seg_ptr may have one slot per entity)
   const int64_t row = cand[order[p0]];  // order indexes the flattened [n, k] candidate matrix
   const int unit = KIND == K_ROTATE ? d / 2 : d;
   const float* e = ent + row * ld_ent;
-  float4 ev[NCH][P], acc[NCH][P];
+  float4 ev[NCH][P], acc[NCH][P], qn[NCH][P];
+  int off[NCH];
 #pragma unroll
-  for (int ch = 0; ch < NCH; ++ch)
+  for (int ch = 0; ch < NCH; ++ch) {
+    off[ch] = min(ch * 256 + lane * 4, unit - 4);
 #pragma unroll
     for (int pl = 0; pl < P; ++pl) {
-      ev[ch][pl] = ld4(e + min(ch * 256 + lane * 4, unit - 4) + pl * unit);
+      ev[ch][pl] = ld4(e + off[ch] + pl * unit);
       acc[ch][pl] = f4(0.f);
     }
-  for (int64_t t = p0; t < p1; ++t) {
-    const int64_t pair = order[t];
+  }
+  // gradient, inverse norm and query row of the pair at position t of `order`
+  auto fetch = [&](int64_t pair, float& gc, float& inv) {
     const int64_t i = pair / k, c = pair - i * k;
-    const float gc = g[i * ldg + c];
-    if (gc == 0.f) continue;
-    const float inv = inv_norm<KIND>(l1, s, i * lds + c);
+    gc = g[i * ldg + c];
+    inv = inv_norm<KIND>(l1, s, i * lds + c);
     const float* qi = q + i * ldq;
+#pragma unroll
+    for (int ch = 0; ch < NCH; ++ch)
+#pragma unroll
+      for (int pl = 0; pl < P; ++pl) qn[ch][pl] = ld4(qi + off[ch] + pl * unit);
+  };
+  float gc_n, inv_n;
+  fetch(order[p0], gc_n, inv_n);
+  int64_t pair_nn = order[p0 + 1 < p1 ? p0 + 1 : p0];
+  for (int64_t t = p0; t < p1; ++t) {
+    const float gc = gc_n, inv = inv_n;
     float4 qv[NCH][P];
 #pragma unroll
     for (int ch = 0; ch < NCH; ++ch)
 #pragma unroll
-      for (int pl = 0; pl < P; ++pl) qv[ch][pl] = ld4(qi + min(ch * 256 + lane * 4, unit - 4) + pl * unit);
+      for (int pl = 0; pl < P; ++pl) qv[ch][pl] = qn[ch][pl];
+    if (t + 1 < p1) {
+      fetch(pair_nn, gc_n, inv_n);
+      pair_nn = order[t + 2 < p1 ? t + 2 : t + 1];
+    }
+    if (gc == 0.f) continue;
 #pragma unroll
     for (int ch = 0; ch < NCH; ++ch) {
       const float4 a = qv[ch][0], b = ev[ch][0];
@@ -339,6 +457,14 @@ __global__ void bucket_scatter_kernel(const int64_t* __restrict__ idx, int64_t n
   order[atomicAdd(reinterpret_cast<unsigned long long*>(cursor + idx[t]), 1ull)] = t;
 }
 
+// counts[idx[t]] += 1 (indexes outside [0, nbuckets) are not counted)
+__global__ void bucket_count_kernel(const int64_t* __restrict__ idx, int64_t n, int64_t nbuckets, int64_t* counts) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= n) return;
+  const int64_t b = idx[t];
+  if (b >= 0 && b < nbuckets) atomicAdd(reinterpret_cast<unsigned long long*>(counts + b), 1ull);
+}
+
 int kind_of(int model) {
   switch (model) {
     case KGE_COMPLEX:
@@ -371,10 +497,21 @@ void dispatch_nch(int nch, A&&... a) {
 template <int KIND, int NCH>
 struct LaunchQ {
   static void run(dim3 grid, size_t sh, hipStream_t st, bool l1, float sigma, const float* q, int64_t ldq,
-                  const float* ent, int64_t ld_ent, const int64_t* cand, int64_t ldc, int k, int d, const float* s,
-                  int64_t lds, const float* g, int64_t ldg, float* dq, int64_t lddq) {
-    cand_bwd_q_kernel<KIND, NCH><<<grid, dim3(NT), sh, st>>>(l1, sigma, q, ldq, ent, ld_ent, cand, ldc, k, d, s, lds,
-                                                             g, ldg, dq, lddq);
+                  const float* ent, int64_t ld_ent, const int64_t* cand, int64_t ldc, const int64_t* col,
+                  int64_t ldcol, int k, int d, const float* s, int64_t lds, const float* g, int64_t ldg, float* dq,
+                  int64_t lddq) {
+    cand_bwd_q_kernel<KIND, NCH><<<grid, dim3(NT), sh, st>>>(l1, sigma, q, ldq, ent, ld_ent, cand, ldc, col, ldcol, k,
+                                                             d, s, lds, g, ldg, dq, lddq);
+  }
+};
+
+template <int KIND, int NCH>
+struct LaunchF {
+  static void run(dim3 grid, hipStream_t st, bool l1, float sigma, const float* q, int64_t ldq, const float* ent,
+                  int64_t ld_ent, const int64_t* cand, int64_t ldc, const int64_t* col, int64_t ldcol, int k, int d,
+                  float* out, int64_t ldo) {
+    cand_fwd_kernel<KIND, NCH><<<grid, dim3(NT), 0, st>>>(l1, sigma, q, ldq, ent, ld_ent, cand, ldc, col, ldcol, k, d,
+                                                          out, ldo);
   }
 };
 
@@ -391,9 +528,9 @@ struct LaunchE {
 
 }  // namespace
 
-extern "C" int kge_score_cand(int model, float l_norm, int dir, const float* q, int64_t ldq, const float* ent,
-                              int64_t ld_ent, const int64_t* cand, int64_t ldc, int64_t n, int64_t k, int d, float* out,
-                              int64_t ldo, void* stream) {
+static int score_cand_impl(int model, float l_norm, int dir, const float* q, int64_t ldq, const float* ent,
+                           int64_t ld_ent, const int64_t* cand, int64_t ldc, const int64_t* col, int64_t ldcol,
+                           int64_t n, int64_t k, int d, float* out, int64_t ldo, void* stream) {
   const int kind = kind_of(model);
   KGE_REQUIRE(kind >= 0 && (dir == KGE_DIR_SP || dir == KGE_DIR_PO) && (l_norm == 1.f || l_norm == 2.f));
   KGE_REQUIRE(n >= 0 && k >= 0 && d > 0 && d <= 4096 && n < (1LL << 31) && k < (1LL << 31));
@@ -407,12 +544,28 @@ extern "C" int kge_score_cand(int model, float l_norm, int dir, const float* q, 
   const bool vec = unit % 4 == 0 && ld_ent % 4 == 0 && aligned16(ent);
   const size_t sh = (size_t)d * sizeof(float);
   const dim3 grid((unsigned)n), block(NT);
+  const int nch = nch_of(unit);
+  if (vec && nch && ldq % 4 == 0 && aligned16(q)) {  // rows and query slices as float4 in registers
+    if (kind == K_DOT)
+      dispatch_nch<LaunchF, K_DOT>(nch, grid, st, l1, sigma, q, ldq, ent, ld_ent, cand, ldc, col, ldcol, (int)k, d, out,
+                                   ldo);
+    else if (kind == K_TRANSE)
+      dispatch_nch<LaunchF, K_TRANSE>(nch, grid, st, l1, sigma, q, ldq, ent, ld_ent, cand, ldc, col, ldcol, (int)k, d,
+                                      out, ldo);
+    else
+      dispatch_nch<LaunchF, K_ROTATE>(nch, grid, st, l1, sigma, q, ldq, ent, ld_ent, cand, ldc, col, ldcol, (int)k, d,
+                                      out, ldo);
+    KGE_CHECK_LAUNCH();
+    return 0;
+  }
   auto go = [&](auto kind_tag) {
     constexpr int K = decltype(kind_tag)::value;
     if (vec)
-      cand_kernel<K, true><<<grid, block, sh, st>>>(l1, sigma, q, ldq, ent, ld_ent, cand, ldc, (int)k, d, out, ldo);
+      cand_kernel<K, true><<<grid, block, sh, st>>>(l1, sigma, q, ldq, ent, ld_ent, cand, ldc, col, ldcol, (int)k, d,
+                                                    out, ldo);
     else
-      cand_kernel<K, false><<<grid, block, sh, st>>>(l1, sigma, q, ldq, ent, ld_ent, cand, ldc, (int)k, d, out, ldo);
+      cand_kernel<K, false><<<grid, block, sh, st>>>(l1, sigma, q, ldq, ent, ld_ent, cand, ldc, col, ldcol, (int)k, d,
+                                                     out, ldo);
   };
   if (kind == K_DOT)
     go(std::integral_constant<int, K_DOT>());
@@ -424,10 +577,24 @@ extern "C" int kge_score_cand(int model, float l_norm, int dir, const float* q, 
   return 0;
 }
 
-extern "C" int kge_score_cand_bwd(int model, float l_norm, int dir, const float* q, int64_t ldq, const float* ent,
-                                  int64_t ld_ent, const int64_t* cand, int64_t ldc, int64_t n, int64_t k, int d,
-                                  const float* s, int64_t lds, const float* g, int64_t ldg, float* dq, int64_t lddq,
-                                  float* d_ent, int64_t ld_dent, void* stream) {
+extern "C" int kge_score_cand(int model, float l_norm, int dir, const float* q, int64_t ldq, const float* ent,
+                              int64_t ld_ent, const int64_t* cand, int64_t ldc, int64_t n, int64_t k, int d, float* out,
+                              int64_t ldo, void* stream) {
+  return score_cand_impl(model, l_norm, dir, q, ldq, ent, ld_ent, cand, ldc, nullptr, 0, n, k, d, out, ldo, stream);
+}
+
+extern "C" int kge_score_cand_ordered(int model, float l_norm, int dir, const float* q, int64_t ldq, const float* ent,
+                                      int64_t ld_ent, const int64_t* cand, int64_t ldc, const int64_t* col,
+                                      int64_t ldcol, int64_t n, int64_t k, int d, float* out, int64_t ldo,
+                                      void* stream) {
+  KGE_REQUIRE(col && ldcol >= k);
+  return score_cand_impl(model, l_norm, dir, q, ldq, ent, ld_ent, cand, ldc, col, ldcol, n, k, d, out, ldo, stream);
+}
+
+static int score_cand_bwd_impl(int model, float l_norm, int dir, const float* q, int64_t ldq, const float* ent,
+                               int64_t ld_ent, const int64_t* cand, int64_t ldc, const int64_t* col, int64_t ldcol,
+                               int64_t n, int64_t k, int d, const float* s, int64_t lds, const float* g, int64_t ldg,
+                               float* dq, int64_t lddq, float* d_ent, int64_t ld_dent, void* stream) {
   const int kind = kind_of(model);
   KGE_REQUIRE(kind >= 0 && (dir == KGE_DIR_SP || dir == KGE_DIR_PO) && (l_norm == 1.f || l_norm == 2.f));
   KGE_REQUIRE(n >= 0 && k >= 0 && d > 0 && d <= 3584 && n < (1LL << 31) && k < (1LL << 31));
@@ -446,17 +613,18 @@ extern "C" int kge_score_cand_bwd(int model, float l_norm, int dir, const float*
   if (!d_ent && nch && unit % 4 == 0 && ldq % 4 == 0 && ld_ent % 4 == 0 && aligned16(q) && aligned16(ent)) {
     const size_t sh = (size_t)NW * d * sizeof(float);
     if (kind == K_DOT)
-      dispatch_nch<LaunchQ, K_DOT>(nch, grid, sh, st, l1, sigma, q, ldq, ent, ld_ent, cand, ldc, (int)k, d, s, lds, g,
-                                   ldg, dq, lddq);
+      dispatch_nch<LaunchQ, K_DOT>(nch, grid, sh, st, l1, sigma, q, ldq, ent, ld_ent, cand, ldc, col, ldcol, (int)k, d,
+                                   s, lds, g, ldg, dq, lddq);
     else if (kind == K_TRANSE)
-      dispatch_nch<LaunchQ, K_TRANSE>(nch, grid, sh, st, l1, sigma, q, ldq, ent, ld_ent, cand, ldc, (int)k, d, s, lds,
-                                      g, ldg, dq, lddq);
+      dispatch_nch<LaunchQ, K_TRANSE>(nch, grid, sh, st, l1, sigma, q, ldq, ent, ld_ent, cand, ldc, col, ldcol, (int)k,
+                                      d, s, lds, g, ldg, dq, lddq);
     else
-      dispatch_nch<LaunchQ, K_ROTATE>(nch, grid, sh, st, l1, sigma, q, ldq, ent, ld_ent, cand, ldc, (int)k, d, s, lds,
-                                      g, ldg, dq, lddq);
+      dispatch_nch<LaunchQ, K_ROTATE>(nch, grid, sh, st, l1, sigma, q, ldq, ent, ld_ent, cand, ldc, col, ldcol, (int)k,
+                                      d, s, lds, g, ldg, dq, lddq);
     KGE_CHECK_LAUNCH();
     return 0;
   }
+  if (col) return KGE_ERR_ALIGN;  // ordered lists are served by the vector kernel only
   const size_t sh = (size_t)(1 + NW) * d * sizeof(float);
   static std::atomic<bool> lds_ok[3][KGE_MAX_DEVICES];
   int fi = 0;
@@ -474,6 +642,24 @@ extern "C" int kge_score_cand_bwd(int model, float l_norm, int dir, const float*
                                                                  s, lds, g, ldg, dq, lddq, d_ent, ld_dent);
   KGE_CHECK_LAUNCH();
   return 0;
+}
+
+extern "C" int kge_score_cand_bwd(int model, float l_norm, int dir, const float* q, int64_t ldq, const float* ent,
+                                  int64_t ld_ent, const int64_t* cand, int64_t ldc, int64_t n, int64_t k, int d,
+                                  const float* s, int64_t lds, const float* g, int64_t ldg, float* dq, int64_t lddq,
+                                  float* d_ent, int64_t ld_dent, void* stream) {
+  return score_cand_bwd_impl(model, l_norm, dir, q, ldq, ent, ld_ent, cand, ldc, nullptr, 0, n, k, d, s, lds, g, ldg, dq,
+                             lddq, d_ent, ld_dent, stream);
+}
+
+extern "C" int kge_score_cand_bwd_q_ordered(int model, float l_norm, int dir, const float* q, int64_t ldq,
+                                            const float* ent, int64_t ld_ent, const int64_t* cand, int64_t ldc,
+                                            const int64_t* col, int64_t ldcol, int64_t n, int64_t k, int d,
+                                            const float* s, int64_t lds, const float* g, int64_t ldg, float* dq,
+                                            int64_t lddq, void* stream) {
+  KGE_REQUIRE(col && ldcol >= k && dq);
+  return score_cand_bwd_impl(model, l_norm, dir, q, ldq, ent, ld_ent, cand, ldc, col, ldcol, n, k, d, s, lds, g, ldg, dq,
+                             lddq, nullptr, 0, stream);
 }
 
 extern "C" int kge_score_cand_bwd_ent(int model, float l_norm, int dir, const float* q, int64_t ldq,
@@ -515,6 +701,14 @@ extern "C" int kge_bucket_scatter(const int64_t* idx, int64_t n, int64_t* cursor
   KGE_REQUIRE(n >= 0 && (n == 0 || (idx && cursor && order)));
   if (n == 0) return 0;
   bucket_scatter_kernel<<<dim3((unsigned)((n + 255) / 256)), dim3(256), 0, as_stream(stream)>>>(idx, n, cursor, order);
+  KGE_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int kge_bucket_count(const int64_t* idx, int64_t n, int64_t nbuckets, int64_t* counts, void* stream) {
+  KGE_REQUIRE(n >= 0 && nbuckets >= 0 && (n == 0 || (idx && counts)));
+  if (n == 0) return 0;
+  bucket_count_kernel<<<dim3((unsigned)((n + 255) / 256)), dim3(256), 0, as_stream(stream)>>>(idx, n, nbuckets, counts);
   KGE_CHECK_LAUNCH();
   return 0;
 }

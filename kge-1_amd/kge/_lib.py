@@ -69,9 +69,13 @@ SIGNATURES = {
     "kge_score_cand": ([_I, _F, _I, _P, _I64, _P, _I64, _P, _I64, _I64, _I64, _I, _P, _I64, _P], _I),
     "kge_score_cand_bwd": ([_I, _F, _I, _P, _I64, _P, _I64, _P, _I64, _I64, _I64, _I, _P, _I64, _P, _I64, _P,
                             _I64, _P, _I64, _P], _I),
+    "kge_score_cand_ordered": ([_I, _F, _I, _P, _I64, _P, _I64, _P, _I64, _P, _I64, _I64, _I64, _I, _P, _I64, _P], _I),
+    "kge_score_cand_bwd_q_ordered": ([_I, _F, _I, _P, _I64, _P, _I64, _P, _I64, _P, _I64, _I64, _I64, _I, _P, _I64,
+                                      _P, _I64, _P, _I64, _P], _I),
     "kge_score_cand_bwd_ent": ([_I, _F, _I, _P, _I64, _P, _I64, _P, _I64, _I64, _I, _P, _P, _I64, _P, _I64, _P,
                                 _I64, _P, _I64, _P], _I),
     "kge_bucket_scatter": ([_P, _I64, _P, _P, _P], _I),
+    "kge_bucket_count": ([_P, _I64, _I64, _P, _P], _I),
     "kge_stage_i64": ([_P, _P, _I64, _P], _I),
     "kge_rank_hist_multi": ([_P, _P, _I64, _I64, _I, _P, _P, _I64, _P], _I),
     "kge_rank_metrics": ([_P, _I64, _I64, _I64, _I, _P, _P], _I),
@@ -651,6 +655,37 @@ def score_cand(model, l_norm, direction, q, ent, cand, out=None):
     return o
 
 
+def score_cand_ordered(model, l_norm, direction, q, ent, cand, col, out=None):
+    """kge_score_cand_ordered: out[i, col[i, c]] = score(q_i, ent[cand[i, c]]) -- the candidate
+    lists in the caller's order (ascending per row: table rows shared through the XCDs' L2),
+    col[i, :] the permutation back to the output columns (contiguous int64 [n, k] both)."""
+    require_device(q, ent, cand, col)
+    if cand.dtype != torch.int64 or col.dtype != torch.int64 or not cand.is_contiguous() or not col.is_contiguous() \
+            or cand.shape != col.shape or cand.dim() != 2:
+        raise ValueError("score_cand_ordered: cand and col are contiguous int64 [n, k]")
+    check_index(cand, ent.shape[0], "candidate index")
+    n, k = cand.shape
+    d = q.shape[1]
+    o = out if out is not None else torch.empty(n, k, device=q.device, dtype=torch.float32)
+    _check(lib().kge_score_cand_ordered(model, float(l_norm), direction, ptr(q), rows(q), ptr(ent), rows(ent),
+                                        ptr(cand), k, ptr(col), k, n, k, d, ptr(o), rows(o), stream()),
+           "kge_score_cand_ordered")
+    return o
+
+
+def score_cand_bwd_q_ordered(model, l_norm, direction, q, ent, cand, col, s, g, dq) -> bool:
+    """kge_score_cand_bwd_q_ordered (dq only).  False when the layout is not served."""
+    n, k = cand.shape
+    rc = lib().kge_score_cand_bwd_q_ordered(model, float(l_norm), direction, ptr(q), rows(q), ptr(ent), rows(ent),
+                                            ptr(cand), k, ptr(col), k, n, k, q.shape[1], ptr(s),
+                                            rows(s) if s is not None else 0, ptr(g), rows(g), ptr(dq), rows(dq),
+                                            stream())
+    if rc == 1002:  # KGE_ERR_ALIGN
+        return False
+    _check(rc, "kge_score_cand_bwd_q_ordered")
+    return True
+
+
 def score_cand_bwd(model, l_norm, direction, q, ent, cand, s, g, dq, d_ent):
     cand = cand if (cand.dtype == torch.int64 and cand.dim() == 2 and cand.stride(1) == 1) else \
         cand.long().contiguous()
@@ -676,7 +711,8 @@ def score_cand_bwd_ent(model, l_norm, direction, q, ent, cand, s, g, d_ent) -> b
     flat = cand.reshape(-1)
     E = ent.shape[0]
     seg_ptr = torch.zeros(E + 1, dtype=torch.int64, device=cand.device)
-    torch.cumsum(torch.bincount(flat, minlength=E), 0, out=seg_ptr[1:])
+    _check(lib().kge_bucket_count(ptr(flat), flat.numel(), E, ptr(seg_ptr[1:]), stream()), "kge_bucket_count")
+    seg_ptr.cumsum_(0)
     cursor = seg_ptr[:-1].clone()
     order = torch.empty_like(flat)
     _check(lib().kge_bucket_scatter(ptr(flat), flat.numel(), ptr(cursor), ptr(order), stream()), "kge_bucket_scatter")

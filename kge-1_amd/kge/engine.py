@@ -673,6 +673,20 @@ def score_spo(kind: int, l_norm: float, ent, sidx, rel, pidx, oidx) -> torch.Ten
     return _ScoreSpo.apply(kind, float(l_norm), ent, L.idx64(sidx), rel, L.idx64(pidx), L.idx64(oidx))
 
 
+def _cand_order(cand: torch.Tensor, n_rows: int):
+    """(sorted candidate lists, their output columns) when ordering pays, else None.  Workgroup i
+    of the candidate kernels gathers the table rows of query i's list; with every list ascending,
+    the workgroups resident on an XCD sweep the table together and a row fetched for one query is
+    found in that XCD's L2 by the others (measured at 512 x 1,025 candidates over 14,541 rows of
+    4 KB: 78 % L2 hits instead of 10 %, forward 268 -> 190 us, dq 262 -> 149 us).  That needs
+    rows that several of an XCD's queries use: (n / 8) * k uses of n_rows rows."""
+    n, k = cand.shape
+    if k < 32 or n * k < 16 * n_rows:
+        return None
+    srt, col = torch.sort(cand, 1)
+    return srt, col
+
+
 class _ScoreCand(torch.autograd.Function):
     @staticmethod
     def forward(ctx, kind, direction, l_norm, ent, eidx, rel, ridx, cand):
@@ -680,15 +694,21 @@ class _ScoreCand(torch.autograd.Function):
         n = eidx.numel()
         d_e, d_r = ent.shape[1], rel.shape[1]
         q = L.prep_query(kind, direction, ent, eidx, rel, ridx, n, d_e, d_r)
-        s = L.score_cand(kind, l_norm, direction, q, window(kind, direction, ent), cand)
+        ent_w = window(kind, direction, ent)
+        order = _cand_order(cand, ent.shape[0])
+        if order is None:
+            s = L.score_cand(kind, l_norm, direction, q, ent_w, cand)
+            order = (cand.new_empty(0), cand.new_empty(0))
+        else:
+            s = L.score_cand_ordered(kind, l_norm, direction, q, ent_w, *order)
         ctx.meta = (kind, direction, l_norm, n, d_e, d_r)
-        ctx.save_for_backward(ent, eidx, rel, ridx, cand, q, s)
+        ctx.save_for_backward(ent, eidx, rel, ridx, cand, q, s, *order)
         return s
 
     @staticmethod
     def backward(ctx, g):
         kind, direction, l_norm, n, d_e, d_r = ctx.meta
-        ent, eidx, rel, ridx, cand, q, s = ctx.saved_tensors
+        ent, eidx, rel, ridx, cand, q, s, srt, col = ctx.saved_tensors
         need_ent, need_rel = ctx.needs_input_grad[3], ctx.needs_input_grad[5]
         d_ent = torch.zeros_like(ent) if need_ent else None
         d_rel = torch.zeros_like(rel) if need_rel else None
@@ -699,7 +719,9 @@ class _ScoreCand(torch.autograd.Function):
         d_ent_w = window(kind, direction, d_ent) if d_ent is not None else None
         ent_done = d_ent is not None and L.score_cand_bwd_ent(kind, l_norm, direction, q, ent_w, cand, s, g,
                                                               d_ent_w)
-        L.score_cand_bwd(kind, l_norm, direction, q, ent_w, cand, s, g, dq, None if ent_done else d_ent_w)
+        if not (dq is not None and srt.numel() and (ent_done or d_ent is None)
+                and L.score_cand_bwd_q_ordered(kind, l_norm, direction, q, ent_w, srt, col, s, g, dq)):
+            L.score_cand_bwd(kind, l_norm, direction, q, ent_w, cand, s, g, dq, None if ent_done else d_ent_w)
         if dq is not None:
             L.prep_query_bwd(kind, direction, ent, eidx, rel, ridx, n, d_e, d_r, dq, d_ent, d_rel)
         return None, None, None, d_ent, None, d_rel, None, None

@@ -1,5 +1,5 @@
-"""C4: RotatE-1024 negative sampling (1024 negatives per slot, s and o), FB15K-237 shape,
-B=512 -- step timing (and a target for rocprofv3)."""
+"""A few negative-sampling steps of BASELINE config C4 (RotatE-1024, 1,024 negatives per corrupted
+slot, FB15K-237 shape, B=512) for rocprofv3.  argv[1]: implementation (triple | batch)."""
 import os
 import sys
 import time
@@ -13,9 +13,11 @@ from kge import Config, Dataset  # noqa: E402
 from kge.job import TrainingJob  # noqa: E402
 
 impl = sys.argv[1] if len(sys.argv) > 1 else "triple"
+model = sys.argv[2] if len(sys.argv) > 2 else "rotate"
+torch.manual_seed(0)
 c = Config()
-c.set("model", "rotate")
-c._import("rotate")
+c.set("model", model)
+c._import(model)
 c.set("job.device", "cuda")
 c.set("lookup_embedder.dim", 1024)
 c.set("train.type", "negative_sampling")
@@ -25,26 +27,21 @@ c.set("negative_sampling.implementation", impl)
 c.set("train.optimizer", "Adagrad")
 c.set("train.optimizer_args", {"lr": 0.1})
 c.set("train.batch_size", 512)
+c.set("engine.row_sharded", "off")
 c.set("verbose", False)
 ds = Dataset.synthetic(c, "fb15k-237", seed=0)
 job = TrainingJob.create(c, ds)
 job._prepare()
+if os.environ.get("SORT_NEG") == "1":  # what would rows of ascending candidates buy?
+    _sample = job._sampler.sample
+    job._sampler.sample = lambda triples, slot: torch.sort(_sample(triples, slot), 1).values
 B = 512
 perm = torch.randperm(job.num_examples, generator=torch.Generator().manual_seed(0))
-
-
-def step(i):
-    return job.train_step(i, job._collate(perm[i * B:(i + 1) * B]))[0]
-
-
 for i in range(5):
-    step(i)
+    job.train_step(i, job._collate(perm[i * B:(i + 1) * B]))
 torch.cuda.synchronize()
 t0 = time.perf_counter()
-n = 20
-for i in range(5, 5 + n):
-    r = step(i)
+for i in range(5, 15):
+    job.train_step(i, job._collate(perm[i * B:(i + 1) * B]))
 torch.cuda.synchronize()
-dt = (time.perf_counter() - t0) / n
-print(f"rotate-1024 NS({impl}) B={B} N=1024: step {dt * 1e3:.3f} ms  "
-      f"{2 * B * 1025 / dt / 1e6:.1f} M scored triples/s  loss {r.avg_loss:.4f}")
+print(f"{model} negative_sampling {impl} step {(time.perf_counter() - t0) / 10 * 1e3:.3f} ms")

@@ -101,10 +101,54 @@ def _ns_job(model, impl, num_neg=31, dim=64, shared=False, filtering=False, E=50
     return job
 
 
+@pytest.mark.parametrize("model,ln", [("distmult", 1.0), ("transe", 1.0), ("transe", 2.0), ("rotate", 1.0),
+                                      ("rotate", 2.0)])
+@pytest.mark.parametrize("d", [128, 1024])
+def test_score_cand_ordered_lists_vs_plain(L, model, ln, d):
+    """The engine orders long candidate lists (ascending per query, kge_score_cand_ordered /
+    kge_score_cand_bwd_q_ordered) when the rows repeat across queries: the scores must be the
+    SAME BITS as kge_score_cand's in the caller's column order (a pair's arithmetic does not
+    depend on its position), the gradients equal up to the summation order."""
+    from kge import engine
+
+    torch.manual_seed(5)
+    E, R, n, k = 900, 7, 70, 300
+    kind = MODEL_IDS[model]
+    d_r = d // 2 if model == "rotate" else d
+    ent = (torch.randn(E, d, device="cuda") * 0.3).requires_grad_()
+    rel = (torch.randn(R, d_r, device="cuda") * 0.3).requires_grad_()
+    eidx = torch.randint(0, E, (n,), device="cuda")
+    ridx = torch.randint(0, R, (n,), device="cuda")
+    cand = torch.randint(0, E, (n, k), device="cuda")
+    cand[:, 7] = cand[:, 11]  # duplicates within a row
+    w = torch.randn(n, k, device="cuda")
+    w[3, 5] = 0.0  # pairs without gradient are skipped
+    assert engine._cand_order(cand, E) is not None
+    for direction in (L.DIR_SP, L.DIR_PO):
+        out = engine.score_cand(kind, direction, ln, ent, eidx, rel, ridx, cand)
+        (out * w).sum().backward()
+        ge, gr = ent.grad.clone(), rel.grad.clone()
+        ent.grad = rel.grad = None
+        # the plain kernels on the same inputs
+        with torch.no_grad():
+            q = L.prep_query(kind, direction, ent, eidx, rel, ridx, n, d, d_r)
+            s = L.score_cand(kind, ln, direction, q, ent, cand)
+            assert torch.equal(out, s)
+            dq = torch.empty_like(q)
+            d_ent, d_rel = torch.zeros_like(ent), torch.zeros_like(rel)
+            assert L.score_cand_bwd_ent(kind, ln, direction, q, ent, cand, s, w, d_ent)
+            L.score_cand_bwd(kind, ln, direction, q, ent, cand, s, w, dq, None)
+            L.prep_query_bwd(kind, direction, ent, eidx, rel, ridx, n, d, d_r, dq, d_ent, d_rel)
+        assert (ge - d_ent).abs().max() <= 2e-5 * d_ent.abs().max()
+        assert (gr - d_rel).abs().max() <= 2e-5 * d_rel.abs().max()
+
+
+@pytest.mark.parametrize("num_neg", [31, 255])
 @pytest.mark.parametrize("model", ["rotate", "complex", "transe", "cp", "simple"])
-def test_ns_implementations_agree(model):
-    """Column 0 = the positive; same negatives through every scoring implementation."""
-    job = _ns_job(model, "triple")
+def test_ns_implementations_agree(model, num_neg):
+    """Column 0 = the positive; same negatives through every scoring implementation (255
+    negatives: the candidate lists are long enough for the engine to order them)."""
+    job = _ns_job(model, "triple", num_neg=num_neg)
     tr = job.dataset.split("train")[:64].long().cuda()
     torch.manual_seed(1)
     for slot in (0, 2):
