@@ -388,12 +388,16 @@ __global__ void __launch_bounds__(NT) rank_rows_kernel(const RankRowsArgs a) {
     };
     uint4 w4 = make_uint4(0u, 0u, 0u, 0u);
     if (threadIdx.x < nquads) w4 = c4[threadIdx.x];
-    for (int r = 0; r < nfilt; ++r) {
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {  // (constant indexes: the arrays stay in registers)
+      if (r >= nfilt) continue;
       const int64_t* ptr = r == 0 ? P.f_ptr : P.t_ptr;
       fb[r] = ptr[li];
       fe[r] = ptr[li + 1];
     }
-    for (int r = 0; r < nfilt; ++r) {
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {
+      if (r >= nfilt) continue;
       const int64_t x = fb[r] + threadIdx.x;
       if (x < fe[r]) {
         const int64_t j = (r == 0 ? a.f_col : a.t_col)[x] - a.c0;
@@ -471,12 +475,14 @@ __global__ void __launch_bounds__(NT) rank_rows_kernel(const RankRowsArgs a) {
     const int64_t* col = r == 0 ? a.f_col : a.t_col;
     gt = 0;
     eq = 0;
-    const int64_t b = pre ? fb[r] : ptr[li], e = pre ? fe[r] : ptr[li + 1];
+    const int64_t pj = r == 0 ? fj[0] : fj[1];  // (selects, not indexed: registers)
+    const unsigned pcode = r == 0 ? fcode[0] : fcode[1];
+    const int64_t b = pre ? (r == 0 ? fb[0] : fb[1]) : ptr[li], e = pre ? (r == 0 ? fe[0] : fe[1]) : ptr[li + 1];
     for (int64_t x0 = b; x0 < e; x0 += NT) {  // uniform trip count
       const int64_t x = x0 + threadIdx.x;
       if (pre && x0 == b) {  // columns and codes are in registers already
-        if (fj[r] >= 0) {
-          count_code(fj[r], fcode[r], -1);
+        if (pj >= 0) {
+          count_code(pj, pcode, -1);
           eq += (t == -INFINITY);
         }
       } else if (x < e) {
