@@ -402,6 +402,12 @@ int kge_score_cand_bwd_ent(int model, float l_norm, int dir, const float* q, int
 int kge_bucket_scatter(const int64_t* idx, int64_t n, int64_t* cursor, int64_t* order,
                        void* stream);
 
+/* Every row of x[n, k] (ids in [0, 2^50), k <= 8192) sorted ascending, stably: sorted[i, :] and the
+ * positions col[i, :] the ids came from (both contiguous [n, k]) -- torch.sort(x, 1, stable=True)
+ * as one launch, the cand / col input of kge_score_cand_ordered. */
+int kge_sort_rows(const int64_t* x, int64_t ldx, int64_t n, int64_t k, int64_t* sorted, int64_t* col,
+                  void* stream);
+
 /* The bucket counts that go with it: counts[idx[t]] += 1 for t in [0, n) (int64 atomics; the
  * caller zeroes counts; indexes outside [0, nbuckets) are skipped) -- torch.bincount without its
  * host round trip for the maximum. */

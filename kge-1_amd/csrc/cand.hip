@@ -465,6 +465,36 @@ __global__ void bucket_count_kernel(const int64_t* __restrict__ idx, int64_t n, 
   if (b >= 0 && b < nbuckets) atomicAdd(reinterpret_cast<unsigned long long*>(counts + b), 1ull);
 }
 
+// Rows of ids sorted ascending inside LDS: a bitonic network over the keys id << 13 | position
+// (ties keep their order: a stable sort), padded with the largest key to npad, a power of two.
+// sorted[i, :] = the ids, col[i, :] = the positions they came from.
+__global__ void __launch_bounds__(512) sort_rows_kernel(const int64_t* __restrict__ x, int64_t ldx, int k, int npad,
+                                                        int64_t* __restrict__ sorted, int64_t* __restrict__ col) {
+  extern __shared__ __attribute__((aligned(16))) unsigned long long key[];
+  const int64_t i = blockIdx.x;
+  for (int t = threadIdx.x; t < npad; t += 512)
+    key[t] = t < k ? ((unsigned long long)x[i * ldx + t] << 13) | (unsigned)t : ~0ull;
+  __syncthreads();
+  for (int size = 2; size <= npad; size <<= 1) {
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      for (int t = threadIdx.x; t < npad / 2; t += 512) {  // pair t: lo has bit `stride` clear
+        const int lo = 2 * t - (t & (stride - 1)), hi = lo + stride;
+        const unsigned long long a = key[lo], b = key[hi];
+        if ((a > b) == ((lo & size) == 0)) {
+          key[lo] = b;
+          key[hi] = a;
+        }
+      }
+      __syncthreads();
+    }
+  }
+  for (int t = threadIdx.x; t < k; t += 512) {
+    const unsigned long long v = key[t];
+    sorted[i * k + t] = (int64_t)v >> 13;
+    col[i * k + t] = (int64_t)(v & 8191ull);
+  }
+}
+
 int kind_of(int model) {
   switch (model) {
     case KGE_COMPLEX:
@@ -709,6 +739,19 @@ extern "C" int kge_bucket_count(const int64_t* idx, int64_t n, int64_t nbuckets,
   KGE_REQUIRE(n >= 0 && nbuckets >= 0 && (n == 0 || (idx && counts)));
   if (n == 0) return 0;
   bucket_count_kernel<<<dim3((unsigned)((n + 255) / 256)), dim3(256), 0, as_stream(stream)>>>(idx, n, nbuckets, counts);
+  KGE_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int kge_sort_rows(const int64_t* x, int64_t ldx, int64_t n, int64_t k, int64_t* sorted, int64_t* col,
+                             void* stream) {
+  KGE_REQUIRE(n >= 0 && k >= 0 && k <= 8192 && n < (1LL << 31) && ldx >= k);
+  KGE_REQUIRE(n == 0 || k == 0 || (x && sorted && col));
+  if (n == 0 || k == 0) return 0;
+  int npad = 2;
+  while (npad < k) npad <<= 1;
+  sort_rows_kernel<<<dim3((unsigned)n), dim3(512), (size_t)npad * 8, as_stream(stream)>>>(x, ldx, (int)k, npad, sorted,
+                                                                                          col);
   KGE_CHECK_LAUNCH();
   return 0;
 }

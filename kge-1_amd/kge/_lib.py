@@ -76,6 +76,7 @@ SIGNATURES = {
                                 _I64, _P, _I64, _P], _I),
     "kge_bucket_scatter": ([_P, _I64, _P, _P, _P], _I),
     "kge_bucket_count": ([_P, _I64, _I64, _P, _P], _I),
+    "kge_sort_rows": ([_P, _I64, _I64, _I64, _P, _P, _P], _I),
     "kge_stage_i64": ([_P, _P, _I64, _P], _I),
     "kge_rank_hist_multi": ([_P, _P, _I64, _I64, _I, _P, _P, _I64, _P], _I),
     "kge_rank_metrics": ([_P, _I64, _I64, _I64, _I, _P, _P], _I),
@@ -653,6 +654,19 @@ def score_cand(model, l_norm, direction, q, ent, cand, out=None):
     _check(lib().kge_score_cand(model, float(l_norm), direction, ptr(q), rows(q), ptr(ent), rows(ent), ptr(cand),
                                 cand.stride(0), n, k, d, ptr(o), rows(o), stream()), "kge_score_cand")
     return o
+
+
+def sort_rows(x):
+    """kge_sort_rows: (ids of every row ascending, the positions they came from) of an int64
+    [n, k <= 8192] matrix of non-negative ids -- torch.sort(x, 1, stable=True) in one launch."""
+    require_device(x)
+    if x.dtype != torch.int64 or x.dim() != 2 or x.stride(1) != 1 or x.shape[1] > 8192:
+        raise ValueError("sort_rows: an int64 [n, k <= 8192] matrix with unit column stride")
+    n, k = x.shape
+    srt, col = torch.empty(n, k, dtype=torch.int64, device=x.device), torch.empty(n, k, dtype=torch.int64,
+                                                                                  device=x.device)
+    _check(lib().kge_sort_rows(ptr(x), x.stride(0) if n > 1 else k, n, k, ptr(srt), ptr(col), stream()), "kge_sort_rows")
+    return srt, col
 
 
 def score_cand_ordered(model, l_norm, direction, q, ent, cand, col, out=None):

@@ -143,6 +143,19 @@ def test_score_cand_ordered_lists_vs_plain(L, model, ln, d):
         assert (gr - d_rel).abs().max() <= 2e-5 * d_rel.abs().max()
 
 
+@pytest.mark.parametrize("n,k,ld", [(5, 1, 1), (3, 2, 7), (64, 1025, 1025), (9, 300, 301), (2, 8192, 8192), (1, 777, 777)])
+def test_sort_rows_is_torch_stable_sort(L, n, k, ld):
+    """kge_sort_rows (bitonic network in LDS) against torch.sort(stable=True): ids and positions,
+    with many repeated ids per row."""
+    torch.manual_seed(n + k)
+    buf = torch.randint(0, max(2, k // 3), (n, ld), device="cuda")
+    buf[0, :k] = 2 ** 40 + 5  # large ids; a row of equal ids keeps its order
+    x = buf[:, :k]
+    srt, col = L.sort_rows(x)
+    exp = torch.sort(x, dim=1, stable=True)
+    assert torch.equal(srt, exp.values) and torch.equal(col, exp.indices)
+
+
 @pytest.mark.parametrize("num_neg", [31, 255])
 @pytest.mark.parametrize("model", ["rotate", "complex", "transe", "cp", "simple"])
 def test_ns_implementations_agree(model, num_neg):
