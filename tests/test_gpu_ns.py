@@ -103,7 +103,7 @@ def _ns_job(model, impl, num_neg=31, dim=64, shared=False, filtering=False, E=50
 
 @pytest.mark.parametrize("model,ln", [("distmult", 1.0), ("transe", 1.0), ("transe", 2.0), ("rotate", 1.0),
                                       ("rotate", 2.0)])
-@pytest.mark.parametrize("d", [128, 1024])
+@pytest.mark.parametrize("d", [128, 1024, 30])  # 30: rows float4 loads cannot read (scalar kernels)
 def test_score_cand_ordered_lists_vs_plain(L, model, ln, d):
     """The engine orders long candidate lists (ascending per query, kge_score_cand_ordered /
     kge_score_cand_bwd_q_ordered) when the rows repeat across queries: the scores must be the
@@ -136,8 +136,9 @@ def test_score_cand_ordered_lists_vs_plain(L, model, ln, d):
             assert torch.equal(out, s)
             dq = torch.empty_like(q)
             d_ent, d_rel = torch.zeros_like(ent), torch.zeros_like(rel)
-            assert L.score_cand_bwd_ent(kind, ln, direction, q, ent, cand, s, w, d_ent)
-            L.score_cand_bwd(kind, ln, direction, q, ent, cand, s, w, dq, None)
+            grouped = L.score_cand_bwd_ent(kind, ln, direction, q, ent, cand, s, w, d_ent)
+            assert grouped == (d % 8 == 0)
+            L.score_cand_bwd(kind, ln, direction, q, ent, cand, s, w, dq, None if grouped else d_ent)
             L.prep_query_bwd(kind, direction, ent, eidx, rel, ridx, n, d, d_r, dq, d_ent, d_rel)
         assert (ge - d_ent).abs().max() <= 2e-5 * d_ent.abs().max()
         assert (gr - d_rel).abs().max() <= 2e-5 * d_rel.abs().max()
