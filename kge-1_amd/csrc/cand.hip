@@ -114,9 +114,36 @@ __global__ void __launch_bounds__(NT) cand_kernel(bool l1, float sigma, const fl
   }
 }
 
+// Sum over the wave without LDS traffic: four DPP steps leave every lane with the sum of its row of
+// 16 lanes, the four row sums are read by v_readlane.  (wave_sum's ds_bpermute butterfly is a
+// chain of six LDS round trips per candidate row, which the one-row-in-flight loop cannot hide.)
+__device__ __forceinline__ float dpp_add(float v, const int ctrl_tag) {
+  const int x = __builtin_bit_cast(int, v);
+  int y;
+  switch (ctrl_tag) {  // the control word must be an immediate
+    case 0: y = __builtin_amdgcn_update_dpp(0, x, 0xB1, 0xF, 0xF, false); break;   // quad_perm [1,0,3,2]
+    case 1: y = __builtin_amdgcn_update_dpp(0, x, 0x4E, 0xF, 0xF, false); break;   // quad_perm [2,3,0,1]
+    case 2: y = __builtin_amdgcn_update_dpp(0, x, 0x141, 0xF, 0xF, false); break;  // row_half_mirror
+    default: y = __builtin_amdgcn_update_dpp(0, x, 0x140, 0xF, 0xF, false); break; // row_mirror
+  }
+  return v + __builtin_bit_cast(float, y);
+}
+
+__device__ __forceinline__ float wave_sum_rows(float v) {
+  v = dpp_add(v, 0);
+  v = dpp_add(v, 1);
+  v = dpp_add(v, 2);
+  v = dpp_add(v, 3);
+  const int x = __builtin_bit_cast(int, v);
+  const float r0 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(x, 0));
+  const float r1 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(x, 16));
+  const float r2 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(x, 32));
+  const float r3 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(x, 48));
+  return (r0 + r1) + (r2 + r3);
+}
+
 // The same scores with the query's slice in registers (lane owns elements ch*256 + lane*4 .. +3,
-// as the backward kernels) and a whole candidate row requested at once.  Per lane the partial
-// sums are formed in the same order as cand_kernel<KIND, true> forms them: the same bits.
+// as the backward kernels) and a whole candidate row requested at once.
 template <int KIND, int NCH>
 __global__ void __launch_bounds__(NT) cand_fwd_kernel(bool l1, float sigma, const float* __restrict__ q, int64_t ldq,
                                                       const float* __restrict__ ent, int64_t ld_ent,
@@ -163,7 +190,7 @@ __global__ void __launch_bounds__(NT) cand_fwd_kernel(bool l1, float sigma, cons
       }
       if (own[ch]) acc += t;
     }
-    return wave_sum(acc);
+    return wave_sum_rows(acc);
   };
   auto put = [&](int c, float a) {
     if (lane == 0 && c < k) out[i * ldo + (coli ? coli[c] : c)] = finish<KIND>(a, l1);
