@@ -301,20 +301,32 @@ __global__ void __launch_bounds__(NT) cand_bwd_q_kernel(bool l1, float sigma, co
   // A candidate is a chain of dependent loads (column -> gradient / norm, id -> row): the next
   // candidate's gradient, norm and id are fetched while this one's row is on its way.  One row
   // per wave in flight, no more (see cand_fwd_kernel).
-  int c = w;
-  if (c < k) {
-    float gc_n, inv_n;
-    meta(c, gc_n, inv_n);
-    int64_t id_n = ci[c];
-    for (; c < k; c += NW) {
-      const float gc = gc_n, inv = inv_n;
-      float4 ev[NCH][P];
-      rows(ev, id_n);
-      if (c + NW < k) {
-        meta(c + NW, gc_n, inv_n);
-        id_n = ci[c + NW];
+  // The distance kinds spend enough arithmetic per row for the waves of a workgroup to drift apart
+  // along the candidate list, and with them the table rows they share with the XCD's other
+  // workgroups: a barrier every 16 candidates keeps them together (RotatE-L1 160 -> 128 us at
+  // 512 x 1,025 x 1,024; dot scores, 96 us without, lose 10 us to it).  Uniform trip count.
+  constexpr int SYNC_EVERY = KIND == K_DOT ? 0 : 16;
+  {
+    const int iters = (k + NW - 1) / NW;
+    float gc_n = 0.f, inv_n = 0.f;
+    int64_t id_n = 0;
+    if (w < k) {
+      meta(w, gc_n, inv_n);
+      id_n = ci[w];
+    }
+    for (int it = 0; it < iters; ++it) {
+      const int c = w + it * NW;
+      if (c < k) {
+        const float gc = gc_n, inv = inv_n;
+        float4 ev[NCH][P];
+        rows(ev, id_n);
+        if (c + NW < k) {
+          meta(c + NW, gc_n, inv_n);
+          id_n = ci[c + NW];
+        }
+        if (gc != 0.f) accumulate(ev, gc, inv);
       }
-      if (gc != 0.f) accumulate(ev, gc, inv);
+      if (SYNC_EVERY > 0 && (it & (SYNC_EVERY - 1)) == SYNC_EVERY - 1) __syncthreads();
     }
   }
   // cross-wave reduction through LDS (each wave's partial row), then one store of dq_i
