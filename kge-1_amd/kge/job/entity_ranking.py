@@ -124,6 +124,11 @@ class EntityRankingJob(EvaluationJob):
         self.triples = self.dataset.split(self.eval_split).long()
         tri = self.triples.numpy()
         E = self.dataset.num_entities()
+        # triples per launch group: eval.batch_size, raised to engine.eval_batch_size while the
+        # [2B, chunk] block of a group stays below 8 GiB as fp32 scores
+        chunk = self.config.get("entity_ranking.chunk_size")
+        cols = E if chunk is None or chunk <= 0 else min(E, chunk)
+        self._bs = max(self.batch_size, min(int(self.config.get("engine.eval_batch_size")), (1 << 30) // max(cols, 1)))
         self.use_test = "test" not in self.filter_splits and self.filter_with_test
         self.rankings = ["_raw", "_filt", "_filt_test"] if self.use_test else ["_raw", "_filt"]
         f_sp, f_po = self._filter_index(self.filter_splits)
@@ -147,8 +152,8 @@ class EntityRankingJob(EvaluationJob):
         # (s, p, ?) / (?, p, o) queries of a batch read ONE contiguous entity-index vector and one
         # relation-index vector (no per-batch gather or concatenation)
         se, sp = [], []
-        for b0 in range(0, len(self.triples), self.batch_size):
-            t = self.triples[b0:b0 + self.batch_size]
+        for b0 in range(0, len(self.triples), self._bs):
+            t = self.triples[b0:b0 + self._bs]
             se += [t[:, 0], t[:, 2]]
             sp += [t[:, 1], t[:, 1]]
         self._stack_e = torch.cat(se).contiguous().to(dev) if se else torch.zeros(0, dtype=torch.int64, device=dev)
@@ -363,9 +368,9 @@ class EntityRankingJob(EvaluationJob):
         if (sharded is not None and getattr(sharded.ops, "rank_rows", None) is not None
                 and sharded.rank_block_applies(self._two_sided)):
             return self._rank_batches_sharded(N, sharded, nrank, hists_sharded, group_hists, ranks_out)
-        for bi, b0 in enumerate(range(0, N, self.batch_size)):
+        for bi, b0 in enumerate(range(0, N, self._bs)):
             with (self._streams.batch(bi) if sharded is None else contextlib.nullcontext()):
-                b1 = min(N, b0 + self.batch_size)
+                b1 = min(N, b0 + self._bs)
                 B = b1 - b0
                 s, o = self._stack_e[2 * b0:2 * b0 + B], self._stack_e[2 * b0 + B:2 * b0 + 2 * B]
                 p, p_po = self._stack_p[2 * b0:2 * b0 + B], self._stack_p[2 * b0 + B:2 * b0 + 2 * B]
@@ -468,7 +473,7 @@ class EntityRankingJob(EvaluationJob):
         from ..sharded import all_reduce
 
         G = max(1, int(self.config.get("engine.eval_exchange_group")))
-        bs = self.batch_size
+        bs = self._bs
         (fp_sp, fp_po, f_col), tstack = self._stacked
         R = self.dataset.num_relations()
         for g0 in range(0, N, G * bs):

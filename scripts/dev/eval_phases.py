@@ -31,7 +31,9 @@ def main():
     c.set("engine.eval_streams", ns)
     c.set("verbose", False)
     c.set("eval.split", "test")
-    c.set("eval.batch_size", 1024)
+    c.set("eval.batch_size", int(os.environ.get("EVAL_BATCH", "1024")))
+    if "ENGINE_EVAL_BATCH" in os.environ:
+        c.set("engine.eval_batch_size", int(os.environ["ENGINE_EVAL_BATCH"]))
     c.set("entity_ranking.metrics_per.head_and_tail", hat)
     if len(sys.argv) > 3:
         c.set("engine.fused_rank", bool(int(sys.argv[3])))

@@ -24,6 +24,11 @@ c.set("train.optimizer", "Adagrad")
 c.set("train.optimizer_args", {"lr": 0.2})
 c.set("train.batch_size", 1024 if train_type == "1vsAll" else 512)
 c.set("verbose", False)
+if os.environ.get("KGE_PROF_OPTIONS") == "dropout_penalties":  # what tuned LibKGE configurations carry
+    c.set("lookup_embedder.dropout", 0.2)
+    c.set("lookup_embedder.regularize_args.weighted", True)
+    c.set(f"{model_name}.entity_embedder.regularize_weight", 1e-6)
+    c.set(f"{model_name}.relation_embedder.regularize_weight", 1e-6)
 if os.environ.get("KGE_NO_GRAPH") == "1":  # per-kernel times of the eager step, for comparison
     c.set("engine.graph_step", False)
 ds = Dataset.synthetic(c, "fb15k-237" if train_type == "1vsAll" else "wn18rr", seed=0)

@@ -151,6 +151,7 @@ def eval_job(f, tag, precision, extra=None):
     c.set("engine.precision", precision.replace("_refined", ""))
     c.set("engine.eval_precision", precision)
     c.set("eval.batch_size", meta["batch_size"])
+    c.set("engine.eval_batch_size", 0)  # the batches of eval.batch_size as they are
     c.set("eval.split", "valid")
     c.set("entity_ranking.chunk_size", -1 if tag == "full" else meta["chunk8"])
     c.set("dataset.num_entities", meta["E"])

@@ -43,6 +43,7 @@ def base_config(model, dim, E, R, extra=None):
     c.set("dataset.num_entities", E)
     c.set("dataset.num_relations", R)
     c.set("lookup_embedder.dim", dim)
+    c.set("engine.eval_batch_size", 0)  # evaluation in the batches of eval.batch_size, as the fixtures were captured
     for k, v in (extra or {}).items():
         c.set(k, v)
     return c

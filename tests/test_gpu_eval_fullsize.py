@@ -58,3 +58,40 @@ def test_entity_ranking_fb15k237_size_dyadic(precision):
         assert trace[k] == pytest.approx(v, rel=1e-6, abs=1e-9), k
     # a non-degenerate ranking: ties present, ranks spread
     assert trace["mean_reciprocal_rank_filtered"] > 0.0 and len(np.unique(ranks["o_filt"])) > 100
+
+
+def test_engine_eval_batch_size_changes_the_grouping_not_the_result():
+    """eval.batch_size 100 (the reference's default, config-default.yaml:324) with and without
+    the engine's larger launch groups (engine.eval_batch_size): identical ranks and metrics, and
+    the trace counts the batches of eval.batch_size either way."""
+    from kge import Config, Dataset, KgeModel
+    from kge.job import EntityRankingJob
+
+    traces, ranks, groups = [], [], []
+    for engine_bs in (0, 1024):
+        c = Config()
+        c.set("model", "complex")
+        c._import("complex")
+        c.set("job.device", "cuda")
+        c.set("lookup_embedder.dim", 128)
+        c.set("lookup_embedder.initialize_args", {"mean": 0.0, "std": 0.1})
+        c.set("eval.split", "valid")
+        c.set("eval.batch_size", 100)
+        c.set("engine.eval_batch_size", engine_bs)
+        c.set("verbose", False)
+        ds = Dataset.synthetic(c, "toy", seed=0, num_entities=3000, num_relations=9, sizes=(20000, 2345, 500))
+        torch.manual_seed(0)
+        model = KgeModel.create(c, ds)
+        model.eval()
+        job = EntityRankingJob(c, ds, model=model)
+        job.capture_ranks = True
+        traces.append(job.run())
+        ranks.append(job.ranks)
+        groups.append(job._bs)
+    assert groups == [100, 1024]
+    assert traces[0]["batches"] == traces[1]["batches"] == 24 and traces[0]["size"] == 2345
+    for k in ranks[0]:
+        np.testing.assert_array_equal(ranks[0][k], ranks[1][k], err_msg=k)
+    for k, v in traces[0].items():
+        if k not in ("epoch_time",) and isinstance(v, float):
+            assert traces[1][k] == v, k

@@ -265,6 +265,7 @@ def test_job_loop_memorises_its_training_triples(train_type):
     c.set("train.max_epochs", 40)
     c.set("valid.every", 20)
     c.set("eval.batch_size", 100)
+    c.set("engine.eval_batch_size", 0)  # the batches of eval.batch_size as they are
     c.set("dataset.num_entities", E)
     c.set("dataset.num_relations", R)
     c.set("verbose", False)

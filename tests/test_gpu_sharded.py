@@ -122,6 +122,7 @@ def test_sharded_jobs_world1_rccl_match_unsharded_jobs(L):
             c.set("train.optimizer_args", {"lr": 0.1})
             c.set("valid.every", 0)
             c.set("eval.batch_size", 100)
+            c.set("engine.eval_batch_size", 0)  # the batches of eval.batch_size as they are
             c.set("random_seed.torch", 3)
             c.set("engine.precision", "fp32")
             c.set("engine.graph_step", False)
@@ -493,6 +494,7 @@ def _jobs_config(mode, precision="fp32"):
     c.set("train.optimizer_args", {"lr": 0.1})
     c.set("valid.every", 0)
     c.set("eval.batch_size", 100)
+    c.set("engine.eval_batch_size", 0)  # the batches of eval.batch_size as they are
     c.set("random_seed.torch", 3)
     c.set("engine.precision", precision)
     c.set("engine.graph_step", False)

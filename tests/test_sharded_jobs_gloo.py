@@ -94,6 +94,7 @@ def _config():
     c.set("valid.every", 1)
     c.set("valid.early_stopping.patience", 0)
     c.set("eval.batch_size", 7)
+    c.set("engine.eval_batch_size", 0)  # the batches of eval.batch_size as they are
     c.set("engine.eval_exchange_group", 3)  # several exchange groups per evaluation, the last one ragged
     c.set("random_seed.torch", SEED)
     return c
