@@ -689,13 +689,13 @@ def gen_kvsall_fixture(with_so=False, loss="kl", loss_arg=float("nan")):
     return fn
 
 
-def gen_ns_fixture(model_key, loss="kl", loss_arg=float("nan"), extra=None, tag=""):
+def gen_ns_fixture(model_key, loss="kl", loss_arg=float("nan"), extra=None, tag="", nneg=8):
     from kge.job import TrainingJob
 
     E, R, splits = make_dataset_splits()
     folder = os.path.join(TMP, f"ds_ns_{model_key}")
     write_dataset(folder, E, R, splits)
-    dim, bs, nb, nneg = 32, 64, 2, 8
+    dim, bs, nb = 32, 64, 2
     config = ds_config(model_key, dim, folder, E, R, {
         "train.type": "negative_sampling", "train.optimizer": "Adagrad", "train.optimizer_args": {"lr": 0.1},
         "train.loss": loss, "train.loss_arg": loss_arg, "train.batch_size": bs,
@@ -1053,6 +1053,10 @@ def main():
              "ns_simple_se": lambda: gen_ns_fixture("simple", "se"),
              "ns_complex_sparse": lambda: gen_ns_fixture("complex", extra={"lookup_embedder.sparse": True},
                                                          tag="_sparse"),
+             # 128 negatives per slot: candidate lists long enough for the engine to order them
+             "ns_rotate_n128": lambda: gen_ns_fixture("rotate", tag="_n128", nneg=128),
+             "ns_complex_n128": lambda: gen_ns_fixture("complex", tag="_n128", nneg=128),
+             "ns_transe_n128": lambda: gen_ns_fixture("transe", tag="_n128", nneg=128),
              "onevsall_bce": gen_1vsall_bce_fixture,
              "penalties": gen_penalty_fixture, "eval_rescal128": gen_eval_rescal128,
              "train_large": gen_train_fixture_large}

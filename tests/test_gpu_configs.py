@@ -495,15 +495,28 @@ def test_c3_kvsall_step_at_wn18rr_size_vs_float64():
 
 
 @pytest.mark.parametrize("impl", ["triple", "all", "batch"])
-@pytest.mark.parametrize("model", ["rotate", "complex"])
-def test_c4_negative_sampling_steps_vs_reference(model, impl):
+@pytest.mark.parametrize("fixture", ["rotate", "complex", "rotate_n128", "complex_n128", "transe_n128"])
+def test_c4_negative_sampling_steps_vs_reference(fixture, impl):
     """Two reference negative-sampling batches (KL with the positive in column 0, eight
     negatives per corrupted slot, Adagrad) with the reference sampler's negatives injected:
-    per-batch loss and the tables after both steps, for every scoring implementation."""
+    per-batch loss and the tables after both steps, for every scoring implementation.  The
+    _n128 fixtures carry 128 negatives per slot: lists the "triple" implementation scores in
+    ascending candidate order (kge_score_cand_ordered), results in the reference's columns."""
+    from kge import engine
     from kge.job import TrainingJob
 
-    f = np.load(os.path.join(GOLDEN, f"train_ns_{model}.npz"))
+    f = np.load(os.path.join(GOLDEN, f"train_ns_{fixture}.npz"))
     meta = json.loads(str(f["meta"]))
+    model = meta["model"]
+    ordered = engine._cand_order(torch.zeros(meta["batch_size"], 1 + meta["num_negatives"], dtype=torch.int64,
+                                             device="cuda"), meta["E"]) is not None
+    assert ordered == fixture.endswith("_n128")
+    if model == "transe" and impl != "triple":
+        # the fixture is the reference's "triple" run: score_spo = -pairwise_distance (eps 1e-6
+        # inside the norm, transe.py:17), while "all" / "batch" score with -cdist (no eps,
+        # transe.py:19-23) -- the L1 gradients sign(x + eps) and sign(x) differ wherever
+        # |x| < 1e-6, a handful of the 5e5 components of such a step, in the reference too
+        pytest.skip("TransE-L1: the reference's own implementations differ at |x| < eps")
     extra = {"train.type": "negative_sampling", "train.optimizer": "Adagrad",
              "train.optimizer_args": {"lr": meta["lr"]}, "train.batch_size": meta["batch_size"],
              "negative_sampling.num_samples.s": meta["num_negatives"], "negative_sampling.num_samples.o": -1,

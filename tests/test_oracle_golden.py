@@ -187,14 +187,15 @@ def test_refseq_kvsall_step_reproduces_reference_trajectory():
     np.testing.assert_allclose(rel.detach().numpy(), f["rel1"], atol=1e-6)
 
 
-def test_refseq_ns_step_reproduces_reference_trajectory():
+@pytest.mark.parametrize("fixture", ["train_ns_rotate.npz", "train_ns_rotate_n128.npz"])
+def test_refseq_ns_step_reproduces_reference_trajectory(fixture):
     """The CPU negative-sampling step replica (refseq.train_step_ns_triple, bench.py's
     cpu_baseline C4 leg) against the reference-captured RotatE steps with the reference's
-    sampled negatives injected ("triple" implementation, kl loss)."""
+    sampled negatives injected ("triple" implementation, kl loss; 8 and 128 negatives per slot)."""
     import torch
     from oracle import refseq
 
-    f = np.load(os.path.join(GOLDEN, "train_ns_rotate.npz"))
+    f = np.load(os.path.join(GOLDEN, fixture))
     meta = json.loads(str(f["meta"]))
     assert meta["implementation"] == "triple" and meta["loss"] == "kl"
     torch.set_num_threads(4)
