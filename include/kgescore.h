@@ -408,6 +408,14 @@ int kge_bucket_scatter(const int64_t* idx, int64_t n, int64_t* cursor, int64_t* 
 int kge_sort_rows(const int64_t* x, int64_t ldx, int64_t n, int64_t k, int64_t* sorted, int64_t* col,
                   void* stream);
 
+/* The order / seg_ptr input of kge_score_cand_bwd_ent from candidate lists that kge_sort_rows has
+ * sorted (srt, col: contiguous [n, k], n <= 4096): seg_ptr[nbuckets + 1] and order[n * k] with
+ * order[slot] = i * k + col[i, position] -- the counting sort of kge_bucket_count +
+ * exclusive scan + kge_bucket_scatter in one launch and without global atomics (every workgroup
+ * owns a range of ids, which is one contiguous run of each sorted row). */
+int kge_group_sorted_rows(const int64_t* srt, const int64_t* col, int64_t n, int64_t k, int64_t nbuckets,
+                          int64_t* seg_ptr, int64_t* order, void* stream);
+
 /* The bucket counts that go with it: counts[idx[t]] += 1 for t in [0, n) (int64 atomics; the
  * caller zeroes counts; indexes outside [0, nbuckets) are skipped) -- torch.bincount without its
  * host round trip for the maximum. */

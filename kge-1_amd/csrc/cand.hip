@@ -534,6 +534,82 @@ __global__ void __launch_bounds__(512) sort_rows_kernel(const int64_t* __restric
   }
 }
 
+// The pairs (i, c) grouped by candidate entity, from candidate lists that are already sorted per
+// row (sort_rows_kernel): a workgroup owns the entities [e0, e0 + R).  In every row its entities
+// are one contiguous run, found by a binary search; the number of pairs before the run, summed over
+// the rows, is where the workgroup's part of `order` starts -- so the counting sort needs no global
+// counters: counts and write cursors of the R entities live in LDS.  seg_ptr[e] = first slot of
+// entity e in order, order[slot] = i * k + col[i, position] (the pair in the caller's columns; the
+// order inside a group is not specified).  Ids outside [0, E) are left out.
+constexpr int GROUP_NT = 512, GROUP_RMAX = 1024;
+__global__ void __launch_bounds__(GROUP_NT) group_sorted_rows_kernel(const int64_t* __restrict__ srt,
+                                                                     const int64_t* __restrict__ col, int n, int k,
+                                                                     int64_t E, int R, int64_t* __restrict__ seg_ptr,
+                                                                     int64_t* __restrict__ order) {
+  extern __shared__ int run_lo[];  // [n] first position of the run, then [n] its end
+  __shared__ int count[GROUP_RMAX], cursor[GROUP_RMAX];
+  __shared__ long long part[GROUP_NT / 64];
+  int* run_hi = run_lo + n;
+  const int64_t e0 = (int64_t)blockIdx.x * R, e1 = e0 + R < E ? e0 + R : E;
+  const int nr = (int)(e1 - e0);
+  for (int r = threadIdx.x; r < nr; r += GROUP_NT) count[r] = 0;
+  __syncthreads();
+  long long before = 0;
+  for (int i = threadIdx.x; i < n; i += GROUP_NT) {
+    const int64_t* row = srt + (int64_t)i * k;
+    int a = 0, b = k;
+    while (a < b) {  // first position with an id >= e0
+      const int m = (a + b) >> 1;
+      if (row[m] < e0) a = m + 1;
+      else b = m;
+    }
+    int j = a;
+    for (; j < k; ++j) {
+      const int64_t e = row[j];
+      if (e < e0 || e >= e1) break;
+      atomicAdd(&count[(int)(e - e0)], 1);
+    }
+    run_lo[i] = a;
+    run_hi[i] = j;
+    before += a;
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) before += __shfl_xor(before, off, 64);
+  if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = before;
+  __syncthreads();
+  long long base = 0;
+#pragma unroll
+  for (int w = 0; w < GROUP_NT / 64; ++w) base += part[w];
+  if (threadIdx.x < 64) {  // exclusive scan of the counts: lane l takes `per` consecutive entities
+    const int per = (nr + 63) / 64, r0 = threadIdx.x * per, r1 = r0 + per < nr ? r0 + per : nr;
+    int sum = 0;
+    for (int r = r0; r < r1; ++r) sum += count[r];
+    int incl = sum;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+      const int v = __shfl_up(incl, off, 64);
+      if ((int)threadIdx.x >= off) incl += v;
+    }
+    int run = incl - sum;
+    for (int r = r0; r < r1; ++r) {
+      cursor[r] = run;
+      seg_ptr[e0 + r] = base + run;
+      run += count[r];
+    }
+    if (threadIdx.x == 63 && e1 == E) seg_ptr[E] = base + incl;
+  }
+  __syncthreads();
+  const int64_t total = (int64_t)n * k;
+  for (int i = threadIdx.x; i < n; i += GROUP_NT) {
+    const int64_t* row = srt + (int64_t)i * k;
+    const int64_t* ci = col + (int64_t)i * k;
+    for (int j = run_lo[i]; j < run_hi[i]; ++j) {
+      const int64_t slot = base + atomicAdd(&cursor[(int)(row[j] - e0)], 1);
+      if (slot < total) order[slot] = (int64_t)i * k + ci[j];
+    }
+  }
+}
+
 int kind_of(int model) {
   switch (model) {
     case KGE_COMPLEX:
@@ -791,6 +867,20 @@ extern "C" int kge_sort_rows(const int64_t* x, int64_t ldx, int64_t n, int64_t k
   while (npad < k) npad <<= 1;
   sort_rows_kernel<<<dim3((unsigned)n), dim3(512), (size_t)npad * 8, as_stream(stream)>>>(x, ldx, (int)k, npad, sorted,
                                                                                           col);
+  KGE_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int kge_group_sorted_rows(const int64_t* srt, const int64_t* col, int64_t n, int64_t k, int64_t nbuckets,
+                                     int64_t* seg_ptr, int64_t* order, void* stream) {
+  KGE_REQUIRE(n >= 0 && n <= 4096 && k >= 0 && k < (1LL << 31) && nbuckets > 0 && nbuckets < (1LL << 40) && seg_ptr);
+  KGE_REQUIRE(n == 0 || k == 0 || (srt && col && order));
+  int64_t r = (nbuckets + 255) / 256;
+  r = r < 32 ? 32 : (r > GROUP_RMAX ? GROUP_RMAX : r);
+  const int64_t nblocks = (nbuckets + r - 1) / r;
+  KGE_REQUIRE(nblocks < (1LL << 31));
+  group_sorted_rows_kernel<<<dim3((unsigned)nblocks), dim3(GROUP_NT), (size_t)(2 * n + 1) * sizeof(int),
+                             as_stream(stream)>>>(srt, col, (int)n, (int)k, nbuckets, (int)r, seg_ptr, order);
   KGE_CHECK_LAUNCH();
   return 0;
 }

@@ -77,6 +77,7 @@ SIGNATURES = {
     "kge_bucket_scatter": ([_P, _I64, _P, _P, _P], _I),
     "kge_bucket_count": ([_P, _I64, _I64, _P, _P], _I),
     "kge_sort_rows": ([_P, _I64, _I64, _I64, _P, _P, _P], _I),
+    "kge_group_sorted_rows": ([_P, _P, _I64, _I64, _I64, _P, _P, _P], _I),
     "kge_stage_i64": ([_P, _P, _I64, _P], _I),
     "kge_rank_hist_multi": ([_P, _P, _I64, _I64, _I, _P, _P, _I64, _P], _I),
     "kge_rank_metrics": ([_P, _I64, _I64, _I64, _I, _P, _P], _I),
@@ -711,10 +712,23 @@ def score_cand_bwd(model, l_norm, direction, q, ent, cand, s, g, dq, d_ent):
                                     rows(d_ent) if d_ent is not None else 0, stream()), "kge_score_cand_bwd")
 
 
-def score_cand_bwd_ent(model, l_norm, direction, q, ent, cand, s, g, d_ent) -> bool:
+def group_sorted_rows(srt, col, num_buckets):
+    """kge_group_sorted_rows: (order, seg_ptr) of the pairs of sorted candidate lists grouped by
+    candidate id (srt, col from sort_rows; at most 4096 rows)."""
+    n, k = srt.shape
+    seg_ptr = torch.empty(num_buckets + 1, dtype=torch.int64, device=srt.device)
+    order = torch.empty(n * k, dtype=torch.int64, device=srt.device)
+    _check(lib().kge_group_sorted_rows(ptr(srt), ptr(col), n, k, num_buckets, ptr(seg_ptr), ptr(order), stream()),
+           "kge_group_sorted_rows")
+    return order, seg_ptr
+
+
+def score_cand_bwd_ent(model, l_norm, direction, q, ent, cand, s, g, d_ent, sorted_lists=None) -> bool:
     """d_ent += d(sum g * scores)/d ent without fp32 atomics: the n*k pairs are grouped by
-    entity with a counting sort (bincount, exclusive scan, kge_bucket_scatter) -- one group
-    slot per entity, fixed size, no host sync -- and each entity row is reduced once.
+    entity with a counting sort -- one group slot per entity, fixed size, no host sync -- and
+    each entity row is reduced once.  sorted_lists: (srt, col) of sort_rows(cand) when the
+    caller has them (the grouping is then one launch, kge_group_sorted_rows; otherwise
+    kge_bucket_count, an exclusive scan and kge_bucket_scatter).
     Returns False (nothing done) when the layout is not supported."""
     unit = q.shape[1] // 2 if model == ROTATE else q.shape[1]
     if unit % 4 or unit > 2048 or rows(q) % 4 or rows(ent) % 4 or rows(d_ent) % 4 or q.data_ptr() % 16 \
@@ -724,12 +738,16 @@ def score_cand_bwd_ent(model, l_norm, direction, q, ent, cand, s, g, d_ent) -> b
     n, k = cand.shape
     flat = cand.reshape(-1)
     E = ent.shape[0]
-    seg_ptr = torch.zeros(E + 1, dtype=torch.int64, device=cand.device)
-    _check(lib().kge_bucket_count(ptr(flat), flat.numel(), E, ptr(seg_ptr[1:]), stream()), "kge_bucket_count")
-    seg_ptr.cumsum_(0)
-    cursor = seg_ptr[:-1].clone()
-    order = torch.empty_like(flat)
-    _check(lib().kge_bucket_scatter(ptr(flat), flat.numel(), ptr(cursor), ptr(order), stream()), "kge_bucket_scatter")
+    if sorted_lists is not None and sorted_lists[0].numel() and n <= 4096:
+        order, seg_ptr = group_sorted_rows(sorted_lists[0], sorted_lists[1], E)
+    else:
+        seg_ptr = torch.zeros(E + 1, dtype=torch.int64, device=cand.device)
+        _check(lib().kge_bucket_count(ptr(flat), flat.numel(), E, ptr(seg_ptr[1:]), stream()), "kge_bucket_count")
+        seg_ptr.cumsum_(0)
+        cursor = seg_ptr[:-1].clone()
+        order = torch.empty_like(flat)
+        _check(lib().kge_bucket_scatter(ptr(flat), flat.numel(), ptr(cursor), ptr(order), stream()),
+               "kge_bucket_scatter")
     _check(lib().kge_score_cand_bwd_ent(model, float(l_norm), direction, ptr(q), rows(q), ptr(ent), rows(ent),
                                         ptr(cand), n, k, q.shape[1], ptr(order), ptr(seg_ptr), ent.shape[0], ptr(s),
                                         rows(s) if s is not None else 0, ptr(g), rows(g), ptr(d_ent), rows(d_ent),

@@ -717,7 +717,7 @@ class _ScoreCand(torch.autograd.Function):
         ent_w = window(kind, direction, ent)
         d_ent_w = window(kind, direction, d_ent) if d_ent is not None else None
         ent_done = d_ent is not None and L.score_cand_bwd_ent(kind, l_norm, direction, q, ent_w, cand, s, g,
-                                                              d_ent_w)
+                                                              d_ent_w, sorted_lists=(srt, col))
         if not (dq is not None and srt.numel() and (ent_done or d_ent is None)
                 and L.score_cand_bwd_q_ordered(kind, l_norm, direction, q, ent_w, srt, col, s, g, dq)):
             L.score_cand_bwd(kind, l_norm, direction, q, ent_w, cand, s, g, dq, None if ent_done else d_ent_w)

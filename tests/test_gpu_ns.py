@@ -157,6 +157,29 @@ def test_sort_rows_is_torch_stable_sort(L, n, k, ld):
     assert torch.equal(srt, exp.values) and torch.equal(col, exp.indices)
 
 
+@pytest.mark.parametrize("n,k,E", [(512, 1025, 14541), (70, 300, 900), (3, 40, 5000), (600, 33, 100), (1, 1, 1),
+                                   (16, 64, 300000)])
+def test_group_sorted_rows_is_the_counting_sort(L, n, k, E):
+    """kge_group_sorted_rows (grouping from sorted candidate lists, LDS counters per entity range)
+    against the bincount / cumsum grouping of the flattened candidate matrix: the same segment
+    pointers, and every entity's segment holds exactly its pairs (in the caller's columns)."""
+    torch.manual_seed(n * k)
+    cand = torch.randint(0, E, (n, k), device="cuda")
+    if k > 8:
+        cand[:, 3] = cand[:, 5]  # duplicates within a row
+        cand[0, :] = E - 1       # a row of one (the last) entity
+    srt, col = L.sort_rows(cand)
+    order, seg_ptr = L.group_sorted_rows(srt, col, E)
+    flat = cand.reshape(-1)
+    exp_ptr = torch.zeros(E + 1, dtype=torch.int64, device="cuda")
+    exp_ptr[1:] = torch.cumsum(torch.bincount(flat, minlength=E), 0)
+    assert torch.equal(seg_ptr, exp_ptr)
+    # a permutation of all pairs, each in the segment of its entity
+    assert torch.equal(torch.sort(order).values, torch.arange(n * k, device="cuda"))
+    ent_of_slot = torch.repeat_interleave(torch.arange(E, device="cuda"), seg_ptr[1:] - seg_ptr[:-1])
+    assert torch.equal(flat[order], ent_of_slot)
+
+
 @pytest.mark.parametrize("num_neg", [31, 255])
 @pytest.mark.parametrize("model", ["rotate", "complex", "transe", "cp", "simple"])
 def test_ns_implementations_agree(model, num_neg):
