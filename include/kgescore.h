@@ -404,9 +404,12 @@ int kge_bucket_scatter(const int64_t* idx, int64_t n, int64_t* cursor, int64_t* 
 
 /* Every row of x[n, k] (ids in [0, 2^50), k <= 8192) sorted ascending, stably: sorted[i, :] and the
  * positions col[i, :] the ids came from (both contiguous [n, k]) -- torch.sort(x, 1, stable=True)
- * as one launch, the cand / col input of kge_score_cand_ordered. */
-int kge_sort_rows(const int64_t* x, int64_t ldx, int64_t n, int64_t k, int64_t* sorted, int64_t* col,
-                  void* stream);
+ * as one launch, the cand / col input of kge_score_cand_ordered.  id_bound: 0, or an exclusive
+ * upper bound of the ids (the number of entities); with id_bound <= 2^21 and k <= 2048 the sort
+ * runs on 32-bit keys, and ids outside [0, id_bound) -- invalid for every consumer -- come out
+ * clamped into that range. */
+int kge_sort_rows(const int64_t* x, int64_t ldx, int64_t n, int64_t k, int64_t id_bound, int64_t* sorted,
+                  int64_t* col, void* stream);
 
 /* The order / seg_ptr input of kge_score_cand_bwd_ent from candidate lists that kge_sort_rows has
  * sorted (srt, col: contiguous [n, k], n <= 4096): seg_ptr[nbuckets + 1] and order[n * k] with

@@ -76,7 +76,7 @@ SIGNATURES = {
                                 _I64, _P, _I64, _P], _I),
     "kge_bucket_scatter": ([_P, _I64, _P, _P, _P], _I),
     "kge_bucket_count": ([_P, _I64, _I64, _P, _P], _I),
-    "kge_sort_rows": ([_P, _I64, _I64, _I64, _P, _P, _P], _I),
+    "kge_sort_rows": ([_P, _I64, _I64, _I64, _I64, _P, _P, _P], _I),
     "kge_group_sorted_rows": ([_P, _P, _I64, _I64, _I64, _P, _P, _P], _I),
     "kge_stage_i64": ([_P, _P, _I64, _P], _I),
     "kge_rank_hist_multi": ([_P, _P, _I64, _I64, _I, _P, _P, _I64, _P], _I),
@@ -657,16 +657,19 @@ def score_cand(model, l_norm, direction, q, ent, cand, out=None):
     return o
 
 
-def sort_rows(x):
+def sort_rows(x, id_bound=0):
     """kge_sort_rows: (ids of every row ascending, the positions they came from) of an int64
-    [n, k <= 8192] matrix of non-negative ids -- torch.sort(x, 1, stable=True) in one launch."""
+    [n, k <= 8192] matrix of non-negative ids -- torch.sort(x, 1, stable=True) in one launch.
+    id_bound: an exclusive upper bound of the ids when the caller knows one (32-bit keys below
+    2^21: faster), 0 otherwise."""
     require_device(x)
     if x.dtype != torch.int64 or x.dim() != 2 or x.stride(1) != 1 or x.shape[1] > 8192:
         raise ValueError("sort_rows: an int64 [n, k <= 8192] matrix with unit column stride")
     n, k = x.shape
     srt, col = torch.empty(n, k, dtype=torch.int64, device=x.device), torch.empty(n, k, dtype=torch.int64,
                                                                                   device=x.device)
-    _check(lib().kge_sort_rows(ptr(x), x.stride(0) if n > 1 else k, n, k, ptr(srt), ptr(col), stream()), "kge_sort_rows")
+    _check(lib().kge_sort_rows(ptr(x), x.stride(0) if n > 1 else k, n, k, int(id_bound), ptr(srt), ptr(col), stream()),
+           "kge_sort_rows")
     return srt, col
 
 

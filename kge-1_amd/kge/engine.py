@@ -683,7 +683,7 @@ def _cand_order(cand: torch.Tensor, n_rows: int):
     n, k = cand.shape
     if k < 32 or n * k < 16 * n_rows:
         return None
-    return L.sort_rows(cand) if k <= 8192 else tuple(torch.sort(cand, 1))
+    return L.sort_rows(cand, n_rows) if k <= 8192 else tuple(torch.sort(cand, 1))
 
 
 class _ScoreCand(torch.autograd.Function):

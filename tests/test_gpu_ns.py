@@ -144,7 +144,9 @@ def test_score_cand_ordered_lists_vs_plain(L, model, ln, d):
         assert (gr - d_rel).abs().max() <= 2e-5 * d_rel.abs().max()
 
 
-@pytest.mark.parametrize("n,k,ld", [(5, 1, 1), (3, 2, 7), (64, 1025, 1025), (9, 300, 301), (2, 8192, 8192), (1, 777, 777)])
+@pytest.mark.parametrize("n,k,ld", [(5, 1, 1), (3, 2, 7), (64, 1025, 1025), (9, 300, 301), (2, 8192, 8192), (1, 777, 777),
+                                    (4, 3, 3), (4, 5, 5), (7, 64, 64), (7, 255, 256), (7, 256, 256), (7, 257, 300),
+                                    (3, 512, 512), (3, 1024, 1024), (3, 2048, 2048), (3, 2049, 2049)])
 def test_sort_rows_is_torch_stable_sort(L, n, k, ld):
     """kge_sort_rows (bitonic network in LDS) against torch.sort(stable=True): ids and positions,
     with many repeated ids per row."""
@@ -155,6 +157,12 @@ def test_sort_rows_is_torch_stable_sort(L, n, k, ld):
     srt, col = L.sort_rows(x)
     exp = torch.sort(x, dim=1, stable=True)
     assert torch.equal(srt, exp.values) and torch.equal(col, exp.indices)
+    # with a bound on the ids (32-bit keys below 2^21 and up to 2,048 columns)
+    buf[0, :k] = 7
+    exp = torch.sort(x, dim=1, stable=True)
+    for bound in (max(8, k // 3 + 1), 1 << 21, (1 << 21) + 1):
+        srt, col = L.sort_rows(x, bound)
+        assert torch.equal(srt, exp.values) and torch.equal(col, exp.indices), bound
 
 
 @pytest.mark.parametrize("n,k,E", [(512, 1025, 14541), (70, 300, 900), (3, 40, 5000), (600, 33, 100), (1, 1, 1),
