@@ -347,9 +347,8 @@ __global__ void __launch_bounds__(NT) cand_bwd_q_kernel(bool l1, float sigma, co
 }
 
 // d_ent, vectorised, one wave per entity group (pairs of order[seg_ptr[u] .. seg_ptr[u+1])).
-// The group is a chain of dependent loads per pair (pair index -> gradient / norm -> query row);
-// the loop keeps the NEXT pair's query row in flight while the current one is accumulated and
-// fetches the pair index two ahead, so that a pair costs one L2 round trip instead of three.
+// A pair is a chain of dependent loads (pair index -> gradient / norm -> query row): the loop takes
+// several pairs per round trip.
 template <int KIND, int NCH>
 __global__ void __launch_bounds__(256) cand_bwd_ent_kernel(bool l1, float sigma, const float* __restrict__ q,
                                                            int64_t ldq, const float* __restrict__ ent,
@@ -369,7 +368,7 @@ __global__ void __launch_bounds__(256) cand_bwd_ent_kernel(bool l1, float sigma,
   const int64_t row = cand[order[p0]];  // order indexes the flattened [n, k] candidate matrix
   const int unit = KIND == K_ROTATE ? d / 2 : d;
   const float* e = ent + row * ld_ent;
-  float4 ev[NCH][P], acc[NCH][P], qn[NCH][P];
+  float4 ev[NCH][P], acc[NCH][P];
   int off[NCH];
 #pragma unroll
   for (int ch = 0; ch < NCH; ++ch) {
@@ -380,32 +379,11 @@ __global__ void __launch_bounds__(256) cand_bwd_ent_kernel(bool l1, float sigma,
       acc[ch][pl] = f4(0.f);
     }
   }
-  // gradient, inverse norm and query row of the pair at position t of `order`
-  auto fetch = [&](int64_t pair, float& gc, float& inv) {
-    const int64_t i = pair / k, c = pair - i * k;
-    gc = g[i * ldg + c];
-    inv = inv_norm<KIND>(l1, s, i * lds + c);
-    const float* qi = q + i * ldq;
-#pragma unroll
-    for (int ch = 0; ch < NCH; ++ch)
-#pragma unroll
-      for (int pl = 0; pl < P; ++pl) qn[ch][pl] = ld4(qi + off[ch] + pl * unit);
-  };
-  float gc_n, inv_n;
-  fetch(order[p0], gc_n, inv_n);
-  int64_t pair_nn = order[p0 + 1 < p1 ? p0 + 1 : p0];
-  for (int64_t t = p0; t < p1; ++t) {
-    const float gc = gc_n, inv = inv_n;
-    float4 qv[NCH][P];
-#pragma unroll
-    for (int ch = 0; ch < NCH; ++ch)
-#pragma unroll
-      for (int pl = 0; pl < P; ++pl) qv[ch][pl] = qn[ch][pl];
-    if (t + 1 < p1) {
-      fetch(pair_nn, gc_n, inv_n);
-      pair_nn = order[t + 2 < p1 ? t + 2 : t + 1];
-    }
-    if (gc == 0.f) continue;
+  // D pairs at a time: their indexes were fetched during the previous batch, their gradients /
+  // norms and query rows (the 2-MB query block is L2 resident, so several rows in flight cost
+  // nothing here) are requested together, then accumulated in the order of `order`.
+  constexpr int D = NCH * P <= 4 ? 4 : (NCH * P <= 8 ? 2 : 1);
+  auto accumulate = [&](const float4 (&qv)[NCH][P], float gc, float inv) {
 #pragma unroll
     for (int ch = 0; ch < NCH; ++ch) {
       const float4 a = qv[ch][0], b = ev[ch][0];
@@ -424,6 +402,29 @@ __global__ void __launch_bounds__(256) cand_bwd_ent_kernel(bool l1, float sigma,
         }
       }
     }
+  };
+  int64_t pr[D];
+#pragma unroll
+  for (int u = 0; u < D; ++u) pr[u] = order[p0 + u < p1 ? p0 + u : p1 - 1];
+  for (int64_t t = p0; t < p1; t += D) {
+    float gc[D], inv[D];
+    float4 qv[D][NCH][P];
+#pragma unroll
+    for (int u = 0; u < D; ++u) {  // (a slot past the group's end repeats its last pair with gradient 0)
+      const int64_t pair = pr[u], i = pair / k, c = pair - i * k;
+      gc[u] = t + u < p1 ? g[i * ldg + c] : 0.f;
+      inv[u] = inv_norm<KIND>(l1, s, i * lds + c);
+      const float* qi = q + i * ldq;
+#pragma unroll
+      for (int ch = 0; ch < NCH; ++ch)
+#pragma unroll
+        for (int pl = 0; pl < P; ++pl) qv[u][ch][pl] = ld4(qi + off[ch] + pl * unit);
+    }
+#pragma unroll
+    for (int u = 0; u < D; ++u) pr[u] = order[t + D + u < p1 ? t + D + u : p1 - 1];
+#pragma unroll
+    for (int u = 0; u < D; ++u)
+      if (gc[u] != 0.f) accumulate(qv[u], gc[u], inv[u]);
   }
   float* de = d_ent + row * ld_dent;
 #pragma unroll
