@@ -610,6 +610,9 @@ extern "C" int kge_dev_score_dot_persist(int variant, const void* qhi, const voi
     case 51: return launch_persist16<256, 256, 2, 4, 5, true>(h, l, ldq, t, ldt, tidx, n, m, d, s, lds, st);
     case 52: return launch_persist16<256, 256, 2, 4, 6, true>(h, l, ldq, t, ldt, tidx, n, m, d, s, lds, st);
     case 53: return launch_persist16<256, 256, 2, 4, 7, true>(h, l, ldq, t, ldt, tidx, n, m, d, s, lds, st);
+    // 128 x 128 tiles, four waves, 64 KB of LDS: two workgroups (of two launches on two streams) fit a CU
+    case 60: return launch_persist16<128, 128, 2, 2, 0, true>(h, l, ldq, t, ldt, tidx, n, m, d, s, lds, st);
+    case 61: return launch_persist16<128, 128, 2, 2>(h, l, ldq, t, ldt, tidx, n, m, d, s, lds, st);
     default: return KGE_ERR_ARG;
   }
 }
