@@ -835,7 +835,10 @@ static int score_cand_bwd_impl(int model, float l_norm, int dir, const float* q,
   const int unit = kind == K_ROTATE ? d / 2 : d;
   const int nch = nch_of(unit);
   const dim3 grid((unsigned)n);
-  if (!d_ent && nch && unit % 4 == 0 && ldq % 4 == 0 && ld_ent % 4 == 0 && aligned16(q) && aligned16(ent)) {
+  // (the vector kernel's cross-wave reduction takes NW x d floats of LDS: up to the 64 KB every
+  // kernel may use without asking, d <= 2048)
+  if (!d_ent && nch && unit % 4 == 0 && ldq % 4 == 0 && ld_ent % 4 == 0 && aligned16(q) && aligned16(ent) &&
+      (size_t)NW * d * sizeof(float) <= 65536) {
     const size_t sh = (size_t)NW * d * sizeof(float);
     if (kind == K_DOT)
       dispatch_nch<LaunchQ, K_DOT>(nch, grid, sh, st, l1, sigma, q, ldq, ent, ld_ent, cand, ldc, col, ldcol, (int)k, d,

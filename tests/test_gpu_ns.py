@@ -188,6 +188,39 @@ def test_group_sorted_rows_is_the_counting_sort(L, n, k, E):
     assert torch.equal(flat[order], ent_of_slot)
 
 
+@pytest.mark.parametrize("ordered", [False, True])
+def test_score_cand_rotate_dim_3072_vs_float64(L, ordered):
+    """RotatE with 3,072-float entity rows (the backward takes up to 3,584): scores and both
+    gradients against float64 autograd of rotate.py:18-50's arithmetic.  The vector form of the
+    query-gradient pass would need more LDS than a kernel gets without asking: it runs its
+    scalar form at this width."""
+    from kge import engine
+
+    torch.manual_seed(3)
+    E, R, d = 600, 5, 3072
+    n, k = (24, 420) if ordered else (5, 40)
+    ent = (torch.randn(E, d, device="cuda") * 0.3).requires_grad_()
+    rel = ((torch.rand(R, d // 2, device="cuda") * 2 - 1) * 3.14159).requires_grad_()
+    eidx = torch.randint(0, E, (n,), device="cuda")
+    ridx = torch.randint(0, R, (n,), device="cuda")
+    cand = torch.randint(0, E, (n, k), device="cuda")
+    w = torch.randn(n, k, device="cuda")
+    assert (engine._cand_order(cand, E) is not None) == ordered
+    out = engine.score_cand(MODEL_IDS["rotate"], L.DIR_SP, 1.0, ent, eidx, rel, ridx, cand)
+    (out * w).sum().backward()
+    e64, r64 = ent.detach().double().requires_grad_(), rel.detach().double().requires_grad_()
+    h = d // 2
+    s = e64[eidx]
+    c, sn = torch.cos(r64[ridx]), torch.sin(r64[ridx])
+    qr, qi = s[:, :h] * c - s[:, h:] * sn, s[:, :h] * sn + s[:, h:] * c
+    o = e64[cand]  # [n, k, d]
+    ref = torch.sqrt((qr[:, None] - o[..., :h]) ** 2 + (qi[:, None] - o[..., h:]) ** 2).sum(-1)
+    (ref * w.double()).sum().backward()
+    assert (out.double() - ref).abs().max() <= 2e-6 * ref.abs().max()
+    assert (ent.grad.double() - e64.grad).abs().max() <= 2e-5 * e64.grad.abs().max()
+    assert (rel.grad.double() - r64.grad).abs().max() <= 2e-5 * r64.grad.abs().max()
+
+
 @pytest.mark.parametrize("num_neg", [31, 255])
 @pytest.mark.parametrize("model", ["rotate", "complex", "transe", "cp", "simple"])
 def test_ns_implementations_agree(model, num_neg):
