@@ -594,9 +594,11 @@ __global__ void __launch_bounds__(1024) rank_metrics_kernel(const float* __restr
                                                             int kmax, double* __restrict__ out) {
   constexpr int NT = 1024, UNROLL = 8;
   __shared__ double red[3][NT];
+  __shared__ float head[NT];  // the first NT counts, for the hits quotients
   const int tid = threadIdx.x;
   const float* h = hists + (int64_t)blockIdx.x * ld;
   double n = 0.0, s1 = 0.0, s2 = 0.0;
+  head[tid] = 0.f;
   // few workgroups run (one per histogram), so nothing hides a load's latency but the loads of the
   // same thread: UNROLL of them are in flight at a time
   for (int64_t j0 = tid; j0 < e; j0 += (int64_t)NT * UNROLL) {
@@ -606,6 +608,7 @@ __global__ void __launch_bounds__(1024) rank_metrics_kernel(const float* __restr
       const int64_t j = j0 + (int64_t)u * NT;
       c[u] = j < e ? h[j] : 0.f;
     }
+    if (j0 == tid) head[tid] = c[0];
 #pragma unroll
     for (int u = 0; u < UNROLL; ++u) {
       const float rank = (float)(j0 + (int64_t)u * NT + 1);
@@ -626,12 +629,18 @@ __global__ void __launch_bounds__(1024) rank_metrics_kernel(const float* __restr
   }
   double* o = out + (int64_t)blockIdx.x * (3 + kmax);
   if (tid < 3) o[tid] = red[tid][0];
+  // hits@(tid + 1): the cumulative counts of the first ranks in fp32, as torch.cumsum forms them
+  // -- a prefix scan: the counts are integers, so below 2^24 evaluation triples every partial sum
+  // is exact whatever the order of the additions
+  for (int off = 1; off < NT; off <<= 1) {
+    const float v = tid >= off ? head[tid - off] : 0.f;
+    __syncthreads();
+    head[tid] += v;
+    __syncthreads();
+  }
   if (tid < kmax) {
-    // hits@(tid + 1): the cumulative count summed in fp32 in index order, as torch.cumsum does
-    const float nf = (float)red[0][0];  // exact: integer counts far below 2^24
-    float cum = 0.f;
-    for (int k = 0; k <= tid && k < e; ++k) cum += h[k];
-    o[3 + tid] = nf > 0.f ? (double)(cum / nf) : 0.0;
+    const float nf = (float)red[0][0];
+    o[3 + tid] = nf > 0.f ? (double)(head[tid] / nf) : 0.0;
   }
 }
 
