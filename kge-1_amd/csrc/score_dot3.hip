@@ -388,18 +388,45 @@ __global__ void __launch_bounds__(64 * WM * WN, 1)
         const int tjr = tj_n;
         if (x + 1 < TM) row_info(x + 1, ts_n, bd_n, tj_n);
         unsigned word = 0;
+        if (__builtin_expect(__any(__builtin_fabsf(ts) == INFINITY), 0)) {
+          // a row whose true score is infinite (or was NaN): comparisons as they are written down
 #pragma unroll
-        for (int y = 0; y < TN; ++y) {
-          const int jb = y * 16 + 4 * fs_e;  // of the wave's 64 columns
-          const int rem = m - jw - jb;       // columns jb + r with r >= rem lie past m
+          for (int y = 0; y < TN; ++y) {
 #pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            float v = acc[x][y][r];
-            v = v == v ? v : -INFINITY;
-            unsigned code = (v > ts) ? 1u : ((v == ts) ? 2u : 0u);
-            code = (__builtin_fabsf(v - ts) <= bd) ? 3u : code;
-            code = (r < rem && jb + r != tjr) ? code : 0u;
-            word |= code << (8 * y + 2 * r);
+            for (int r = 0; r < 4; ++r) {
+              float v = acc[x][y][r];
+              v = v == v ? v : -INFINITY;
+              unsigned code = (v > ts) ? 1u : ((v == ts) ? 2u : 0u);
+              code = (__builtin_fabsf(v - ts) <= bd) ? 3u : code;
+              word |= code << (8 * y + 2 * r);
+            }
+          }
+        } else {
+          // A finite true score: "inside the band" is |v - ts| <= bd, and v == ts lies inside every
+          // band >= 0, so a refined row needs no equality test; an unrefined row (bd < 0) takes
+          // the band 0, whose members ARE the ties -- their code 3 is turned into 2 below.  A NaN
+          // score fails both comparisons (code 0, as -inf would), an infinite one is outside any band.
+          const float bd0 = bd < 0.f ? 0.f : bd;
+#pragma unroll
+          for (int y = 0; y < TN; ++y) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const float v = acc[x][y][r];
+              unsigned code = (v > ts) ? (1u << (8 * y + 2 * r)) : 0u;
+              code = (__builtin_fabsf(v - ts) <= bd0) ? (3u << (8 * y + 2 * r)) : code;
+              word |= code;
+            }
+          }
+          if (bd < 0.f) word ^= word & (word >> 1) & 0x55555555u;  // 3 -> 2
+        }
+        // the true column and the columns past m carry code 0
+        if (tjr >= 0 && ((tjr >> 2) & 3) == fs_e) word &= ~(3u << (8 * (tjr >> 4) + 2 * (tjr & 3)));
+        if (m - jw < WCOLS) {
+#pragma unroll
+          for (int y = 0; y < TN; ++y) {
+            const int rem = m - jw - (y * 16 + 4 * fs_e);  // columns 16 y + 4 fs + r with r >= rem lie past m
+            const unsigned keep = rem >= 4 ? 0xFFu : (rem <= 0 ? 0u : ((1u << (2 * rem)) - 1u));
+            word &= ~(0xFFu << (8 * y)) | (keep << (8 * y));
           }
         }
         const int i = m0 + wr * (BM / WM) + x * 16 + fr_e;
