@@ -774,6 +774,23 @@ def sharded_c5(args, world, rank, device, prec):
     # batch (world x B triples, the same on every rank: forward, cross-shard softmax statistics,
     # gradient planes, dQ reduce_scatter, dE local) -- RowShardedScorer.train_1vsall_global, the body
     # of ShardedTraining1vsAll's step without the optimizer
+    # The step keeps the [2 x rows, cols] logits and their gradient planes: about 80 GB per rank.
+    # Every rank must take the same decision (a rank that skipped or failed alone would leave the
+    # others waiting in the step's collectives), so the ranks agree on it first; ranks that share a
+    # GPU (a rehearsal of several ranks on one device) share its memory.
+    from kge.sharded import all_reduce
+    ndev = max(1, torch.cuda.device_count())
+    share = (world + ndev - 1) // ndev
+    need = share * 2.3 * (2.0 * rows) * cols * 4
+    fits = torch.tensor([1.0 if need < torch.cuda.mem_get_info(device)[0] else 0.0], device=device, dtype=torch.float64)
+    if world > 1:
+        all_reduce(fits, op=dist.ReduceOp.MIN)
+    if float(fits) < 1.0:
+        res["train_skipped"] = (f"{need / 2**30:.0f} GiB needed on this device for {share} rank(s): "
+                                "not measured here (every GPU of a node holds one rank)")
+        del sharded, ent
+        torch.cuda.empty_cache()
+        return res
     try:
         gt = torch.Generator(device=device).manual_seed(11)  # the same batch on every rank
         tr = torch.stack([torch.randint(0, E, (rows,), device=device, generator=gt),
