@@ -11,6 +11,14 @@ n, k, d, E = 512, 1025, 1024, 14541
 q = torch.randn(n, d, device="cuda") * 0.1
 ent = torch.randn(E, d, device="cuda") * 0.1
 cand = torch.randint(0, E, (n, k), device="cuda")
+if len(sys.argv) > 1 and sys.argv[1] == "xcd":
+    # what a split of every list into 8 entity ranges, range x served by XCD x, could reach: here
+    # query i (workgroup i, XCD i % 8) draws all its candidates from range i % 8 -- the same reuse
+    # of table rows inside an XCD as 512 queries x 128 candidates per range
+    r = torch.arange(n, device="cuda") % 8
+    cand = (torch.rand(n, k, device="cuda") * (E // 8)).long() + (r * (E // 8))[:, None]
+    cand = torch.sort(cand, 1).values
+    print("candidates of query i in entity range i % 8, ascending")
 if len(sys.argv) > 1 and sys.argv[1] == "sorted":  # ascending candidates per query: rows shared in the XCD's L2
     cand = torch.sort(cand, 1).values
     print("candidates in ascending order per query")
