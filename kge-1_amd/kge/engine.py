@@ -681,7 +681,10 @@ def _cand_order(cand: torch.Tensor, n_rows: int):
     4 KB: 78 % L2 hits instead of 10 %, forward 268 -> 190 us, dq 262 -> 149 us).  That needs
     rows that several of an XCD's queries use: (n / 8) * k uses of n_rows rows."""
     n, k = cand.shape
-    if k < 32 or n * k < 16 * n_rows:
+    # (inside a recorded step the lists are always ordered: the other grouping of the d_ent pass
+    # goes through a library scan, whose memset nodes do not belong in a HIP graph)
+    recording = cand.is_cuda and torch.cuda.is_current_stream_capturing() and n <= 4096 and k <= 8192
+    if (k < 32 or n * k < 16 * n_rows) and not recording:
         return None
     return L.sort_rows(cand, n_rows) if k <= 8192 else tuple(torch.sort(cand, 1))
 

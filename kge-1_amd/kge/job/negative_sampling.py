@@ -22,8 +22,32 @@ import time
 
 import torch
 
-from ..util.sampler import KgeSampler, O, P, S
-from .train import TrainingJob
+from ..util.sampler import KgeSampler, KgeUniformSampler, O, P, S
+from .train import TrainingJob, _GraphStep
+
+
+class _NSGraphStep(_GraphStep):
+    """The negative-sampling step as a recorded graph (engine.graph_step): the batch's B triples are
+    the recorded index block; the negatives are drawn inside the recording (torch's generator
+    advances with every replay), scored, and the loss, both backward passes and the optimizer
+    step follow -- some 50 launches that otherwise cost more host time than device time at the
+    usual handful of negatives.  Batches that bring their own negatives, and partial batches,
+    run eagerly."""
+
+    def _capacity(self) -> int:
+        return 3 * self.job.batch_size
+
+    def _block(self, batch):
+        triples = batch["triples"]
+        if "negative_samples" in batch or triples.dim() != 2 or tuple(triples.shape) != (self.job.batch_size, 3):
+            return None
+        return triples.long().reshape(-1)
+
+    def _recorded_batch(self):
+        return {"triples": self.static.view(self.job.batch_size, 3)}
+
+    def _penalty_batch(self):
+        return self._recorded_batch()
 
 
 class TrainingJobNegativeSampling(TrainingJob):
@@ -67,6 +91,20 @@ class TrainingJobNegativeSampling(TrainingJob):
         super()._prepare()
         self._replicas_only()
         self.num_examples = self.dataset.split(self.train_split).size(0)
+        # The step is recorded when nothing in it needs the host: negatives drawn by torch.randint
+        # (no filtering rounds, no shared sample), scored by the candidate kernels, the loss fused.
+        opt = self.optimizer
+        sampler = self._sampler
+        self._graph_step = None
+        if (self.config.get("engine.graph_step") and torch.device(self.device).type == "cuda"
+                and self._fused_loss is not None and self._implementation == "triple"
+                and type(sampler) is KgeUniformSampler and not sampler.shared and not any(sampler.filter_positives)
+                and sampler.num_samples[P] == 0
+                and self.batch_size <= 4096 and 1 + max(sampler.num_samples) <= 8192  # engine._cand_order
+                and hasattr(opt, "graph_safe") and opt.graph_safe() and not self.pre_batch_hooks
+                and self._penalties_recordable(weighted_ok=True)
+                and self.model._lookup_tables() is not None):
+            self._graph_step = _NSGraphStep(self)
 
     def _collate(self, example_ids):
         return {"triples": self.dataset.split(self.train_split)[example_ids, :].long()}
@@ -74,7 +112,7 @@ class TrainingJobNegativeSampling(TrainingJob):
     # --------------------------------------------------------------------- scoring
     def _scores(self, triples: torch.Tensor, slot: int, neg: torch.Tensor) -> torch.Tensor:
         """[chunk, 1 + N] scores, column 0 the positive."""
-        cand = torch.cat((triples[:, [slot]], neg), 1)
+        cand = torch.cat((triples[:, slot:slot + 1], neg), 1)
         n, k = cand.shape
         if self._implementation == "triple":
             out = None

@@ -19,10 +19,12 @@ c = Config()
 c.set("model", model)
 c._import(model)
 c.set("job.device", "cuda")
-c.set("lookup_embedder.dim", 1024)
+c.set("lookup_embedder.dim", int(os.environ.get("NS_DIM", "1024")))
 c.set("train.type", "negative_sampling")
 c.set("train.loss", "kl")
-c.set("negative_sampling.num_samples.s", 1024)
+c.set("negative_sampling.num_samples.s", int(os.environ.get("NS_NEG", "1024")))
+if os.environ.get("KGE_NO_GRAPH") == "1":
+    c.set("engine.graph_step", False)
 c.set("negative_sampling.implementation", impl)
 c.set("train.optimizer", "Adagrad")
 c.set("train.optimizer_args", {"lr": 0.1})
@@ -41,7 +43,9 @@ for i in range(5):
     job.train_step(i, job._collate(perm[i * B:(i + 1) * B]))
 torch.cuda.synchronize()
 t0 = time.perf_counter()
-for i in range(5, 15):
+for i in range(5, 5 + int(os.environ.get("NS_STEPS", "10"))):
     job.train_step(i, job._collate(perm[i * B:(i + 1) * B]))
 torch.cuda.synchronize()
-print(f"{model} negative_sampling {impl} step {(time.perf_counter() - t0) / 10 * 1e3:.3f} ms")
+print(f"{model} negative_sampling {impl} step {(time.perf_counter() - t0) / int(os.environ.get('NS_STEPS', '10')) * 1e3:.3f} ms")
+gs = getattr(job, "_graph_step", None)
+print("graph step:", None if gs is None else ("recorded" if gs.graph is not None else f"not recorded: {gs.error}"))

@@ -269,3 +269,39 @@ def test_ns_training_lowers_loss():
         first = tr["avg_loss"] if first is None else first
         last = tr["avg_loss"]
     assert np.isfinite(last) and last < first
+
+
+@pytest.mark.parametrize("model,num_neg", [("complex", 7), ("rotate", 200), ("transe", 40)])
+def test_recorded_ns_step_replays_like_the_eager_step(model, num_neg):
+    """engine.graph_step for negative sampling: the step recorded once and replayed (negatives
+    drawn inside the recording, torch's generator advancing per replay) against the same job
+    stepping eagerly from the same seed -- the same negatives, hence the same losses and tables,
+    replay after replay, with eager work and synchronisations of the test in between."""
+    def run(graph):
+        job = _ns_job(model, "triple", num_neg=num_neg)
+        job.config.set("engine.graph_step", graph)
+        job._prepare()
+        torch.manual_seed(123)
+        perm = torch.randperm(job.num_examples, generator=torch.Generator().manual_seed(0))
+        losses, tables = [], []
+        for i in range(9):
+            res, _, _ = job.train_step(i, job._collate(perm[i * 128:(i + 1) * 128]))
+            losses.append(float(res.avg_loss))
+            torch.cuda.synchronize()
+            tables.append(job.model._entity_embedder._embeddings.weight.detach().clone())
+            _ = (tables[-1] * 2).sum().item()  # unrelated eager work between the replays
+        return job, losses, tables
+
+    job_g, loss_g, tab_g = run(True)
+    job_e, loss_e, tab_e = run(False)
+    assert job_g._graph_step is not None and job_g._graph_step.graph is not None, job_g._graph_step.error
+    assert job_e._graph_step is None
+    np.testing.assert_allclose(loss_g, loss_e, rtol=2e-5)
+    for i, (a, b) in enumerate(zip(tab_g, tab_e)):
+        # the entity-grouped sums add their pairs in no fixed order: differences of an ulp, which an
+        # L1 distance turns into a flipped sign(x) for the odd component with |x| ~ 1e-7 -- a
+        # handful of elements may move by a step's worth, the tables as a whole not at all
+        diff = (a - b).abs()
+        off = int((diff > 2e-5 * b.abs().max()).sum())
+        assert off <= 8 and float(diff.mean()) <= 1e-7 * float(b.abs().max()), (i, off, float(diff.mean()))
+    assert len(set(loss_g)) == len(loss_g)  # every replay drew new negatives (and saw a new batch)
