@@ -24,6 +24,8 @@ c.set("train.optimizer", "Adagrad")
 c.set("train.optimizer_args", {"lr": 0.2})
 c.set("train.batch_size", 1024 if train_type == "1vsAll" else 512)
 c.set("verbose", False)
+if os.environ.get("KGE_PROF_OPTIONS") == "dropout":
+    c.set("lookup_embedder.dropout", 0.2)
 if os.environ.get("KGE_PROF_OPTIONS") == "dropout_penalties":  # what tuned LibKGE configurations carry
     c.set("lookup_embedder.dropout", 0.2)
     c.set("lookup_embedder.regularize_args.weighted", True)
@@ -44,3 +46,5 @@ for i in range(8, 18):
     job.train_step(i, job._collate(perm[i * B:(i + 1) * B]))
 torch.cuda.synchronize()
 print(f"{model_name} {train_type} step {(time.perf_counter() - t0) / 10 * 1e3:.3f} ms")
+gs = getattr(job, "_graph_step", None)
+print("graph step:", None if gs is None else ("recorded" if gs.graph is not None else f"not recorded: {gs.error}"))
