@@ -1,7 +1,9 @@
-"""Dev probe: host-side (cProfile) cost of a training step, e.g. `distmult KvsAll`."""
+"""cProfile of the host side of eager training steps (argv: model, train type; KGE_PROF_OPTIONS as
+in prof_train.py): where the time of a step goes that is not replayed from a recorded graph."""
 import cProfile
 import os
 import pstats
+import runpy
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
@@ -9,35 +11,13 @@ sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "kge-1_amd"))
 import torch  # noqa: E402
 
-from kge import Config, Dataset  # noqa: E402
-from kge.job import TrainingJob  # noqa: E402
-
-model_name = sys.argv[1] if len(sys.argv) > 1 else "distmult"
-train_type = sys.argv[2] if len(sys.argv) > 2 else "KvsAll"
-c = Config()
-c.set("model", model_name)
-c._import(model_name)
-c.set("job.device", "cuda")
-c.set("lookup_embedder.dim", 512)
-c.set("lookup_embedder.initialize_args", {"mean": 0.0, "std": 0.1})
-c.set("train.type", train_type)
-c.set("train.optimizer", "Adagrad")
-c.set("train.optimizer_args", {"lr": 0.2})
-c.set("train.batch_size", 1024 if train_type == "1vsAll" else 512)
-c.set("verbose", False)
-ds = Dataset.synthetic(c, "fb15k-237" if train_type == "1vsAll" else "wn18rr", seed=0)
-job = TrainingJob.create(c, ds)
-job._prepare()
-B = c.get("train.batch_size")
-perm = torch.randperm(job.num_examples, generator=torch.Generator().manual_seed(0))
-for i in range(8):
-    job.train_step(i, job._collate(perm[i * B:(i + 1) * B]))
+g = runpy.run_path(os.path.join(ROOT, "scripts", "dev", "prof_train.py"))
+job, perm, B = g["job"], g["perm"], g["B"]
 torch.cuda.synchronize()
 pr = cProfile.Profile()
 pr.enable()
-for i in range(8, 58):
+for i in range(20, 40):
     job.train_step(i, job._collate(perm[i * B:(i + 1) * B]))
 torch.cuda.synchronize()
 pr.disable()
-st = pstats.Stats(pr)
-st.sort_stats("cumulative").print_stats(45)
+pstats.Stats(pr).sort_stats("tottime").print_stats(28)
