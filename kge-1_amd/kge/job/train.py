@@ -417,34 +417,41 @@ class _GraphStep:
         block = self._block(batch)
         if block is None or block.numel() > self._capacity():
             return None
-        n = block.numel()
         if self.graph is None:
             if not self._record(batch_index, block):
                 return None
             # recording counted this step in the optimizer state already
         else:
-            # a copy from pageable memory would block the host until the device drains;
-            # stage through pinned memory (two buffers: the read of batch b - 1 may still be
-            # pending) and upload it with a kernel in stream order
-            if not self.pinned:
-                self.pinned = [[torch.empty(self._capacity(), dtype=torch.int64, pin_memory=True), None]
-                               for _ in range(2)]
-            slot = self.pinned[self.turn]
-            self.turn ^= 1
-            if slot[1] is not None:
-                slot[1].synchronize()
-            slot[0][:n].copy_(block)
-            _lib.stage_i64(slot[0][:n], self.static[:n])  # a kernel, not a DMA copy, on this stream
-            slot[1] = torch.cuda.Event()
-            slot[1].record()
+            self._upload(block)
             job.optimizer.advance_steps(self.stepped)
         self.graph.replay()
         t += time.time()
         return TrainingJob._ProcessBatchResult(self._loss_of(block), job.batch_size, 0.0, t, 0.0)
 
+    def _upload(self, block):
+        """The batch's index block into the recorded device buffer, in stream order.  A copy from
+        pageable memory would block the host until the device drains: staged through pinned memory
+        (two buffers: the read of batch b - 1 may still be pending) and uploaded by a kernel."""
+        n = block.numel()
+        if not self.pinned:
+            self.pinned = [[torch.empty(self._capacity(), dtype=torch.int64, pin_memory=True), None]
+                           for _ in range(2)]
+        slot = self.pinned[self.turn]
+        self.turn ^= 1
+        if slot[1] is not None:
+            slot[1].synchronize()
+        slot[0][:n].copy_(block)
+        _lib.stage_i64(slot[0][:n], self.static[:n])  # a kernel, not a DMA copy, on this stream
+        slot[1] = torch.cuda.Event()
+        slot[1].record()
+
     def _loss_of(self, block):
         """The loss the step reports, from what the recording returned."""
         return self.loss
+
+    def _pool(self):
+        """The memory pool the recording allocates from (None: one of its own)."""
+        return None
 
     def _record(self, batch_index, block) -> bool:
         job = self.job
@@ -452,11 +459,14 @@ class _GraphStep:
         steps = {p: st["step"].clone() for p, st in opt.state.items() if "step" in st}
         host = torch.zeros(self._capacity(), dtype=torch.int64)
         host[:block.numel()] = block
-        self.static = host.to(job.device)
+        if self.static is None:
+            self.static = host.to(job.device)
+        else:  # recorded again (another learning rate, another variant of the step): the same buffer
+            self.static.copy_(host)
         opt.zero_grad(set_to_none=True)
         g = torch.cuda.CUDAGraph()
         try:
-            with torch.cuda.graph(g):
+            with torch.cuda.graph(g, pool=self._pool()):
                 res = job.process_batch(batch_index, self._recorded_batch())
                 pen = job._penalty_backward(batch_index, self._penalty_batch())
                 opt.step()
@@ -523,6 +533,73 @@ class _KvsAllGraphStep(_GraphStep):
         B = self.job.batch_size
         two = len(self.job._part_spec) == 2 and int(block[3 * B + 1]) < B
         return self.loss[1 if two else 0]
+
+
+class _KvsAllSplitGraphStep(_KvsAllGraphStep):
+    """The KvsAll step with dropout in the embedders: its two query types are scored one after the
+    other (each against its own dropped copy of the entity table), so the shapes of a step depend
+    on where the batch splits into (s, p, ?) and (?, p, o) queries.  ONE RECORDING PER SPLIT POINT:
+    the split of a shuffled batch is binomial, a few dozen values occur at all, and every recording
+    reads the same index buffer and allocates from one shared pool (a step's intermediates are dead
+    when it ends; its loss is copied to the host before the next replay is issued).  Beyond
+    MAX_GRAPHS different splits a batch runs eagerly."""
+
+    MAX_GRAPHS = 160
+
+    def __init__(self, job):
+        super().__init__(job)
+        self.graphs = {}  # split point -> (graph, loss, penalty, parameters it steps)
+        self.n_first = 0
+        self._shared_pool = None
+
+    def disable(self):
+        super().disable()
+        self.graphs = {}
+
+    def _pool(self):
+        if self._shared_pool is None:
+            self._shared_pool = torch.cuda.graph_pool_handle()
+        return self._shared_pool
+
+    def _recorded_batch(self):
+        B = self.job.batch_size
+        st = self.static
+        return {"split": (st[:B], st[B:2 * B], st[2 * B:3 * B + 1], st[3 * B + 2:], self.n_first)}
+
+    def _loss_of(self, block):
+        return self.loss
+
+    def run(self, batch_index, batch):
+        job = self.job
+        if self.disabled:
+            return None
+        if self.warm < self.WARMUP:
+            self.warm += 1
+            return None
+        if self.graphs and self._hyper() != self.hyper:
+            self.graphs = {}  # another learning rate: every split is recorded anew
+        t = -time.time()
+        block = self._block(batch)
+        if block is None or block.numel() > self._capacity():
+            return None
+        B = job.batch_size
+        n_first = int(block[3 * B + 1])
+        entry = self.graphs.get(n_first)
+        if entry is None:
+            if len(self.graphs) >= self.MAX_GRAPHS:
+                return None
+            self.n_first = n_first
+            self.graph = None
+            if not self._record(batch_index, block):
+                return None
+            entry = self.graphs[n_first] = (self.graph, self.loss, self.penalty, self.stepped)
+        else:
+            self._upload(block)
+            job.optimizer.advance_steps(entry[3])
+        self.graph, self.loss, self.penalty, self.stepped = entry
+        self.graph.replay()
+        t += time.time()
+        return TrainingJob._ProcessBatchResult(self.loss, B, 0.0, t, 0.0)
 
 
 class TrainingJob1vsAll(TrainingJob):
@@ -807,9 +884,42 @@ class TrainingJobKvsAll(TrainingJob):
                 and hasattr(opt, "graph_safe") and opt.graph_safe()
                 and not self.pre_batch_hooks
                 and not sharding_enabled(self.config)
-                and self._penalties_recordable(weighted_ok=False)  # its triples vary in number
-                and self._stacked_applicable()):
-            self._graph_step = _KvsAllGraphStep(self)
+                and self._penalties_recordable(weighted_ok=False)):  # its triples vary in number
+            if self._stacked_applicable():
+                self._graph_step = _KvsAllGraphStep(self)
+            elif self._split_applicable():
+                self._graph_step = _KvsAllSplitGraphStep(self)
+
+    def _split_applicable(self) -> bool:
+        """Whether the step can be recorded per split point (_KvsAllSplitGraphStep): lookup
+        embedders whose only addition is dropout (the fused loss in its embedding-row form)."""
+        from ..model.reciprocal_relations_model import ReciprocalRelationsModel
+
+        m = self.model
+        return (not isinstance(m, ReciprocalRelationsModel) and m._lookup_tables() is None
+                and m._lookup_embedders_with_dropout() and self._fused_loss_kind()[0] == "kl")
+
+    def _process_split(self, split, bs):
+        """The recorded step's body when the query types are scored one after the other (dropout):
+        rows [0, n_first) of the device block of _stacked_block are the first query type's, the
+        rest the second's; n_first is a host integer (one recording per value)."""
+        eidx, ridx, l_ptr, l_col, n_first = split
+        spans = [(0, 0, n_first)] if len(self._part_spec) == 1 else [(0, 0, n_first), (1, n_first, bs)]
+        fwd = bwd = 0.0
+        total = None
+        for qi, a, b in spans:
+            if b <= a:
+                continue
+            fwd -= time.time()
+            # (the label pointer keeps its absolute positions into l_col)
+            loss = self.model._xent_dropout(eidx[a:b], ridx[a:b], self._part_spec[qi][0], l_col, 1.0 / bs,
+                                            l_ptr[a:b + 1], self.label_smoothing)
+            fwd += time.time()
+            bwd -= time.time()
+            loss.backward()
+            bwd += time.time()
+            total = loss.detach()  # the reference keeps the last query type's value
+        return TrainingJob._ProcessBatchResult(total, bs, 0.0, fwd, bwd)
 
     def _stacked_applicable(self) -> bool:
         """Whether the recorded step's engine pass (KgeModel.score_xent_stacked) serves this model."""
@@ -935,6 +1045,8 @@ class TrainingJobKvsAll(TrainingJob):
     def _process_batch(self, batch_index, batch) -> TrainingJob._ProcessBatchResult:
         if "stacked" in batch:
             return self._process_stacked(batch["stacked"], self.batch_size)
+        if "split" in batch:
+            return self._process_split(batch["split"], self.batch_size)
         t = -time.time()
         ex = batch["examples"].numpy()
         bs = len(ex)

@@ -38,13 +38,22 @@ job = TrainingJob.create(c, ds)
 job._prepare()
 B = c.get("train.batch_size")
 perm = torch.randperm(job.num_examples, generator=torch.Generator().manual_seed(0))
-for i in range(8):
-    job.train_step(i, job._collate(perm[i * B:(i + 1) * B]))
+WARM, STEPS = int(os.environ.get("PROF_WARM", "8")), int(os.environ.get("PROF_STEPS", "10"))
+nb = job.num_examples // B
+
+
+def ids(i):  # (epochs of the same permutation when the run is longer than one)
+    return perm[(i % nb) * B:(i % nb + 1) * B]
+
+
+for i in range(WARM):
+    job.train_step(i, job._collate(ids(i)))
 torch.cuda.synchronize()
 t0 = time.perf_counter()
-for i in range(8, 18):
-    job.train_step(i, job._collate(perm[i * B:(i + 1) * B]))
+for i in range(WARM, WARM + STEPS):
+    job.train_step(i, job._collate(ids(i)))
 torch.cuda.synchronize()
-print(f"{model_name} {train_type} step {(time.perf_counter() - t0) / 10 * 1e3:.3f} ms")
+print(f"{model_name} {train_type} step {(time.perf_counter() - t0) / STEPS * 1e3:.3f} ms")
 gs = getattr(job, "_graph_step", None)
-print("graph step:", None if gs is None else ("recorded" if gs.graph is not None else f"not recorded: {gs.error}"))
+print("graph step:", None if gs is None else ("recorded" if gs.graph is not None else f"not recorded: {gs.error}"),
+      f"({len(gs.graphs)} split points)" if hasattr(gs, "graphs") else "")

@@ -233,6 +233,50 @@ def test_kvsall_graph_step_matches_eager(model):
     assert g[4] == e[4] == len(batches) and g[5] == e[5] == len(batches)
 
 
+@pytest.mark.parametrize("model", ["distmult", "complex"])
+def test_kvsall_graph_step_with_dropout_one_recording_per_split_matches_eager(model):
+    """KvsAll with dropout in the embedders: the query types are scored one after the other, each
+    against its own dropped copy of the entity table, so the step is recorded once PER SPLIT POINT
+    of the batch (train.py's _KvsAllSplitGraphStep; all recordings share one buffer and one memory
+    pool).  Against the eager job from the same seed: torch's dropout draws the same masks in both
+    (same calls, same shapes), so losses, tables and optimizer state must agree step after step --
+    over 40 steps that record a dozen splits and replay each several times, in any order."""
+    runs = {}
+    for graph in (False, True):
+        job = _kvsall_job(graph, model, batch=32)
+        for e in (job.model.get_s_embedder(), job.model.get_p_embedder()):
+            e.dropout.p = 0.3
+        job._prepare()  # decides on the graph step with the dropout in place
+        n = job.num_examples
+        torch.manual_seed(11)
+        g = torch.Generator().manual_seed(3)
+        batches = [torch.randperm(n, generator=g)[:32] for _ in range(40)]
+        batches.insert(7, torch.randperm(n, generator=g)[:20])  # a partial batch: eager
+        losses, splits = [], []
+        for b, ids in enumerate(batches):
+            splits.append(int((ids < job.query_last_example[0]).sum()) if len(ids) == 32 else -1)
+            res, _, _ = job.train_step(b, job._collate(ids))
+            losses.append(float(res.loss))
+        if graph:
+            gs = job._graph_step
+            assert gs is not None and gs.graphs, f"not recorded: {None if gs is None else gs.error}"
+            recorded = set(splits[2:]) - {-1}  # (two eager warm-up steps)
+            assert set(gs.graphs) == recorded and len(recorded) < len(splits) - 12  # splits were replayed
+        else:
+            assert job._graph_step is None
+        st = job.optimizer.state
+        ent = job.model.get_s_embedder()._embeddings.weight
+        rel = job.model.get_p_embedder()._embeddings.weight
+        runs[graph] = (np.array(losses), ent.detach().cpu().numpy(), rel.detach().cpu().numpy(),
+                       st[ent]["sum"].cpu().numpy(), int(st[ent]["step"]))
+    e, g = runs[False], runs[True]
+    np.testing.assert_allclose(g[0], e[0], rtol=1e-4, atol=1e-7)
+    for a, b in ((g[1], e[1]), (g[2], e[2])):  # (a different mask anywhere would move rows by O(0.1))
+        assert np.abs(a - b).max() <= 1e-3 * np.abs(b).max() and np.abs(a - b).mean() <= 1e-5 * np.abs(b).max()
+    np.testing.assert_allclose(g[3], e[3], rtol=1e-2, atol=1e-4 * np.abs(e[3]).max())
+    assert g[4] == e[4] == len(batches)
+
+
 def test_kvsall_graph_step_falls_back_when_labels_exceed_capacity():
     """A batch whose positives do not fit the recorded label buffer runs eagerly (same result)."""
     job = _kvsall_job(True, "distmult")
