@@ -71,6 +71,9 @@ def parse():
                     help="N > 1: batches per rank exchanged by one all_gather in the grouped schedule")
     ap.add_argument("--c5", action="store_true", help="N = 1: also time one rank's Wikidata5M shard (configs[4])")
     ap.add_argument("--no-c5", action="store_true", help="N > 1: skip the row-sharded Wikidata5M step")
+    ap.add_argument("--leg-timeout", type=float, default=float(os.environ.get("KGE_BENCH_LEG_TIMEOUT", "420")),
+                    help="N > 1: seconds the legs reported beside the headline (Wikidata5M shard, row-sharded "
+                         "evaluation) may take together before rank 0 prints the line without them")
     ap.add_argument("--launch-check", action="store_true",
                     help="only join the process group, check that the world size equals --gpus and print "
                          "{launch_check, n_gpus}: tests the N-rank launch without any GPU work")
@@ -567,11 +570,15 @@ def main():
            "roofline": roofline}
     out.update(extra_n)
 
-    if world > 1 and not args.no_extras:
-        try:
-            out["eval_row_sharded"] = sharded_eval(args, world, rank, device, model, c)
-        except Exception as e:  # reported, never fatal for the headline (every rank runs the same code)
-            out["eval_row_sharded"] = {"error": f"{type(e).__name__}: {e}"[:300]}
+    if world > 1:
+        # the headline is measured: what follows is reported beside it, under a deadline
+        legs = OptionalLegs(out, rank, args.leg_timeout)
+        if not args.no_c5:
+            legs.run("row_sharded_c5", lambda: sharded_c5(args, world, rank, device, prec))
+        if not args.no_extras:
+            legs.run("eval_row_sharded", lambda: sharded_eval(args, world, rank, device, model, c))
+        if not legs.done():
+            time.sleep(60.0)  # the timer has fired: it prints the line and ends the process
     if rank == 0 and world == 1 and not args.no_extras:
         out["extras"], eval_ctx = extras(args, model, c, E, R, device)
     else:
@@ -600,6 +607,56 @@ def launch_check(world, rank):
         print(json.dumps({"launch_check": True, "n_gpus": world, "ranks_counted": int(t)}))
     if world > 1:
         dist.destroy_process_group()
+
+
+class OptionalLegs:
+    """N > 1: the legs reported beside the headline (Wikidata5M shard, row-sharded evaluation) run
+    under a deadline.  They are collectives over all ranks, and a collective that never completes
+    (a transport problem on a node this code has not run on before) would otherwise keep rank 0
+    from ever printing the headline it has already measured.  Every rank starts the same timer
+    when the legs begin; when it fires, rank 0 prints the line as it stands, with the unfinished
+    legs named in `optional_legs_timed_out`, and every rank leaves with status 0 (os._exit: the
+    main thread may be blocked inside the collective).  Finished in time, nothing differs."""
+
+    def __init__(self, out: dict, rank: int, seconds: float):
+        import threading
+
+        self.out, self.rank, self.seconds = out, rank, seconds
+        self.pending = []
+        self._lock = threading.Lock()
+        self._finished = False
+        self._timer = threading.Timer(seconds, self._expired)
+        self._timer.daemon = True
+        self._timer.start()
+
+    def run(self, name, fn):
+        self.pending.append(name)
+        try:
+            res = fn()
+        except Exception as e:  # reported, never fatal for the headline (every rank runs the same code)
+            res = {"error": f"{type(e).__name__}: {e}"[:300]}
+        with self._lock:
+            self.out[name] = res
+            self.pending.remove(name)
+
+    def done(self) -> bool:
+        """Stops the timer; False when it has already fired (the line is printed, the process leaving)."""
+        with self._lock:
+            self._timer.cancel()
+            fired, self._finished = self._finished, True
+        return not fired
+
+    def _expired(self):
+        with self._lock:
+            if self._finished:
+                return
+            self._finished = True
+            if self.rank == 0:
+                self.out["optional_legs_timed_out"] = {"legs": list(self.pending), "after_seconds": self.seconds}
+                print(json.dumps(self.out), flush=True)
+        if self.rank != 0:
+            time.sleep(2.0)  # rank 0 prints first
+        os._exit(0)
 
 
 def sharded_headline(args, world, rank, device, ent, rel, prec, s_all, p_all, step_full_table):
@@ -690,8 +747,6 @@ def sharded_headline(args, world, rank, device, ent, rel, prec, s_all, p_all, st
         "replicated_dp": {"ms_per_step": sec_dp * 1e3, "value": world * B * E / sec_dp,
                           "what": f"every rank scores its {B} queries against a replica of the whole table "
                                   f"(KgeModel.score_sp); no collective in the step"}}
-    if not args.no_c5:
-        extra["row_sharded_c5"] = sharded_c5(args, world, rank, device, prec)
     return sec_head, world * B, hi - lo, extra
 
 

@@ -73,7 +73,7 @@ def main():
         rows.append(((marks["t0"] - a) * 1e3, (marks["issued"] - marks["t0"]) * 1e3,
                      (marks["done"] - marks["issued"]) * 1e3, (b - marks["done"]) * 1e3, marks["metrics_fn"] * 1e3))
     med = np.median(np.array(rows[1:]), axis=0)
-    print(f"streams {ns} head_and_tail {hat}: before loop {med[0]:.3f} ms, loop issued in {med[1]:.3f} ms, device "
+    print(f"group {ej._bs} total {med[:4].sum():.3f} ms; streams {ns} head_and_tail {hat}: before loop {med[0]:.3f} ms, loop issued in {med[1]:.3f} ms, device "
           f"done {med[2]:.3f} ms later, metrics {med[3]:.3f} ms (of which the metric sums + copy {med[4]:.3f} ms)", flush=True)
 
 
