@@ -79,7 +79,9 @@ __device__ __forceinline__ void store_tile(const f32x4 (&acc)[TM][TN], unsigned 
 // ---------------------------------------------------------------------------------------
 // dQ partial slabs: slab[z][i][j] = sum_{e in K chunk z} G[i, e] * T[e, j]
 // ghi / glo: G planes, row stride ldgp (bf16 elements), columns [K, round_up(K, 32)) zero.
-template <bool PIPE>
+// GROUP: the three MFMAs of a band issued as three runs over y with one A fragment held per run
+// (instead of three per accumulator in turn): same order per accumulator, bit-identical.
+template <bool PIPE, bool GROUP>
 __global__ void __launch_bounds__(NT, 1)
     bwd3p_q_kernel(const __bf16* __restrict__ ghi, const __bf16* __restrict__ glo, int64_t ldgp,
                    const float* __restrict__ t, int64_t ldt, int n, int N, int K, int kchunk, int nrt, int nct,
@@ -243,8 +245,20 @@ __global__ void __launch_bounds__(NT, 1)
           store_b(nxt);
           load_b(min(st + 2, nst - 1) * BK);
         }
+        if constexpr (GROUP) {
 #pragma unroll
-        for (int y = 0; y < TN; ++y) mfma3(x, y, x & 1);
+          for (int y = 0; y < TN; ++y)
+            acc[x][y] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al[x & 1], b_h[y], acc[x][y], 0, 0, 0);
+#pragma unroll
+          for (int y = 0; y < TN; ++y)
+            acc[x][y] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[x & 1], b_l[y], acc[x][y], 0, 0, 0);
+#pragma unroll
+          for (int y = 0; y < TN; ++y)
+            acc[x][y] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[x & 1], b_h[y], acc[x][y], 0, 0, 0);
+        } else {
+#pragma unroll
+          for (int y = 0; y < TN; ++y) mfma3(x, y, x & 1);
+        }
         __builtin_amdgcn_sched_barrier(0);
       }
       KGE_WAIT_VM(2);  // A(st + 1) has landed
@@ -253,12 +267,36 @@ __global__ void __launch_bounds__(NT, 1)
       asm volatile("" ::: "memory");
       read_a(nxt, 0, 0);
       __builtin_amdgcn_sched_barrier(0);
+      if constexpr (GROUP) {
+        constexpr int HS = (TM - 1) & 1;
 #pragma unroll
-      for (int y = 0; y < TN; ++y) {
-        mfma3(TM - 1, y, (TM - 1) & 1);
+        for (int y = 0; y < TN; ++y)
+          acc[TM - 1][y] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al[HS], b_h[y], acc[TM - 1][y], 0, 0, 0);
         __builtin_amdgcn_sched_barrier(0);
-        read_b(nxt, y);
-        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int y = 0; y < TN; ++y) {
+          acc[TM - 1][y] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[HS], b_l[y], acc[TM - 1][y], 0, 0, 0);
+          __builtin_amdgcn_sched_barrier(0);
+          const int rb_ = wc * WCOLS + y * 16 + fr;
+          b_l[y] = *reinterpret_cast<const bf16x8*>(nxt + 2 * PLANE_A + PLANE_B + sw16_off(rb_, fs));
+          __builtin_amdgcn_sched_barrier(0);
+        }
+#pragma unroll
+        for (int y = 0; y < TN; ++y) {
+          acc[TM - 1][y] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[HS], b_h[y], acc[TM - 1][y], 0, 0, 0);
+          __builtin_amdgcn_sched_barrier(0);
+          const int rb_ = wc * WCOLS + y * 16 + fr;
+          b_h[y] = *reinterpret_cast<const bf16x8*>(nxt + 2 * PLANE_A + sw16_off(rb_, fs));
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      } else {
+#pragma unroll
+        for (int y = 0; y < TN; ++y) {
+          mfma3(TM - 1, y, (TM - 1) & 1);
+          __builtin_amdgcn_sched_barrier(0);
+          read_b(nxt, y);
+          __builtin_amdgcn_sched_barrier(0);
+        }
       }
     }
   } else
@@ -355,7 +393,7 @@ __device__ __forceinline__ bf16x8 tr_frag16(const unsigned char* img, int c0, in
 // NSTG LDS stage buffers: 2 = the next stage's transfers are in flight during a stage's MFMAs;
 // 3 = the next two stages' (144 KB of LDS), which covers HBM latency when the G planes are not
 // resident in the memory-side cache.
-template <int NSTG>
+template <int NSTG, bool GROUP>
 __global__ void __launch_bounds__(NT, 1)
     bwd3p_t_kernel(const __bf16* __restrict__ ghi, const __bf16* __restrict__ glo, int64_t ldgp, int64_t gcols,
                    const __bf16* __restrict__ qhi, const __bf16* __restrict__ qlo, int64_t ldqp, int64_t qcols,
@@ -425,11 +463,23 @@ __global__ void __launch_bounds__(NT, 1)
     for (int x = 0; x < TM; ++x) {
       const bf16x8 a_h = tr_frag16<BM>(ahi, wr * (BM / WM) + x * 16, lane);
       const bf16x8 a_l = tr_frag16<BM>(alo, wr * (BM / WM) + x * 16, lane);
+      if constexpr (GROUP) {
 #pragma unroll
-      for (int y = 0; y < TN; ++y) {
-        acc[x][y] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a_l, b_h[y], acc[x][y], 0, 0, 0);
-        acc[x][y] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a_h, b_l[y], acc[x][y], 0, 0, 0);
-        acc[x][y] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a_h, b_h[y], acc[x][y], 0, 0, 0);
+        for (int y = 0; y < TN; ++y)
+          acc[x][y] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a_l, b_h[y], acc[x][y], 0, 0, 0);
+#pragma unroll
+        for (int y = 0; y < TN; ++y)
+          acc[x][y] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a_h, b_l[y], acc[x][y], 0, 0, 0);
+#pragma unroll
+        for (int y = 0; y < TN; ++y)
+          acc[x][y] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a_h, b_h[y], acc[x][y], 0, 0, 0);
+      } else {
+#pragma unroll
+        for (int y = 0; y < TN; ++y) {
+          acc[x][y] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a_l, b_h[y], acc[x][y], 0, 0, 0);
+          acc[x][y] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a_h, b_l[y], acc[x][y], 0, 0, 0);
+          acc[x][y] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a_h, b_h[y], acc[x][y], 0, 0, 0);
+        }
       }
     }
   };
@@ -478,6 +528,7 @@ __global__ void __launch_bounds__(NT, 1)
 
 int g_bwdp_pipe = 1;    // dev builds can switch the dQ kernel back to its plain loop (kge_dev_bwdp_pipe)
 int g_bwdp_stages = 3;  // ... and the dE kernel back to two LDS stage buffers (kge_dev_bwdp_stages)
+int g_bwdp_group = 3;   // ... bit 0: dQ, bit 1: dE with the grouped MFMA order; 0: accumulator by accumulator (kge_dev_bwdp_group)
 
 int splits_q(int64_t n, int64_t m, int d, int cus) {
   const int64_t tiles = ((n + BM - 1) / BM) * ((d + BN - 1) / BN);
@@ -519,14 +570,16 @@ extern "C" int kge_score_dot_bwd_q_planes(const void* g_hi, const void* g_lo, in
   hipStream_t st = as_stream(stream);
   static std::atomic<bool> lds_ok[KGE_MAX_DEVICES];
   static std::atomic<bool> lds_ok_plain[KGE_MAX_DEVICES];
-  const bool pipe = g_bwdp_pipe != 0;
-  if (const int e = pipe ? kge_allow_lds((const void*)bwd3p_q_kernel<true>, 2 * STAGE, lds_ok)
-                         : kge_allow_lds((const void*)bwd3p_q_kernel<false>, 2 * STAGE, lds_ok_plain))
+  static std::atomic<bool> lds_ok_group[KGE_MAX_DEVICES];
+  const bool pipe = g_bwdp_pipe != 0, group = pipe && (g_bwdp_group & 1);
+  if (const int e = group  ? kge_allow_lds((const void*)bwd3p_q_kernel<true, true>, 2 * STAGE, lds_ok_group)
+                    : pipe ? kge_allow_lds((const void*)bwd3p_q_kernel<true, false>, 2 * STAGE, lds_ok)
+                           : kge_allow_lds((const void*)bwd3p_q_kernel<false, false>, 2 * STAGE, lds_ok_plain))
     return e;
   const int nrt = (int)((n + BM - 1) / BM), nct = (d + BN - 1) / BN;
   const int64_t blocks = (int64_t)nrt * nct * splits;
   if (blocks > 0x7fffffff) return KGE_ERR_ARG;
-  auto kern = pipe ? bwd3p_q_kernel<true> : bwd3p_q_kernel<false>;
+  auto kern = group ? bwd3p_q_kernel<true, true> : pipe ? bwd3p_q_kernel<true, false> : bwd3p_q_kernel<false, false>;
   kern<<<dim3((unsigned)blocks), dim3(NT), 2 * STAGE, st>>>((const __bf16*)g_hi, (const __bf16*)g_lo, ldgp, t, ldt, (int)n,
                                                             d, (int)m, kchunk, nrt, nct, ws);
   KGE_CHECK_LAUNCH();
@@ -551,14 +604,16 @@ extern "C" int kge_score_dot_bwd_t_planes(const void* g_hi, const void* g_lo, in
   hipStream_t st = as_stream(stream);
   static std::atomic<bool> lds_ok[KGE_MAX_DEVICES];
   static std::atomic<bool> lds_ok2[KGE_MAX_DEVICES];
-  const bool three = g_bwdp_stages == 3;
-  if (const int e = three ? kge_allow_lds((const void*)bwd3p_t_kernel<3>, 3 * STAGE, lds_ok)
-                          : kge_allow_lds((const void*)bwd3p_t_kernel<2>, 2 * STAGE, lds_ok2))
+  static std::atomic<bool> lds_ok_group[KGE_MAX_DEVICES];
+  const bool three = g_bwdp_stages == 3, group = three && (g_bwdp_group & 2);
+  if (const int e = group   ? kge_allow_lds((const void*)bwd3p_t_kernel<3, true>, 3 * STAGE, lds_ok_group)
+                    : three ? kge_allow_lds((const void*)bwd3p_t_kernel<3, false>, 3 * STAGE, lds_ok)
+                            : kge_allow_lds((const void*)bwd3p_t_kernel<2, false>, 2 * STAGE, lds_ok2))
     return e;
   const int nrt = (int)((m + BM - 1) / BM), nct = (d + BN - 1) / BN;
   const int64_t blocks = (int64_t)nrt * nct;
   if (blocks > 0x7fffffff) return KGE_ERR_ARG;
-  auto kern = three ? bwd3p_t_kernel<3> : bwd3p_t_kernel<2>;
+  auto kern = group ? bwd3p_t_kernel<3, true> : three ? bwd3p_t_kernel<3, false> : bwd3p_t_kernel<2, false>;
   kern<<<dim3((unsigned)blocks), dim3(NT), (three ? 3 : 2) * STAGE, st>>>(
       (const __bf16*)g_hi, (const __bf16*)g_lo, ldgp, gcols, (const __bf16*)q_hi, (const __bf16*)q_lo, ldqp, qcols,
       (int)m, d, (int)n_pad, nct, dt, lddt, accumulate, gscale);
@@ -569,4 +624,5 @@ extern "C" int kge_score_dot_bwd_t_planes(const void* g_hi, const void* g_lo, in
 #ifdef KGE_DEV_BUILD  // libkgescore_dev.so only
 extern "C" void kge_dev_bwdp_pipe(int on) { g_bwdp_pipe = on; }
 extern "C" void kge_dev_bwdp_stages(int n) { g_bwdp_stages = n == 2 ? 2 : 3; }
+extern "C" void kge_dev_bwdp_group(int mask) { g_bwdp_group = mask & 3; }
 #endif
