@@ -508,34 +508,70 @@ __global__ void __launch_bounds__(NT) rank_rows_kernel(const RankRowsArgs a) {
 }
 
 // out[0] = max over rows of the Euclidean row norm (out[0] must hold 0 on entry): a wave per
-// row, 2 rows per wave (a wave's rows are read one after the other, each a chain of dependent
-// loads: many short workgroups hide that latency, few long ones do not -- 43 us at 16 rows per
-// wave for a 30-MB table), one atomic per workgroup
+// row, 2 rows per wave, one atomic per workgroup (many short workgroups: a wave's loads are few
+// and its reduction depends on all of them -- 43 us at 16 rows per wave for a 30-MB table).
+// VEC (rows of a multiple of 4 floats, 16-B aligned): both rows of a wave are read together as
+// float4s, all of their loads in flight before the first is used.
 constexpr int NORM_ROWS = 8;
+template <bool VEC>
 __global__ void __launch_bounds__(256) row_norm_max_kernel(const float* __restrict__ t, int64_t ldt, int64_t m, int d,
                                                            float* out) {
   __shared__ float wmax[4];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   float best = 0.f;
-  for (int i = 0; i < NORM_ROWS / 4; ++i) {
-    const int64_t r = (int64_t)blockIdx.x * NORM_ROWS + wave * (NORM_ROWS / 4) + i;
-    if (r >= m) break;  // wave-uniform
-    float ss = 0.f;
-    for (int k = lane; k < d; k += 64) {
-      const float v = t[r * ldt + k];
-      ss += v * v;
-    }
+  auto take = [&](float ss) {
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) ss += __shfl_xor(ss, off, 64);
     ss = sqrtf(ss) * 1.000001f;
     best = (ss > best || ss != ss) ? ss : best;  // a NaN row poisons the maximum
+  };
+  if constexpr (VEC) {
+    static_assert(NORM_ROWS == 8, "two rows per wave");
+    const int64_t r0 = (int64_t)blockIdx.x * NORM_ROWS + wave * 2;
+    if (r0 < m) {  // wave-uniform
+      const int64_t r1 = r0 + 1 < m ? r0 + 1 : r0;  // a last odd row is read twice
+      const float4* a = reinterpret_cast<const float4*>(t + r0 * ldt);
+      const float4* b = reinterpret_cast<const float4*>(t + r1 * ldt);
+      float sa = 0.f, sb = 0.f;
+      const int d4 = d / 4;
+      int k = lane;
+      for (; k + 64 < d4; k += 128) {  // four loads in flight
+        const float4 a0 = a[k], b0 = b[k], a1 = a[k + 64], b1 = b[k + 64];
+        sa += a0.x * a0.x + a0.y * a0.y + a0.z * a0.z + a0.w * a0.w;
+        sb += b0.x * b0.x + b0.y * b0.y + b0.z * b0.z + b0.w * b0.w;
+        sa += a1.x * a1.x + a1.y * a1.y + a1.z * a1.z + a1.w * a1.w;
+        sb += b1.x * b1.x + b1.y * b1.y + b1.z * b1.z + b1.w * b1.w;
+      }
+      if (k < d4) {
+        const float4 a0 = a[k], b0 = b[k];
+        sa += a0.x * a0.x + a0.y * a0.y + a0.z * a0.z + a0.w * a0.w;
+        sb += b0.x * b0.x + b0.y * b0.y + b0.z * b0.z + b0.w * b0.w;
+      }
+      take(sa);
+      take(sb);
+    }
+  } else {
+    for (int i = 0; i < NORM_ROWS / 4; ++i) {
+      const int64_t r = (int64_t)blockIdx.x * NORM_ROWS + wave * (NORM_ROWS / 4) + i;
+      if (r >= m) break;  // wave-uniform
+      float ss = 0.f;
+      for (int k = lane; k < d; k += 64) {
+        const float v = t[r * ldt + k];
+        ss += v * v;
+      }
+      take(ss);
+    }
   }
   if (lane == 0) wmax[wave] = best;
   __syncthreads();
   if (threadIdx.x == 0) {
     for (int w = 1; w < 4; ++w) best = (wmax[w] > best || wmax[w] != wmax[w]) ? wmax[w] : best;
-    // non-negative floats order like their bit patterns (NaN above every number)
-    atomicMax(reinterpret_cast<unsigned*>(out), __float_as_uint(best));
+    // non-negative floats order like their bit patterns (NaN above every number).  The maximum only
+    // grows, so a workgroup whose rows do not exceed the value it reads (possibly a stale, i.e.
+    // lower, one) has nothing to add: all but a few skip the atomic, which the L2 would otherwise
+    // serialise over a thousand workgroups on one address.
+    unsigned* o = reinterpret_cast<unsigned*>(out);
+    if (__float_as_uint(best) > *reinterpret_cast<volatile unsigned*>(o)) atomicMax(o, __float_as_uint(best));
   }
 }
 
@@ -661,8 +697,13 @@ extern "C" int kge_row_norm_max(const float* t, int64_t ldt, int64_t m, int d, f
   KGE_REQUIRE(m >= 0 && d > 0 && (t || m == 0) && out && ldt >= d);
   hipStream_t st = as_stream(stream);
   zero1_kernel<<<dim3(1), dim3(1), 0, st>>>(out);
-  if (m > 0)
-    row_norm_max_kernel<<<dim3((unsigned)((m + NORM_ROWS - 1) / NORM_ROWS)), dim3(256), 0, st>>>(t, ldt, m, d, out);
+  if (m > 0) {
+    const dim3 grid((unsigned)((m + NORM_ROWS - 1) / NORM_ROWS));
+    if (d % 4 == 0 && ldt % 4 == 0 && aligned16(t))
+      row_norm_max_kernel<true><<<grid, dim3(256), 0, st>>>(t, ldt, m, d, out);
+    else
+      row_norm_max_kernel<false><<<grid, dim3(256), 0, st>>>(t, ldt, m, d, out);
+  }
   KGE_CHECK_LAUNCH();
   return 0;
 }

@@ -5,6 +5,8 @@
 * its refinement of reduced-precision scores: counts must EQUAL those of exactly computed
   scores (float64 dot products rounded to fp32) on inputs built to be full of near-ties that
   the bf16x3 contraction mis-orders."""
+import math
+
 import numpy as np
 import pytest
 import torch
@@ -492,3 +494,21 @@ def test_prep_split2_band_matches_separate_launches(L, model, d):
     # and against float64: the band is never narrower than band_rel |q| tmax
     exact = 7e-5 * q0.double().norm(dim=1) * float(tmax)
     assert bool((b1.double() >= exact * (1 - 1e-7)).all())
+
+
+@pytest.mark.parametrize("m,d,ld", [(1, 4, 4), (7, 512, 512), (1001, 516, 516), (333, 260, 264), (65, 1000, 1000),
+                                    (50, 30, 31), (14541, 512, 512)])
+def test_row_norm_max_is_a_tight_upper_bound_of_the_largest_row_norm(L, m, d, ld):
+    """kge_row_norm_max (the table factor of the refinement band): never below the largest
+    Euclidean row norm in float64, at most a few 1e-6 above it -- on the float4 path (rows of a
+    multiple of 4 floats, 16-B aligned; odd row counts, a d / 4 that is not a multiple of 64 or
+    128) and on the scalar path (d = 30, ld = 31); a NaN row poisons it."""
+    g = torch.Generator().manual_seed(m * 1000 + d)
+    buf = torch.randn(m, ld, generator=g).cuda()
+    t = buf[:, :d]
+    want = float(t.double().norm(dim=1).max())
+    got = float(L.row_norm_max(t))
+    assert want <= got <= want * (1 + 1e-5), (want, got)
+    if m > 1:
+        buf[m - 1, d - 1] = float("nan")
+        assert math.isnan(float(L.row_norm_max(t)))
