@@ -105,6 +105,7 @@ class EntityRankingJob(EvaluationJob):
         self._refine = False  # set per run from engine.eval_precision
         self._streams = None  # engine.BatchStreams, made by the first run
         self._rank_weights = None  # [2, E] fp64: ranks 1..E and their fp32 reciprocals
+        self._graph_state = {}  # engine.graph_eval: the recorded device pass and what it depends on
         self.ranks: Dict[str, np.ndarray] = {}
 
     # ---------------------------------------------------------------- preparation
@@ -265,13 +266,7 @@ class EntityRankingJob(EvaluationJob):
         sharded = self._sharded_scorer()
         chunk = self.config.get("entity_ranking.chunk_size")
         chunk = E if chunk is None or chunk < 0 else chunk
-        #: [ranking, direction (tail "o", head "s"), rank] histograms
-        hists_d = torch.zeros(nrank, 2, E, device=dev)
-        hists_flat = hists_d.view(nrank * 2, E)
         hists_sharded = torch.zeros(2, nrank, E, device=dev) if sharded is not None else None
-        group_hists = {name: torch.zeros(nrank, 2, len(names) + 1, E, device=dev)
-                       for name, (names, _) in self._groups.items()}
-        tmax = None
         ent_rows = None
         self._shard_refinement = None
         if sharded is not None:
@@ -312,21 +307,33 @@ class EntityRankingJob(EvaluationJob):
                 self._fused_rank = True
                 if ent_rows is None:
                     ent_rows = tabs[0].detach()
-        ranks_out = {f"{d}{r}": [] for d in "so" for r in self.rankings}
-        epoch_time = -time.time()
         N = len(self.triples)
-        if self._refine:
-            tmax = _lib.row_norm_max(ent_rows)  # ahead of the batches: every stream reads it
-        # independent batches take turns on engine.eval_streams HIP streams; every accumulation
-        # across batches (histograms, group counts) is an atomic add of exact small integers.
-        # The row-sharded path stays on one stream: its collectives are ordered per process.
         if self._streams is None:
+            # independent batches take turns on engine.eval_streams HIP streams; every accumulation
+            # across batches (histograms, group counts) is an atomic add of exact small integers.
+            # The row-sharded path stays on one stream: its collectives are ordered per process.
             from ..engine import BatchStreams
 
             self._streams = BatchStreams(dev, self.config.get("engine.eval_streams"))
-        with self._streams if sharded is None else contextlib.nullcontext():
-            self._rank_batches(N, E, chunk, sharded, nrank, hists_flat, hists_sharded, group_hists, ranks_out,
-                               ent_rows, tmax)
+
+        def device_pass(hists, ghists, ranks_out):
+            """All device work of the run: adds every batch's ranks to the (zeroed) histograms."""
+            tmax = _lib.row_norm_max(ent_rows) if self._refine else None  # ahead of the batches: every stream reads it
+            with self._streams if sharded is None else contextlib.nullcontext():
+                self._rank_batches(N, E, chunk, sharded, nrank, hists.view(nrank * 2, E), hists_sharded, ghists,
+                                   ranks_out, ent_rows, tmax)
+
+        epoch_time = -time.time()
+        recorded = self._recorded_pass(device_pass, sharded, nrank, E, chunk, ent_rows) if sharded is None else None
+        if recorded is not None:
+            hists_d, group_hists, ranks_out = recorded
+        else:
+            #: [ranking, direction (tail "o", head "s"), rank] histograms
+            hists_d = torch.zeros(nrank, 2, E, device=dev)
+            group_hists = {name: torch.zeros(nrank, 2, len(names) + 1, E, device=dev)
+                           for name, (names, _) in self._groups.items()}
+            ranks_out = {f"{d}{r}": [] for d in "so" for r in self.rankings}
+            device_pass(hists_d, group_hists, ranks_out)
         epoch_time += time.time()
         metrics = {}
         if hists_sharded is not None:
@@ -360,6 +367,63 @@ class EntityRankingJob(EvaluationJob):
         if was_training:
             self.model.train()
         return trace
+
+    def _recorded_pass(self, device_pass, sharded, nrank, E, chunk, ent_rows):
+        """engine.graph_eval: the device work of an evaluation run -- every batch of the split, on
+        all of its streams -- recorded ONCE as a HIP graph and replayed by every later run of this
+        job (a training job validates with one EntityRankingJob, epoch after epoch).  The split, the
+        filter lists, the grouping and every shape are fixed per job, and the kernels read the
+        model's tables through their addresses, so a replay ranks with the weights as they are then.
+        The host otherwise spends as long issuing the ~100 launches of a run as the device spends
+        running them.  The first run of a configuration is eager (kernel attributes, allocator),
+        the second is recorded; anything the recording depends on (tables re-created, another
+        precision, ranks to capture, ...) is part of its key, and a changed key starts over.
+        Returns (histograms, group histograms, ranks) of this run, or None: run eagerly."""
+        st = self._graph_state
+        if (st.get("disabled") or not self.config.get("engine.graph_eval")
+                or torch.device(self.device).type != "cuda" or torch.cuda.is_current_stream_capturing()):
+            return None
+        tabs = self.model._lookup_tables()
+        if tabs is None or self.model.get_scorer().engine_kind is None:
+            return None  # embedders / scorers outside the engine may synchronise
+        stacked = [t for part in self._stacked if part is not None for t in part]
+        key = (tuple((t.data_ptr(), tuple(t.shape)) for t in tabs), ent_rows.data_ptr() if ent_rows is not None else 0,
+               tuple(t.data_ptr() for t in stacked), self._stack_e.data_ptr(), self._stack_p.data_ptr(),
+               tuple((name, ids.data_ptr()) for name, (_, ids) in self._groups.items()),
+               nrank, E, chunk, self._bs, self._refine, self._fused_rank, self._two_sided, self.tie_handling,
+               self.capture_ranks, len(self._streams.streams), self.model.get_scorer().precision_override)
+        if st.get("key") != key:  # first run of this configuration: eager
+            st.clear()
+            st["key"] = key
+            return None
+        if "graph" not in st:
+            dev = self.device
+            hists = torch.zeros(nrank, 2, E, device=dev)
+            ghists = {name: torch.zeros(nrank, 2, len(names) + 1, E, device=dev)
+                      for name, (names, _) in self._groups.items()}
+            ranks_out = {f"{d}{r}": [] for d in "so" for r in self.rankings}
+            g = torch.cuda.CUDAGraph()
+            try:
+                with torch.cuda.graph(g):
+                    hists.zero_()  # fill kernels (no memset nodes)
+                    for h in ghists.values():
+                        h.zero_()
+                    device_pass(hists, ghists, ranks_out)
+            except Exception as e:  # not recordable: this job evaluates eagerly from now on
+                import traceback
+
+                st.clear()
+                st["disabled"] = True
+                st["error"] = f"{type(e).__name__}: {e}\n{traceback.format_exc()}"
+                try:  # an invalidated capture reports its error once more at the next call
+                    torch.cuda.synchronize()
+                except Exception:
+                    pass
+                self.config.log(f"engine.graph_eval disabled: {st['error']}")
+                return None
+            st["graph"], st["out"] = g, (hists, ghists, ranks_out)
+        st["graph"].replay()
+        return st["out"]
 
     def _rank_batches(self, N, E, chunk, sharded, nrank, hists_flat, hists_sharded, group_hists, ranks_out,
                       ent_rows, tmax):

@@ -2,6 +2,9 @@
 device finishing it, and the metric arithmetic after it.
 
     python scripts/dev/eval_phases.py [streams] [head_and_tail 0|1] [fused_rank 0|1]
+
+KGE_GRAPH_EVAL=1: the runs with engine.graph_eval (recorded device pass) timed as a whole -- the
+phase marks synchronise inside the loop, which a recording cannot contain.
 """
 import os
 import sys
@@ -41,8 +44,21 @@ def main():
     torch.manual_seed(0)
     model = KgeModel.create(c, ds)
     model.eval()
+    graph = os.environ.get("KGE_GRAPH_EVAL", "0") == "1"
+    c.set("engine.graph_eval", graph)
     ej = EntityRankingJob(c, ds, model=model)
     ej._prepare()
+    if graph:
+        ts = []
+        for _ in range(10):
+            torch.cuda.synchronize()
+            a = time.perf_counter()
+            ej._run()
+            torch.cuda.synchronize()
+            ts.append((time.perf_counter() - a) * 1e3)
+        print(f"group {ej._bs} graph_eval: runs {' '.join(f'{t:.3f}' for t in ts)} ms (first eager, second records); "
+              f"median of the replays {np.median(ts[2:]):.3f} ms, recorded: {'graph' in ej._graph_state}", flush=True)
+        return
     inner = ej._rank_batches
     marks = {}
 

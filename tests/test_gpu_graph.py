@@ -613,3 +613,105 @@ def test_kvsall_graph_step_with_unweighted_penalty_matches_eager():
     assert batch["triples"].shape[1] == 3
     res, pen, _ = job.train_step(0, batch)
     assert float(pen) > 0
+
+
+@pytest.mark.parametrize("model_name,per", [("complex", True), ("distmult", False), ("transe", False)])
+def test_recorded_evaluation_pass_equals_eager_on_every_replay(model_name, per):
+    """engine.graph_eval: the job's first run is eager, its second records the device work of the
+    run (all batches, both streams) and replays it, later runs only replay.  Every run must give
+    the ranks and metrics of an eager job on the same weights -- also after the tables were
+    updated in place between runs (a replay reads the weights as they are then), with eager
+    device work and synchronisations between the replays."""
+    from kge import Config, Dataset, KgeModel
+    from kge.job import EntityRankingJob
+
+    def config(graph):
+        c = Config()
+        c.set("model", model_name)
+        c._import(model_name)
+        c.set("job.device", "cuda")
+        c.set("lookup_embedder.dim", 128)
+        c.set("lookup_embedder.initialize_args", {"mean": 0.0, "std": 0.1})
+        c.set("eval.split", "valid")
+        c.set("eval.batch_size", 256)
+        c.set("engine.eval_batch_size", 0)  # five batches, the last one partial
+        c.set("engine.graph_eval", graph)
+        c.set("entity_ranking.metrics_per.head_and_tail", per)
+        c.set("entity_ranking.metrics_per.relation_type", per)
+        c.set("verbose", False)
+        return c
+
+    c = config(True)
+    ds = Dataset.synthetic(c, "toy", seed=0, num_entities=1500, num_relations=7, sizes=(12000, 1100, 300))
+    torch.manual_seed(0)
+    model = KgeModel.create(c, ds)
+    model.eval()
+    job = EntityRankingJob(c, ds, model=model)
+    job.capture_ranks = True
+    eager = EntityRankingJob(config(False), ds, model=model)
+    eager.capture_ranks = True
+    g = torch.Generator(device="cuda").manual_seed(3)
+    ent = model._entity_embedder._embeddings.weight
+    rel = model._relation_embedder._embeddings.weight
+    states = []
+    for run in range(5):
+        if run in (2, 4):  # the tables change in place, as an optimizer step changes them
+            with torch.no_grad():
+                ent.add_(torch.randn(ent.shape, device="cuda", generator=g) * 0.05)
+                rel.add_(torch.randn(rel.shape, device="cuda", generator=g) * 0.05)
+        got = job.run()
+        got_ranks = {k: v.copy() for k, v in job.ranks.items()}
+        states.append("graph" in job._graph_state)
+        torch.cuda.synchronize()
+        want = eager.run()  # eager device work between the replays
+        assert "graph" not in eager._graph_state
+        for k, v in eager.ranks.items():
+            np.testing.assert_array_equal(got_ranks[k], v, err_msg=f"run {run} {k}")
+        for k, v in want.items():
+            if k != "epoch_time" and isinstance(v, float):
+                assert got[k] == v, (run, k)
+    assert states == [False, True, True, True, True], job._graph_state.get("error")
+    # a job that now has to capture other ranks starts over: eager, then recorded again
+    job.capture_ranks = False
+    job.run()
+    assert "graph" not in job._graph_state
+    job.run()
+    assert "graph" in job._graph_state
+
+
+def test_evaluation_that_cannot_be_recorded_runs_eagerly():
+    """A device pass that raises while it is being recorded (here: a hook that refuses to run under
+    stream capture) switches engine.graph_eval off for the job: the same run and every later one
+    evaluate eagerly, with the eager job's metrics."""
+    from kge import Config, Dataset, KgeModel
+    from kge.job import EntityRankingJob
+
+    c = Config()
+    c.set("model", "complex")
+    c._import("complex")
+    c.set("job.device", "cuda")
+    c.set("lookup_embedder.dim", 64)
+    c.set("lookup_embedder.initialize_args", {"mean": 0.0, "std": 0.1})
+    c.set("eval.split", "valid")
+    c.set("eval.batch_size", 128)
+    c.set("verbose", False)
+    ds = Dataset.synthetic(c, "toy", seed=1, num_entities=700, num_relations=5, sizes=(6000, 500, 100))
+    torch.manual_seed(0)
+    model = KgeModel.create(c, ds)
+    model.eval()
+    job = EntityRankingJob(c, ds, model=model)
+    first = job.run()
+    inner = job._rank_batches
+
+    def refuses_capture(*a, **k):
+        if torch.cuda.is_current_stream_capturing():
+            raise RuntimeError("not under capture")
+        return inner(*a, **k)
+
+    job._rank_batches = refuses_capture
+    for _ in range(3):
+        again = job.run()
+        assert job._graph_state.get("disabled") and "not under capture" in job._graph_state["error"]
+        for k, v in first.items():
+            if k != "epoch_time" and isinstance(v, float):
+                assert again[k] == v, k
