@@ -571,7 +571,8 @@ __global__ void __launch_bounds__(256) row_norm_max_kernel(const float* __restri
     // lower, one) has nothing to add: all but a few skip the atomic, which the L2 would otherwise
     // serialise over a thousand workgroups on one address.
     unsigned* o = reinterpret_cast<unsigned*>(out);
-    if (__float_as_uint(best) > *reinterpret_cast<volatile unsigned*>(o)) atomicMax(o, __float_as_uint(best));
+    if (__float_as_uint(best) > __hip_atomic_load(o, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+      atomicMax(o, __float_as_uint(best));
   }
 }
 

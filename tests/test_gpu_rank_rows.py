@@ -328,7 +328,26 @@ def _near_tie_tables(rng, n, m, d, copies):
     return q, t, true_idx
 
 
-@pytest.mark.parametrize("n_a,n_b,m,c0,d,with_test,refined,max_filt,ld_pad", [
+def _random_rank_cases(count, seed=20):
+    """Seeded random shapes for the fused-ranking test: ragged batches (the second one empty now and
+    then), entity counts around and between the 256-column panels, row widths that are multiples of 4
+    but not of the 32-column K stage, chunk offsets, padded code rows."""
+    rng = np.random.default_rng(seed)
+    cases = []
+    for _ in range(count):
+        n_a = int(rng.integers(5, 420))
+        n_b = 0 if rng.random() < 0.2 else (n_a if rng.random() < 0.3 else int(rng.integers(1, 420)))
+        m = int(rng.choice([rng.integers(n_a + n_b, n_a + n_b + 300), rng.integers(1000, 6000),
+                            256 * rng.integers(4, 12) + rng.integers(-1, 2)]))
+        m = max(m, n_a + n_b)
+        c0 = int(rng.choice([0, 0, rng.integers(1, 900)]))
+        max_filt = min(int(rng.choice([3, 30, 300])), (c0 + m + 40) // 2)  # lists drawn without replacement
+        cases.append((n_a, n_b, m, c0, int(rng.choice([8, 20, 36, 64, 100, 132, 256, 516])), bool(rng.random() < 0.5),
+                      bool(rng.random() < 0.7), max_filt, int(rng.choice([0, 0, 1, 2, 3]))))
+    return cases
+
+
+@pytest.mark.parametrize("n_a,n_b,m,c0,d,with_test,refined,max_filt,ld_pad", _random_rank_cases(12) + [
     (300, 300, 3001, 0, 512, True, True, 30, 0),     # two 256-row tiles per batch, a ragged last entity panel
     (100, 100, 1000, 700, 128, True, True, 30, 0),   # 128-row tiles; a chunk starting at column 700
     (64, 0, 257, 0, 64, False, True, 30, 0),         # one batch; one column past a panel
