@@ -349,6 +349,17 @@ class _ScoreXentPlanes(torch.autograd.Function):
 
 
 _ARANGE = {}
+_ZEROS_I64 = {}
+
+
+def _zeros_i64(n: int, device) -> torch.Tensor:
+    """n int64 zeros on the device, kept and shared (read-only: the label vector "column 0")."""
+    key = (n, str(device))
+    if key not in _ZEROS_I64:
+        if torch.cuda.is_current_stream_capturing():
+            return torch.zeros(n, dtype=torch.int64, device=device)  # recorded with the step
+        _ZEROS_I64[key] = torch.zeros(n, dtype=torch.int64, device=device)
+    return _ZEROS_I64[key]
 
 
 def _arange(n: int, device) -> torch.Tensor:
@@ -712,8 +723,20 @@ class _ScoreCand(torch.autograd.Function):
         kind, direction, l_norm, n, d_e, d_r = ctx.meta
         ent, eidx, rel, ridx, cand, q, s, srt, col = ctx.saved_tensors
         need_ent, need_rel = ctx.needs_input_grad[3], ctx.needs_input_grad[5]
-        d_ent = torch.zeros_like(ent) if need_ent else None
-        d_rel = torch.zeros_like(rel) if need_rel else None
+        # Inside a training job's step (in_place_row_gradients) a dense gradient that an earlier
+        # backward of the step left in .grad -- the other corrupted slot's -- takes this one's rows
+        # where it stands: every kernel below accumulates, so neither a zero fill of a table-sized
+        # buffer nor autograd's sum of two of them is needed.
+        from .model.embedder.lookup_embedder import _in_place_ok
+
+        def held(t):  # the dense gradient a leaf table already holds, if this backward may add to it
+            g_t = t.grad if t.is_leaf and t.requires_grad else None
+            return g_t if g_t is not None and g_t.is_contiguous() and _in_place_ok(g_t, t, torch.float32) else None
+
+        ent_in_place = need_ent and held(ent) is not None
+        rel_in_place = need_rel and held(rel) is not None
+        d_ent = ent.grad if ent_in_place else (torch.zeros_like(ent) if need_ent else None)
+        d_rel = rel.grad if rel_in_place else (torch.zeros_like(rel) if need_rel else None)
         dq = torch.empty_like(q) if (need_ent or need_rel) else None
         g = _rows(g.float())
         # candidate rows repeat across queries: grouped per entity (sort) instead of atomics
@@ -726,7 +749,7 @@ class _ScoreCand(torch.autograd.Function):
             L.score_cand_bwd(kind, l_norm, direction, q, ent_w, cand, s, g, dq, None if ent_done else d_ent_w)
         if dq is not None:
             L.prep_query_bwd(kind, direction, ent, eidx, rel, ridx, n, d_e, d_r, dq, d_ent, d_rel)
-        return None, None, None, d_ent, None, d_rel, None, None
+        return (None, None, None, None if ent_in_place else d_ent, None, None if rel_in_place else d_rel, None, None)
 
 
 def score_cand(kind: int, direction: int, l_norm: float, ent: torch.Tensor, eidx: torch.Tensor, rel: torch.Tensor,
@@ -750,7 +773,7 @@ class _XentColumn0(torch.autograd.Function):
     def forward(ctx, scores, scale):
         s = _rows(scores.float())
         n = s.shape[0]
-        labels = torch.zeros(n, dtype=torch.int64, device=s.device)
+        labels = _zeros_i64(n, s.device)  # kept: no fill kernel per call
         g = torch.empty_like(s)
         loss_rows = L.softmax_xent(s, labels, scale, g=g)
         ctx.save_for_backward(g)

@@ -41,10 +41,12 @@ class _NSGraphStep(_GraphStep):
         triples = batch["triples"]
         if "negative_samples" in batch or triples.dim() != 2 or tuple(triples.shape) != (self.job.batch_size, 3):
             return None
-        return triples.long().reshape(-1)
+        # column-major: the recorded [B, 3] view below then has contiguous columns, which the scoring
+        # calls take as they are (a row-major block costs a copy kernel per column and slot)
+        return triples.long().t().reshape(-1)
 
     def _recorded_batch(self):
-        return {"triples": self.static.view(self.job.batch_size, 3)}
+        return {"triples": self.static.view(3, self.job.batch_size).t()}
 
     def _penalty_batch(self):
         return self._recorded_batch()

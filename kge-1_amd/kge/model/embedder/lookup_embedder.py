@@ -19,27 +19,43 @@ from ..kge_model import KgeEmbedder
 import contextlib
 import threading
 
-_state = threading.local()
+
+class _InPlaceState:
+    """Process-wide, not thread-local: the backward of a CUDA graph runs on autograd's device
+    thread, which a flag local to the calling thread never reaches."""
+
+    def __init__(self):
+        self.depth = 0
+        self.lock = threading.Lock()
+
+    @property
+    def on(self) -> bool:
+        return self.depth > 0
+
+
+_state = _InPlaceState()
 
 
 @contextlib.contextmanager
 def in_place_row_gradients():
-    """While active (this thread), the backward of embed() and of the recorded Lp penalty adds
-    its rows straight into a dense ``weight.grad`` that an earlier backward of the same step has
-    left, and hands autograd no gradient of its own.  That is only right when the caller wants
-    the gradients ACCUMULATED in ``.grad`` -- a training job around its own ``backward()`` calls.
-    Outside it the Functions return the dense gradient like any other op, so
+    """While active (process-wide: see _InPlaceState), the backward of embed(), of the recorded Lp
+    penalty and of the candidate scores adds its rows straight into a dense ``weight.grad`` that an
+    earlier backward of the same step has left, and hands autograd no gradient of its own.  That is
+    only right when the caller wants the gradients ACCUMULATED in ``.grad`` -- a training job
+    around its own ``backward()`` calls, with no other thread differentiating through the same
+    tables meanwhile.  Outside it the Functions return the dense gradient like any other op, so
     ``torch.autograd.grad``, gradient hooks and accumulation wrappers see it."""
-    prev = getattr(_state, "on", False)
-    _state.on = True
+    with _state.lock:
+        _state.depth += 1
     try:
         yield
     finally:
-        _state.on = prev
+        with _state.lock:
+            _state.depth -= 1
 
 
 def _in_place_ok(held, weight, dtype) -> bool:
-    return (getattr(_state, "on", False) and held is not None and not held.is_sparse and held.dtype == dtype
+    return (_state.on and held is not None and not held.is_sparse and held.dtype == dtype
             and held.shape == weight.shape and not torch.is_grad_enabled())
 
 

@@ -305,3 +305,59 @@ def test_recorded_ns_step_replays_like_the_eager_step(model, num_neg):
         off = int((diff > 2e-5 * b.abs().max()).sum())
         assert off <= 64 and float(diff.mean()) <= 1e-6 * float(b.abs().max()), (i, off, float(diff.mean()))
     assert len(set(loss_g)) == len(loss_g)  # every replay drew new negatives (and saw a new batch)
+
+
+def test_in_place_row_gradients_reach_the_backward_on_the_device(monkeypatch):
+    """in_place_row_gradients() must be seen by backward functions that autograd runs on its
+    DEVICE thread (every CUDA backward): the second corrupted slot of a negative-sampling step adds
+    its candidate and query rows into the gradient the first slot left (no zero fill of a
+    table-sized buffer, no sum of two of them), with the same gradients as the plain path."""
+    from kge import Config, Dataset
+    from kge.job import TrainingJob
+    from kge.model.embedder import lookup_embedder as le
+
+    def job():
+        c = Config()
+        c.set("model", "complex")
+        c._import("complex")
+        c.set("job.device", "cuda")
+        c.set("lookup_embedder.dim", 64)
+        c.set("lookup_embedder.initialize_args", {"mean": 0.0, "std": 0.1})
+        c.set("train.type", "negative_sampling")
+        c.set("train.loss", "kl")
+        c.set("negative_sampling.num_samples.s", 40)
+        c.set("negative_sampling.implementation", "triple")
+        c.set("train.optimizer", "Adagrad")
+        c.set("train.batch_size", 64)
+        c.set("engine.graph_step", False)
+        c.set("verbose", False)
+        ds = Dataset.synthetic(c, "toy", seed=0, num_entities=500, num_relations=5, sizes=(2000, 100, 100))
+        torch.manual_seed(0)
+        j = TrainingJob.create(c, ds)
+        j._prepare()
+        return j
+
+    seen = []
+    real = le._in_place_ok
+
+    def spy(held, weight, dtype):
+        ok = real(held, weight, dtype)
+        seen.append(ok)
+        return ok
+
+    monkeypatch.setattr(le, "_in_place_ok", spy)
+    a, b = job(), job()
+    batch = a._collate(torch.arange(64))
+    g = torch.Generator(device="cuda").manual_seed(5)
+    negs = [torch.randint(0, 500, (64, 40), device="cuda", generator=g) for _ in range(3)]
+    batch["negative_samples"] = negs
+    a.optimizer.zero_grad()
+    with le.in_place_row_gradients():
+        a.process_batch(0, batch)
+    assert any(seen), "no backward saw the in-place flag"
+    seen.clear()
+    b.optimizer.zero_grad()
+    b.process_batch(0, batch)  # outside the context: autograd sums the slots' gradients
+    assert not any(seen)
+    for pa, pb in zip(a.model.parameters(), b.model.parameters()):
+        torch.testing.assert_close(pa.grad, pb.grad, rtol=1e-5, atol=1e-7)
