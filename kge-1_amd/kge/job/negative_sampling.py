@@ -158,7 +158,7 @@ class TrainingJobNegativeSampling(TrainingJob):
                     for slot in (S, P, O)]
         prepare += time.time()
         fwd = bwd = 0.0
-        total = torch.zeros((), device=self.device)
+        total = None
         chunk = self._max_chunk_size if self._max_chunk_size > 0 else bs
         labels = None
         for c in range(math.ceil(bs / chunk)):
@@ -168,12 +168,13 @@ class TrainingJobNegativeSampling(TrainingJob):
                 ns = self._sampler.num_samples[slot]
                 if ns <= 0:
                     continue
-                if labels is None or labels.shape != (hi - lo, 1 + ns):
-                    labels = torch.zeros(hi - lo, 1 + ns, device=self.device)
-                    labels[:, 0] = 1.0
                 fwd -= time.time()
                 scores = self._scores(tr, slot, negs[slot][lo:hi])
-                if self._fused_loss is not None and scores.is_cuda:
+                fused = self._fused_loss is not None and scores.is_cuda
+                if not fused and (labels is None or labels.shape != (hi - lo, 1 + ns)):
+                    labels = torch.zeros(hi - lo, 1 + ns, device=self.device)  # only kge.util.loss reads them
+                    labels[:, 0] = 1.0
+                if fused:
                     from .. import engine
 
                     kind, arg = self._fused_loss
@@ -185,5 +186,7 @@ class TrainingJobNegativeSampling(TrainingJob):
                 bwd -= time.time()
                 loss.backward()
                 bwd += time.time()
-                total = total + loss.detach()
+                total = loss.detach() if total is None else total + loss.detach()
+        if total is None:
+            total = torch.zeros((), device=self.device)
         return TrainingJob._ProcessBatchResult(total.detach(), bs, prepare, fwd, bwd)
