@@ -184,7 +184,7 @@ class TrainingJobNegativeSampling(TrainingJob):
                     loss = self.loss(scores, labels, num_negatives=ns) / bs
                 fwd += time.time()
                 bwd -= time.time()
-                loss.backward()
+                self._backward(loss)
                 bwd += time.time()
                 total = loss.detach() if total is None else total + loss.detach()
         if total is None:

@@ -255,6 +255,14 @@ class TrainingJob(Job):
     def _collate(self, example_ids):
         raise NotImplementedError
 
+    def _backward(self, value: torch.Tensor):
+        """value.backward() for a 0-dim loss with a PERSISTENT seed gradient: autograd otherwise
+        makes ones_like(value) per call, a fill kernel that a recorded step replays every time."""
+        one = getattr(self, "_seed_one", None)
+        if one is None or one.device != value.device or one.dtype != value.dtype:
+            one = self._seed_one = torch.ones((), device=value.device, dtype=value.dtype)
+        value.backward(one)
+
     def _fused_loss_kind(self):
         """(kind, offset) of the loss the engine fuses into the scoring pass for this job --
         ("kl", 0.0) for train.loss kl (softmax cross entropy / KL), ("bce", loss_arg) for
@@ -303,7 +311,7 @@ class TrainingJob(Job):
         0-dim tensor (0.0 when nothing regularises) -- not read on the host here."""
         total = 0.0
         for _, pv in self.model.penalty(epoch=self.epoch, batch_index=batch_index, batch=batch):
-            pv.backward()
+            self._backward(pv) if pv.dim() == 0 else pv.backward()
             total = pv.detach() + total
         return total
 
@@ -613,7 +621,6 @@ class TrainingJob1vsAll(TrainingJob):
         self.type_str = "1vsAll"
         self._graph_step = None
         self._sharded = None
-        self._one = None
         #: compute ops of the row-sharded path; None: the engine (kge.sharded.EngineOps).
         #: Tests inject CPU ops here to run the exchange logic over gloo.
         self.sharded_ops = None
@@ -674,9 +681,7 @@ class TrainingJob1vsAll(TrainingJob):
             total, _ = both
             fwd += time.time()
             bwd = -time.time()
-            if self._one is None:
-                self._one = torch.ones((), device=total.device, dtype=total.dtype)
-            total.backward(self._one)  # a persistent seed gradient: no fill kernel per step
+            self._backward(total)  # a persistent seed gradient: no fill kernel per step
             bwd += time.time()
             return TrainingJob._ProcessBatchResult(total.detach(), bs, t, fwd, bwd)
         loss_sp = self.model.score_sp_xent(s_, p_, o_, 1.0 / bs) if fused else None
@@ -977,7 +982,7 @@ class TrainingJobKvsAll(TrainingJob):
             raise RuntimeError("the scorer cannot run both query types in one engine pass")
         total, per_type = losses
         bwd = -time.time()
-        total.backward()
+        self._backward(total)
         bwd += time.time()
         # both query types' losses: the caller picks the one the reference would report
         return TrainingJob._ProcessBatchResult(per_type, bs, 0.0, fwd, bwd)
@@ -1126,6 +1131,6 @@ class TrainingJobKvsAll(TrainingJob):
             return None
         total, per_type = losses
         bwd = -time.time()
-        total.backward()
+        self._backward(total)
         bwd += time.time()
         return TrainingJob._ProcessBatchResult(per_type[1], bs, t, fwd, bwd)
