@@ -309,11 +309,11 @@ class TrainingJob(Job):
     def _penalty_backward(self, batch_index, batch):
         """The penalty terms of the batch (train.py:320-337): backward on each, and their sum as a
         0-dim tensor (0.0 when nothing regularises) -- not read on the host here."""
-        total = 0.0
+        total = None
         for _, pv in self.model.penalty(epoch=self.epoch, batch_index=batch_index, batch=batch):
             self._backward(pv) if pv.dim() == 0 else pv.backward()
-            total = pv.detach() + total
-        return total
+            total = pv.detach() if total is None else pv.detach() + total
+        return 0.0 if total is None else total
 
     def _penalties_recordable(self, weighted_ok: bool) -> bool:
         """Whether the model's penalty terms can be part of a recorded step: none at all, or Lp
@@ -330,19 +330,25 @@ class TrainingJob(Job):
         return True
 
 
-class _LazyBatch(dict):
-    """A batch dict whose entries are made by a callable the first time they are read."""
+class _TripleColumns:
+    """A batch's triples as KgeModel.penalty reads them -- ``.to(device)``, then the index columns
+    ``[:, S]``, ``[:, P]``, ``[:, O]`` -- served from three contiguous device vectors: a recorded
+    step neither stacks them into a [B, 3] tensor nor copies its strided columns out again."""
 
-    def __init__(self, **makers):
-        super().__init__()
-        self._makers = makers
+    def __init__(self, s, p, o):
+        self._cols = (s, p, o)
 
-    def __missing__(self, key):
-        value = self[key] = self._makers[key]()
-        return value
+    def to(self, *args, **kwargs):
+        return self
 
-    def __contains__(self, key):
-        return dict.__contains__(self, key) or key in self._makers
+    def __len__(self):
+        return len(self._cols[0])
+
+    def __getitem__(self, key):
+        rows, col = key
+        if rows != slice(None) or not isinstance(col, int):
+            raise IndexError("only whole columns [:, S | P | O] of the recorded triples are served")
+        return self._cols[col]
 
 
 class _GraphStep:
@@ -407,7 +413,7 @@ class _GraphStep:
         s_row, o_row, p_row = (TrainingJob1vsAll.INDEX_BLOCK.index(c) for c in (S, O, P))
         # built on first use: only weighted penalties read the triples, and the stack is a kernel
         # that would otherwise be recorded into every step
-        return _LazyBatch(triples=lambda: torch.stack((cols[s_row], cols[p_row], cols[o_row]), 1))
+        return {"triples": _TripleColumns(cols[s_row], cols[p_row], cols[o_row])}
 
     # ---- the step
     def run(self, batch_index, batch):
