@@ -615,8 +615,15 @@ def test_kvsall_graph_step_with_unweighted_penalty_matches_eager():
     assert float(pen) > 0
 
 
-@pytest.mark.parametrize("model_name,per", [("complex", True), ("distmult", False), ("transe", False)])
-def test_recorded_evaluation_pass_equals_eager_on_every_replay(model_name, per):
+@pytest.mark.parametrize("model_name,per,extra", [
+    ("complex", True, {}), ("distmult", False, {}), ("transe", False, {}),
+    # entity chunks (counts accumulated over three chunks, histograms in a launch of their own)
+    ("complex", False, {"entity_ranking.chunk_size": 600}),
+    # a reciprocal-relations model: both directions' true scores, (?, p, o) as (o, p + R, ?)
+    ("reciprocal", False, {"entity_ranking.filter_with_test": False}),
+    ("complex", False, {"engine.eval_precision": "fp32", "engine.eval_streams": 1}),
+])
+def test_recorded_evaluation_pass_equals_eager_on_every_replay(model_name, per, extra):
     """engine.graph_eval: the job's first run is eager, its second records the device work of the
     run (all batches, both streams) and replays it, later runs only replay.  Every run must give
     the ranks and metrics of an eager job on the same weights -- also after the tables were
@@ -627,8 +634,14 @@ def test_recorded_evaluation_pass_equals_eager_on_every_replay(model_name, per):
 
     def config(graph):
         c = Config()
-        c.set("model", model_name)
-        c._import(model_name)
+        if model_name == "reciprocal":
+            c.set("model", "reciprocal_relations_model")
+            c._import("reciprocal_relations_model")
+            c.set("reciprocal_relations_model.base_model.type", "complex")
+            c._import("complex")
+        else:
+            c.set("model", model_name)
+            c._import(model_name)
         c.set("job.device", "cuda")
         c.set("lookup_embedder.dim", 128)
         c.set("lookup_embedder.initialize_args", {"mean": 0.0, "std": 0.1})
@@ -636,6 +649,8 @@ def test_recorded_evaluation_pass_equals_eager_on_every_replay(model_name, per):
         c.set("eval.batch_size", 256)
         c.set("engine.eval_batch_size", 0)  # five batches, the last one partial
         c.set("engine.graph_eval", graph)
+        for k, v in extra.items():
+            c.set(k, v)
         c.set("entity_ranking.metrics_per.head_and_tail", per)
         c.set("entity_ranking.metrics_per.relation_type", per)
         c.set("verbose", False)
@@ -651,8 +666,7 @@ def test_recorded_evaluation_pass_equals_eager_on_every_replay(model_name, per):
     eager = EntityRankingJob(config(False), ds, model=model)
     eager.capture_ranks = True
     g = torch.Generator(device="cuda").manual_seed(3)
-    ent = model._entity_embedder._embeddings.weight
-    rel = model._relation_embedder._embeddings.weight
+    ent, rel = (t for t in model._lookup_tables())
     states = []
     for run in range(5):
         if run in (2, 4):  # the tables change in place, as an optimizer step changes them
