@@ -334,7 +334,6 @@ class EntityRankingJob(EvaluationJob):
                            for name, (names, _) in self._groups.items()}
             ranks_out = {f"{d}{r}": [] for d in "so" for r in self.rankings}
             device_pass(hists_d, group_hists, ranks_out)
-        epoch_time += time.time()
         metrics = {}
         if hists_sharded is not None:
             hists_d += hists_sharded.permute(1, 0, 2)
@@ -356,6 +355,9 @@ class EntityRankingJob(EvaluationJob):
         suffixes = [RANKING_SUFFIX[r] + ("_" + key if key != "all" else "")
                     for key in keyed for r in self.rankings]
         metrics.update(self._compute_metrics_stacked(torch.cat(list(keyed.values())), suffixes))
+        # closed after the metrics (entity_ranking.py:111, 388): their device-to-host copy waits for
+        # the batches, so this is the run's wall time, not the time it took to issue it
+        epoch_time += time.time()
         if self.capture_ranks:
             self.ranks = {k: torch.cat(v).cpu().numpy() if v else np.zeros(0, np.int64)
                           for k, v in ranks_out.items()}
