@@ -342,6 +342,18 @@ int kge_softmax_grad_planes(const float* s, int64_t lds, int64_t n, int64_t n_pa
                             int64_t c0, const int64_t* labels, const float* lse, float scale,
                             float* planes, int64_t ld, void* stream);
 
+/* The same planes for train.loss bce on a row shard (loss.py:137-158 BCEWithLogitsKgeLoss, reduction
+ * "sum", on scores + offset against the one-hot rows of 1vsAll, train.py:1041-1057): G = scale *
+ * (sigmoid(s + offset) - y), y = 1 in column labels[i] - c0 when that lies in [0, m).  Binary cross
+ * entropy couples no columns, so a shard needs nothing from the others.  loss_part [n,
+ * kge_grad_planes_chunks(ld)] receives each column chunk's share of row i's loss,
+ * sum_j softplus(x_ij) - y_ij x_ij (unscaled; the caller sums it in a fixed order); rows
+ * [n, n_pad) of loss_part are not written. */
+int64_t kge_grad_planes_chunks(int64_t ld);
+int kge_bce_grad_planes(const float* s, int64_t lds, int64_t n, int64_t n_pad, int64_t m, int64_t c0,
+                        const int64_t* labels, float offset, float scale, float* planes, int64_t ld,
+                        float* loss_part, void* stream);
+
 /* ---- per-row candidate lists (negative sampling) -------------------------------------
  * out[i, c] = score(Q[i, :], ent[cand[i, c], :])  i in [0, n), c in [0, k), with the
  * semantics of KgeModel.score_spo on the triple the candidate completes (kge_model.py:620-637):

@@ -747,11 +747,17 @@ extern "C" int kge_softmax_row_stats(const float* s, int64_t lds, int64_t n, int
 // [m, ld) and rows [n, n_pad) are zeroed (K padding of the GEMMs).
 constexpr int GP_CH = 4096;  // columns per workgroup
 
-template <bool VEC>
+// BCE: the same planes for binary cross entropy with logits on x = s + offset against the one-hot
+// label row (loss.py:137-158, reduction "sum"): G = scale (sigmoid(x) - y), and the chunk's share of
+// the row's loss, sum_j softplus(x_j) - y_j x_j, into loss_part[row][chunk] (summed by the caller
+// in a fixed order).  Nothing couples the columns, so a shard needs no statistics of the others.
+template <bool VEC, bool BCE = false>
 __global__ void __launch_bounds__(NT) grad_planes_kernel(const float* __restrict__ s, int64_t lds, int n, int m,
                                                          int64_t c0, const int64_t* __restrict__ labels,
                                                          const float* __restrict__ lse, float scale,
-                                                         float* __restrict__ planes, int64_t ld) {
+                                                         float* __restrict__ planes, int64_t ld, float offset = 0.f,
+                                                         float* __restrict__ loss_part = nullptr) {
+  __shared__ float red[NT / 64];
   const int64_t row = blockIdx.y;
   const int tid = threadIdx.x;
   const int64_t j0 = (int64_t)blockIdx.x * GP_CH, j1 = min(j0 + GP_CH, ld);
@@ -765,8 +771,9 @@ __global__ void __launch_bounds__(NT) grad_planes_kernel(const float* __restrict
     return;
   }
   const float* sr = s + row * lds;
-  const float l = lse[row];
+  const float l = BCE ? 0.f : lse[row];
   const int64_t lab = labels ? labels[row] - c0 : -1;
+  float part = 0.f;
   for (int64_t j = j0 + (int64_t)tid * 4; j < j1; j += (int64_t)NT * 4) {
     float v[4];
     if (VEC && j + 3 < m) {
@@ -779,13 +786,24 @@ __global__ void __launch_bounds__(NT) grad_planes_kernel(const float* __restrict
     float g[4];
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
-      g[c] = j + c < m ? scale * __expf(v[c] - l) : 0.f;  // K padding columns: 0
-      if (j + c == lab && j + c < m) g[c] -= scale;  // a label of another shard may fall into the padding
+      const bool in = j + c < m, hit = j + c == lab && in;  // a label of another shard may fall into the padding
+      if constexpr (BCE) {
+        const float x = v[c] + offset;
+        g[c] = in ? scale * sigmoid_f(x) : 0.f;  // K padding columns: 0
+        if (in) part += softplus_f(x) - (hit ? x : 0.f);
+      } else {
+        g[c] = in ? scale * __expf(v[c] - l) : 0.f;
+      }
+      if (hit) g[c] -= scale;
     }
     bf16x4 h, lw;
     split_bf16x4_pk(make_float4(g[0], g[1], g[2], g[3]), h, lw);
     *reinterpret_cast<bf16x4*>(hi + j) = h;
     *reinterpret_cast<bf16x4*>(lo + j) = lw;
+  }
+  if constexpr (BCE) {
+    part = block_sum<NT>(part, red);
+    if (tid == 0) loss_part[row * gridDim.x + blockIdx.x] = part;
   }
 }
 
@@ -810,6 +828,34 @@ extern "C" int kge_softmax_grad_planes(const float* s, int64_t lds, int64_t n, i
     else
       grad_planes_kernel<false><<<grid, dim3(NT), 0, st>>>(sp, lds, (int)n_here, (int)m, c0, lp, lse + r0, scale,
                                                            planes + r0 * ld, ld);
+    KGE_CHECK_LAUNCH();
+  }
+  return 0;
+}
+
+extern "C" int64_t kge_grad_planes_chunks(int64_t ld) { return ld <= 0 ? 0 : (ld + GP_CH - 1) / GP_CH; }
+
+extern "C" int kge_bce_grad_planes(const float* s, int64_t lds, int64_t n, int64_t n_pad, int64_t m, int64_t c0,
+                                   const int64_t* labels, float offset, float scale, float* planes, int64_t ld,
+                                   float* loss_part, void* stream) {
+  KGE_REQUIRE(n >= 0 && n_pad >= n && n_pad < (1LL << 31) && m > 0 && m < (1LL << 31) && lds >= m);
+  KGE_REQUIRE(s && planes && ld >= m && planes != s && (loss_part || n == 0));
+  if (ld % 32 != 0 || !aligned16(planes)) return KGE_ERR_ALIGN;
+  if (n_pad == 0) return 0;
+  hipStream_t st = as_stream(stream);
+  const int64_t chunks = kge_grad_planes_chunks(ld);
+  for (int64_t r0 = 0; r0 < n_pad; r0 += 65535) {  // grid.y carries the rows, as in kge_softmax_grad_planes
+    const int64_t rows = std::min<int64_t>(65535, n_pad - r0);
+    const int64_t n_here = std::max<int64_t>(0, std::min<int64_t>(n - r0, rows));
+    const dim3 grid((unsigned)chunks, (unsigned)rows);
+    const float* sp = s + r0 * lds;
+    const int64_t* lp = labels ? labels + r0 : nullptr;
+    if (lds % 4 == 0 && aligned16(s))
+      grad_planes_kernel<true, true><<<grid, dim3(NT), 0, st>>>(sp, lds, (int)n_here, (int)m, c0, lp, nullptr, scale,
+                                                                planes + r0 * ld, ld, offset, loss_part + r0 * chunks);
+    else
+      grad_planes_kernel<false, true><<<grid, dim3(NT), 0, st>>>(sp, lds, (int)n_here, (int)m, c0, lp, nullptr, scale,
+                                                                 planes + r0 * ld, ld, offset, loss_part + r0 * chunks);
     KGE_CHECK_LAUNCH();
   }
   return 0;

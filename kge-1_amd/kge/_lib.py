@@ -108,6 +108,8 @@ SIGNATURES = {
     "kge_softmax_row_stats": ([_P, _I64, _I64, _I64, _I64, _P, _P, _P, _P, _P], _I),
     "kge_softmax_grad": ([_P, _I64, _I64, _I64, _I64, _P, _P, _F, _P, _I64, _P], _I),
     "kge_softmax_grad_planes": ([_P, _I64, _I64, _I64, _I64, _I64, _P, _P, _F, _P, _I64, _P], _I),
+    "kge_grad_planes_chunks": ([_I64], _I64),
+    "kge_bce_grad_planes": ([_P, _I64, _I64, _I64, _I64, _I64, _P, _F, _F, _P, _I64, _P, _P], _I),
 }
 
 _lib: Optional[ctypes.CDLL] = None
@@ -793,6 +795,22 @@ def softmax_grad_planes(s, c0, labels, lse, scale):
     _check(lib().kge_softmax_grad_planes(ptr(s), rows(s), n, n_pad, m, int(c0), ptr(labels), ptr(lse), float(scale),
                                          ptr(buf), ld, stream()), "kge_softmax_grad_planes")
     return GradPlanes(buf, n, m)
+
+
+def bce_grad_planes(s, c0, labels, offset, scale):
+    """Binary cross entropy with logits on s + offset against the one-hot rows whose hot column is
+    labels[i] - c0 (when it lies in this block): returns (sum of the block's losses as a 0-dim
+    float64 tensor, unscaled; GradPlanes of G = scale * (sigmoid(s + offset) - y)) -- the row-shard
+    form of the bce loss (kge_bce_grad_planes; any row length)."""
+    labels = idx64(labels)
+    n, m = s.shape
+    n_pad, ld = planes_layout(n, m)
+    buf = torch.empty(n_pad, ld, device=s.device, dtype=torch.float32)
+    chunks = int(lib().kge_grad_planes_chunks(ld))
+    part = torch.empty(n, chunks, device=s.device, dtype=torch.float32)
+    _check(lib().kge_bce_grad_planes(ptr(s), rows(s), n, n_pad, m, int(c0), ptr(labels), float(offset), float(scale),
+                                     ptr(buf), ld, ptr(part), stream()), "kge_bce_grad_planes")
+    return part.double().sum(), GradPlanes(buf, n, m)
 
 
 def softmax_kl(s, l_ptr, l_col, smoothing, scale, g=None, loss=None):

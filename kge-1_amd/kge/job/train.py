@@ -715,7 +715,8 @@ class TrainingJob1vsAll(TrainingJob):
 class ShardedTraining1vsAll:
     """TrainingJob1vsAll over an entity table row-sharded across the processes of a
     torch.distributed world (one per GPU; kge.sharded.RowShardedScorer.train_1vsall_global):
-    vocab-parallel softmax cross entropy, no score or gradient matrix on the link.
+    vocab-parallel softmax cross entropy (train.loss kl) or per-shard binary cross entropy (bce), no
+    score or gradient matrix on the link.
 
     Every rank steps through the same global batches (the batch order is broadcast from
     rank 0) and HOLDS only rows [lo, hi) of the entity table: the model's entity embedder is
@@ -731,8 +732,12 @@ class ShardedTraining1vsAll:
 
         from ..sharded import RowShardedScorer, engine_ops_for, shard_bounds
 
-        if not isinstance(job.loss, KLDivWithSoftmaxKgeLoss):
-            raise NotImplementedError("row-sharded 1vsAll training supports train.loss kl only")
+        if isinstance(job.loss, KLDivWithSoftmaxKgeLoss):
+            self.loss = ("kl", 0.0)
+        elif type(job.loss) is BCEWithLogitsKgeLoss and not job.loss._mean:
+            self.loss = ("bce", float(job.loss._offset))  # elementwise: no statistics cross the shards
+        else:
+            raise NotImplementedError("row-sharded 1vsAll training supports train.loss kl and bce")
         if job.model._lookup_tables() is None and job.sharded_ops is None:
             raise NotImplementedError("row-sharded training needs plain lookup embedders and an engine scorer")
         self.job = job
@@ -778,7 +783,8 @@ class ShardedTraining1vsAll:
         triples = host.to(self.job.device)
         t += time.time()
         fwd = -time.time()
-        loss, d_ent, d_rel = self.scorer.train_1vsall_global(triples, host_triples=host if not host.is_cuda else None)
+        loss, d_ent, d_rel = self.scorer.train_1vsall_global(triples, host_triples=host if not host.is_cuda else None,
+                                                             loss=self.loss)
         fwd += time.time()
         self.ent_param.grad = d_ent
         self.rel_param.grad = d_rel

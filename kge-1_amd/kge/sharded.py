@@ -117,6 +117,24 @@ class ExchangePlan:
         self.mine_host = mine
 
 
+def bce_grad_block(s, c0, labels, offset, scale, g):
+    """train.loss bce on one shard's block of a 1vsAll batch, in torch ops (small blocks, and the CPU
+    ops of the gloo tests): g = scale * (sigmoid(s + offset) - y) with y one-hot at column
+    labels[i] - c0 when that falls into the block; returns the block's unscaled loss sum,
+    sum_ij softplus(x_ij) - y_ij x_ij (loss.py:137-158), as a 0-dim float64 tensor."""
+    x = s + offset if offset != 0.0 else s
+    m = s.shape[1]
+    col = labels - c0
+    inside = (col >= 0) & (col < m)
+    colc = col.clamp(0, m - 1).unsqueeze(1)
+    hot = torch.gather(x, 1, colc).squeeze(1)
+    loss = torch.nn.functional.softplus(x).double().sum() - torch.where(inside, hot, torch.zeros_like(hot)).double().sum()
+    out = torch.sigmoid(x) * scale
+    out.scatter_add_(1, colc, torch.where(inside, -scale, 0.0).to(out.dtype).unsqueeze(1))
+    g.copy_(out)
+    return loss
+
+
 class EngineOps:
     """Default compute: libkgescore."""
 
@@ -192,6 +210,13 @@ class EngineOps:
         dq = self.L.score_dot_bwd_q_planes(gp, tab, dq=dq)
         self.L.score_dot_bwd_t_planes(gp, hi, lo, d_tab, accumulate=True)
         return dq
+
+    def bce_grad_planes(self, s, c0, labels, offset, scale):
+        """(unscaled loss sum of this shard's block, gradient planes) of train.loss bce."""
+        return self.L.bce_grad_planes(s, c0, labels, offset, scale)
+
+    def bce_grad(self, s, c0, labels, offset, scale, g):
+        return bce_grad_block(s, c0, labels, offset, scale, g)
 
     def row_stats(self, s, c0, labels):
         return self.L.softmax_row_stats(s, c0, labels)
@@ -488,7 +513,7 @@ class RowShardedScorer:
     #: directions run one after the other (half the live score memory)
     STACK_MAX_ELEMS = 1 << 34
 
-    def train_1vsall_global(self, tr_all: torch.Tensor, host_triples=None):
+    def train_1vsall_global(self, tr_all: torch.Tensor, host_triples=None, loss=("kl", 0.0)):
         """train_1vsall_grads for a global batch [n, 3] that every rank already holds
         identically (the index batch is tiny, so a job hands every rank the whole batch
         instead of gathering slices).  host_triples: the same batch in host memory (a job's
@@ -503,7 +528,16 @@ class RowShardedScorer:
           3. reduce_scatter of the partial dQ = G_k . E_k in the same owner-major layout: every
              owner receives the summed gradients of its own query rows only;
           4. all_reduce of the relation gradient (each query's at its owner).
-        dE_k = G_k^T . Q stays local with the shard."""
+        dE_k = G_k^T . Q stays local with the shard.
+
+        loss = ("bce", offset): train.loss bce (loss.py:137-158, reduction "sum", on scores + offset
+        against the one-hot rows) instead of the softmax cross entropy.  Binary cross entropy
+        couples no columns, so collective 2 is not needed: every shard turns its logits into its
+        slice of G = scale (sigmoid - y) by itself, and one all_reduce of a scalar gives the loss
+        every rank reports."""
+        loss_kind, loss_offset = loss
+        if loss_kind not in ("kl", "bce"):
+            raise ValueError(f"row-sharded 1vsAll loss {loss_kind!r} (kl or bce)")
         n = tr_all.shape[0]
         scale = 1.0 / n
         E_k = self.hi - self.lo
@@ -566,6 +600,18 @@ class RowShardedScorer:
                 logits = self.ops.score_split(q_hi, q_lo, m, tab_w, out=buf[:, :E_k])
             else:
                 logits = self.ops.score(qg, tab_w, out=buf[:, :E_k])
+            if loss_kind == "bce":  # elementwise: the shard's slice of G and of the loss, no exchange
+                if planes:
+                    part, gp = self.ops.bce_grad_planes(logits, self.lo, lab, loss_offset, scale)
+                    del logits, buf
+                    self.ops.score_bwd_planes(gp, q_hi, q_lo, tab_w, self._win(direction, d_ent), dq=dq[r0:r1])
+                    del gp
+                else:
+                    part = self.ops.bce_grad(logits, self.lo, lab, loss_offset, scale, logits)
+                    self.ops.score_bwd(logits, qg, tab_w, dq[r0:r1], self._win(direction, d_ent))
+                    del logits, buf
+                loss += part * scale
+                continue
             # ---- 2. softmax statistics of every shard, one all_gather
             mx, sm, tg = self.ops.row_stats(logits, self.lo, lab)
             st = torch.stack([mx, sm, tg])
@@ -598,6 +644,11 @@ class RowShardedScorer:
         # ---- 4. the replicated relation table's gradient
         all_reduce(d_rel, group=self.group)
         self.collectives_last_step = 3 + len(groups)
+        if loss_kind == "bce":  # the shards' loss shares (the kl loss is formed from gathered statistics)
+            loss = loss.reshape(1)
+            all_reduce(loss, group=self.group)
+            loss = loss.reshape(())
+            self.collectives_last_step = 4
         return loss, d_ent, d_rel  # loss: a 0-dim float64 tensor on the table's device (no host sync)
 
     # ---------------------------------------------------------------- eval

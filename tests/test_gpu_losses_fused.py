@@ -66,6 +66,46 @@ def test_bce_planes_vs_torch_float64(L, n, m, smoothing, offset, csr):
         assert pad.numel() == 0 or float(pad.float().abs().max()) == 0.0
 
 
+@pytest.mark.parametrize("n,m,c0,offset,strided", [
+    (37, 130, 0, 0.0, False), (64, 257, 1000, -2.0, True), (5, 31, 7, 1.5, False), (130, 5000, 20000, 0.5, True),
+    (1, 4, 0, 0.0, False)])
+def test_bce_grad_planes_of_a_row_shard_vs_torch_float64(L, n, m, c0, offset, strided):
+    """kge_bce_grad_planes: one shard's columns [c0, c0 + m) of the 1vsAll bce loss.  Labels that
+    fall outside the shard contribute no hot column there; the block's loss sum and G = scale
+    (sigmoid(s + offset) - y) (hi + lo planes) equal torch's float64; scores stay untouched."""
+    rng = np.random.default_rng(n * 7 + m)
+    sc = (rng.standard_normal((n, m)) * 6).astype(np.float32)
+    sc[0, :4] = [90.0, -90.0, 0.0, 30.0]
+    labels = rng.integers(max(c0 - m, 0), c0 + 2 * m, size=n).astype(np.int64)  # about a third inside
+    labels[0] = c0  # first column, at the extreme score
+    if n > 2:
+        labels[1], labels[2] = c0 + m - 1, c0 + m  # last column / first one past the shard
+    y = np.zeros((n, m))
+    inside = (labels >= c0) & (labels < c0 + m)
+    y[np.nonzero(inside)[0], labels[inside] - c0] = 1.0
+    x = torch.from_numpy(sc).double() + offset
+    yt = torch.from_numpy(y)
+    ref_loss = float(torch.nn.functional.binary_cross_entropy_with_logits(x, yt, reduction="sum"))
+    scale = 1.0 / 4096
+    ref_g = (scale * (torch.sigmoid(x) - yt)).numpy()
+    if strided:  # a column window of a wider score buffer (row stride != m)
+        wide = torch.full((n, m + 24), 7.0, device="cuda")
+        wide[:, 8:8 + m] = torch.from_numpy(sc).cuda()
+        s = wide[:, 8:8 + m]
+    else:
+        s = torch.from_numpy(sc).cuda()
+    before = s.clone()
+    loss, gp = L.bce_grad_planes(s, c0, torch.from_numpy(labels).cuda(), offset, scale)
+    torch.cuda.synchronize()
+    assert loss.dtype == torch.float64 and loss.dim() == 0
+    assert abs(float(loss) - ref_loss) <= 3e-6 * abs(ref_loss)
+    assert torch.equal(s, before)
+    g = (gp.hi[:n, :m].float() + gp.lo[:n, :m].float()).cpu().numpy()
+    assert np.abs(g - ref_g).max() <= 3e-5 * np.abs(ref_g).max()
+    for pad in (gp.hi[:, m:], gp.lo[:, m:], gp.hi[n:], gp.lo[n:]):
+        assert pad.numel() == 0 or float(pad.float().abs().max()) == 0.0
+
+
 @pytest.mark.parametrize("kind,arg", [("margin_ranking", 1.0), ("margin_ranking", 0.25), ("bce", 0.0), ("bce", -3.0)])
 @pytest.mark.parametrize("n,k", [(64, 9), (512, 1025), (3, 1)])
 def test_ns_loss_vs_torch_float64(L, kind, arg, n, k):

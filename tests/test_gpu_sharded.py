@@ -97,10 +97,12 @@ def test_train_1vsall_grads_world1_matches_fused(L, prec, planes):
         dist.destroy_process_group()
 
 
-def test_sharded_jobs_world1_rccl_match_unsharded_jobs(L):
-    """TrainingJob1vsAll and EntityRankingJob with engine.row_sharded on, over an RCCL world
-    of one process (the degenerate single shard, EngineOps = the HIP kernels): the same loss
-    trajectory, tables and ranks as the unsharded jobs from the same start."""
+@pytest.mark.parametrize("train_loss", ["kl", "bce"])
+def test_sharded_jobs_world1_rccl_match_unsharded_jobs(L, train_loss):
+    """TrainingJob1vsAll (train.loss kl, and bce with an offset) and EntityRankingJob with
+    engine.row_sharded on, over an RCCL world of one process (the degenerate single shard,
+    EngineOps = the HIP kernels): the same loss trajectory, tables and ranks as the unsharded
+    jobs from the same start."""
     from kge import Config, Dataset
     from kge.job import EntityRankingJob, TrainingJob
 
@@ -120,6 +122,9 @@ def test_sharded_jobs_world1_rccl_match_unsharded_jobs(L):
             c.set("train.batch_size", 256)
             c.set("train.max_epochs", 2)
             c.set("train.optimizer_args", {"lr": 0.1})
+            if train_loss == "bce":
+                c.set("train.loss", "bce")
+                c.set("train.loss_arg", -3.0)
             c.set("valid.every", 0)
             c.set("eval.batch_size", 100)
             c.set("engine.eval_batch_size", 0)  # the batches of eval.batch_size as they are
@@ -296,6 +301,44 @@ def _c5_rank_shapes(L, EngineOps, RowShardedScorer):
     got = d_ent[cols].double()
     err = ((got - ref_de)[~touched]).abs().max().item() / ref_de.abs().max().item()
     assert err < 1e-4
+
+
+@pytest.mark.parametrize("planes", [True, False])
+def test_row_sharded_bce_step_world1_vs_float64_autograd(L, planes):
+    """train_1vsall_global with loss ("bce", offset) on the engine (gradient planes, or the fp32
+    gradient block) at world size 1 over RCCL: loss and both tables' gradients against autograd of
+    BCEWithLogits(sum) / B on float64 ComplEx scores (train.py:1041-1057 with loss.py:137-158)."""
+    from kge.sharded import EngineOps, RowShardedScorer
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()))
+    dist.init_process_group("nccl", rank=0, world_size=1)
+    try:
+        E, R, B, d, offset = 1517, 11, 96, 64, -1.0
+        torch.manual_seed(3)
+        ent = torch.randn(E, d, device="cuda") * 0.4
+        rel = torch.randn(R, d, device="cuda") * 0.4
+        g = torch.Generator().manual_seed(4)
+        tr = torch.stack([torch.randint(0, E, (B,), generator=g), torch.randint(0, R, (B,), generator=g),
+                          torch.randint(0, E, (B,), generator=g)], 1).cuda()
+        e64, r64 = ent.double().requires_grad_(), rel.double().requires_grad_()
+        ref = 0.0
+        for direction, q_col, lab_col in ((0, 0, 2), (1, 2, 0)):
+            q = complex_q(e64[tr[:, q_col]], r64[tr[:, 1]], direction)
+            y = torch.zeros(B, E, device="cuda", dtype=torch.float64)
+            y[torch.arange(B), tr[:, lab_col]] = 1.0
+            ref = ref + torch.nn.functional.binary_cross_entropy_with_logits(q @ e64.T + offset, y, reduction="sum") / B
+        ref.backward()
+        ref = float(ref.detach())
+        sh = RowShardedScorer(ent, 0, E, E, rel, EngineOps(L.COMPLEX, L.PREC_BF16X3))
+        sh.PLANES_MIN_ELEMS = 0 if planes else 1 << 62
+        loss, d_ent, d_rel = sh.train_1vsall_global(tr, loss=("bce", offset))
+        torch.cuda.synchronize()
+        assert sh.collectives_last_step == 4
+        assert abs(float(loss) - ref) <= 2e-5 * abs(ref)
+        assert float((d_ent.double() - e64.grad).abs().max()) <= 2e-4 * float(e64.grad.abs().max())
+        assert float((d_rel.double() - r64.grad).abs().max()) <= 2e-4 * float(r64.grad.abs().max())
+    finally:
+        dist.destroy_process_group()
 
 
 def _world2_batch():

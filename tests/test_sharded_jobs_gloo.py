@@ -129,7 +129,7 @@ def _lp(table, idx, w, p, weighted):
     return (w / p * (rows ** p * cnt.float().view(-1, 1))).sum() / len(idx)
 
 
-def _worker(rank, world, port, out_q, penalties=None):
+def _worker(rank, world, port, out_q, penalties=None, bce_offset=None):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
@@ -137,6 +137,10 @@ def _worker(rank, world, port, out_q, penalties=None):
         from kge.job import EntityRankingJob, TrainingJob
 
         c = _config()
+        if bce_offset is not None:
+            c.set("train.loss", "bce")
+            c.set("train.loss_arg", bce_offset)
+            c.set("valid.every", 0)
         ds = Dataset(c, None)
         ds._triples = {k: torch.from_numpy(v.astype(np.int32)) for k, v in _splits().items()}
         job = TrainingJob.create(c, ds)
@@ -150,6 +154,13 @@ def _worker(rank, world, port, out_q, penalties=None):
         traces = job.run()
         assert job._sharded is not None and job._sharded.world == world
         lo, hi = job._sharded.lo, job._sharded.hi
+        if bce_offset is not None:
+            assert job._sharded.loss == ("bce", bce_offset) and job._sharded.scorer.collectives_last_step == 4
+            job._sharded.sync_model()
+            out_q.put((rank, [t["avg_loss"] for t in traces],
+                       job.model._entity_embedder._embeddings.weight.detach().numpy().copy(),
+                       job.model._relation_embedder._embeddings.weight.detach().numpy().copy()))
+            return
         if penalties:
             job._sharded.sync_model()
             out_q.put((rank, [t["avg_loss"] for t in traces], [t["avg_penalty"] for t in traces],
@@ -174,7 +185,7 @@ def _worker(rank, world, port, out_q, penalties=None):
         dist.destroy_process_group()
 
 
-def _unsharded_reference(penalties=None):
+def _unsharded_reference(penalties=None, bce_offset=None):
     """The same training run without any sharding, by torch autograd."""
     splits = _splits()
     ent0, rel0 = _tables()
@@ -194,7 +205,13 @@ def _unsharded_reference(penalties=None):
             loss = 0.0
             for direction, e_col, lab_col in ((0, 0, 2), (1, 2, 0)):
                 q = _prep(direction, ent, tr[:, e_col], rel, tr[:, 1])
-                loss = loss + torch.nn.functional.cross_entropy(q @ ent.T, tr[:, lab_col], reduction="sum") / len(tr)
+                if bce_offset is None:
+                    loss = loss + torch.nn.functional.cross_entropy(q @ ent.T, tr[:, lab_col], reduction="sum") / len(tr)
+                else:  # loss.py:137-158: BCEWithLogits(sum) on scores + offset against the one-hot rows
+                    y = torch.zeros(len(tr), E)
+                    y[torch.arange(len(tr)), tr[:, lab_col]] = 1.0
+                    loss = loss + torch.nn.functional.binary_cross_entropy_with_logits(
+                        q @ ent.T + bce_offset, y, reduction="sum") / len(tr)
             if penalties:  # kge_model.py:588-605: subjects, relations, objects
                 (we, pe, ee), (wr, pr, er) = PENALTIES[penalties]
                 pen = (_lp(ent, tr[:, 0], we, pe, ee) + _lp(rel, tr[:, 1], wr, pr, er)
@@ -207,7 +224,7 @@ def _unsharded_reference(penalties=None):
             tot += float(loss.detach()) * len(tr) - (float(pen.detach()) * len(tr) if penalties else 0.0)
         losses.append(tot / len(train))
         pens.append(pen_tot / n_batches)
-        if penalties:
+        if penalties or bce_offset is not None:
             continue
         _, m = K.entity_ranking("complex", ent.detach().double().numpy(), rel.detach().double().numpy(), splits,
                                 eval_split="valid", filter_splits=("train", "valid"), batch_size=7)
@@ -252,6 +269,28 @@ def test_sharded_training_and_eval_jobs_world2_match_unsharded():
             np.testing.assert_array_equal(ranks[k], v, err_msg=k)
         for k, v in ometrics.items():
             assert metrics[k] == pytest.approx(v, rel=1e-5, abs=1e-9), k
+
+
+def test_sharded_training_job_with_bce_world2_matches_unsharded():
+    """train.loss bce (with an offset) through the row-sharded TrainingJob1vsAll: every shard forms
+    its slice of the loss and of the gradient by itself (4 collectives per step, no statistics
+    exchange); loss trajectory and trained tables equal the unsharded autograd run."""
+    world, offset = 2, -2.0
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q, None, offset)) for r in range(world)]
+    for pr in procs:
+        pr.start()
+    res = sorted([q.get(timeout=240) for _ in range(world)], key=lambda x: x[0])
+    for pr in procs:
+        pr.join(timeout=60)
+        assert pr.exitcode == 0
+    ref_losses, _, ref_ent, ref_rel = _unsharded_reference(bce_offset=offset)
+    for rank, losses, ent, rel in res:
+        np.testing.assert_allclose(losses, ref_losses, rtol=1e-5)
+        np.testing.assert_allclose(ent, ref_ent, atol=2e-5)
+        np.testing.assert_allclose(rel, ref_rel, atol=2e-5)
 
 
 @pytest.mark.parametrize("case", sorted(PENALTIES))
