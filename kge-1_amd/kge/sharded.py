@@ -360,6 +360,9 @@ class _Ticket:
 class RowShardedScorer:
     #: smallest [n, E_k] score block whose training gradient is kept as bf16 planes
     PLANES_MIN_ELEMS = 1 << 25
+    #: the same for train.loss bce (whose fp32 gradient is formed by torch ops: 0.95 ms per step at
+    #: 2,048 x 14,541 against 0.53 ms through the planes)
+    BCE_PLANES_MIN_ELEMS = 1 << 20
 
     def __init__(self, ent_shard: torch.Tensor, lo: int, hi: int, num_entities: int, rel: torch.Tensor, ops,
                  group=None):
@@ -593,7 +596,10 @@ class RowShardedScorer:
             # gradient planes pay off once the GEMMs dominate the step (a few more launches and
             # one more [m, E_k] buffer: at 1,024 x 14,541 the fp32 path is 10 % faster, at
             # 1,024 x 574,311 the planes are 16 % faster)
-            planes = (m * E_k >= self.PLANES_MIN_ELEMS and getattr(self.ops, "train_planes_ok", None) is not None
+            # (bce has no fused fp32-gradient kernel: its fp32 path is a dozen elementwise torch
+            # passes over the block, so the one-pass planes kernel takes over much earlier)
+            min_elems = self.PLANES_MIN_ELEMS if loss_kind == "kl" else min(self.PLANES_MIN_ELEMS, self.BCE_PLANES_MIN_ELEMS)
+            planes = (m * E_k >= min_elems and getattr(self.ops, "train_planes_ok", None) is not None
                       and self.ops.train_planes_ok(self.ent, direction))
             if planes:
                 q_hi, q_lo = self.ops.split_padded(qg)

@@ -330,7 +330,7 @@ def test_row_sharded_bce_step_world1_vs_float64_autograd(L, planes):
         ref.backward()
         ref = float(ref.detach())
         sh = RowShardedScorer(ent, 0, E, E, rel, EngineOps(L.COMPLEX, L.PREC_BF16X3))
-        sh.PLANES_MIN_ELEMS = 0 if planes else 1 << 62
+        sh.PLANES_MIN_ELEMS = sh.BCE_PLANES_MIN_ELEMS = 0 if planes else 1 << 62
         loss, d_ent, d_rel = sh.train_1vsall_global(tr, loss=("bce", offset))
         torch.cuda.synchronize()
         assert sh.collectives_last_step == 4
