@@ -358,7 +358,7 @@ def _world2_batch():
     return E, R, d, B, ent, rel, tr
 
 
-def _world2_worker(rank, world, port, planes, out_q):
+def _world2_worker(rank, world, port, planes, out_q, loss=("kl", 0.0)):
     """One of two ranks sharing the GPU; collectives over gloo (device tensors staged through host
     memory by kge.sharded), compute on the engine."""
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
@@ -371,10 +371,10 @@ def _world2_worker(rank, world, port, planes, out_q):
         lo, hi = shard_bounds(E, world, rank)
         sc = RowShardedScorer(ent[lo:hi].cuda().contiguous(), lo, hi, E, rel.cuda(),
                               EngineOps(_lib.COMPLEX, _lib.PREC_BF16X3))
-        if planes:
-            sc.PLANES_MIN_ELEMS = 0
-        loss, d_ent, d_rel = sc.train_1vsall_global(tr.cuda())
-        out_q.put((rank, lo, hi, float(loss), d_ent.cpu().numpy(), d_rel.cpu().numpy()))
+        sc.PLANES_MIN_ELEMS = sc.BCE_PLANES_MIN_ELEMS = 0 if planes else 1 << 62
+        value, d_ent, d_rel = sc.train_1vsall_global(tr.cuda(), loss=loss)
+        assert sc.collectives_last_step == 4
+        out_q.put((rank, lo, hi, float(value), d_ent.cpu().numpy(), d_rel.cpu().numpy()))
     finally:
         dist.destroy_process_group()
 
@@ -419,6 +419,42 @@ def test_train_1vsall_world2_on_the_engine_matches_fused(L, planes):
     ref_e, ref_r = we.grad.cpu().numpy(), wr.grad.cpu().numpy()
     for rank, lo, hi, l2, d_ent, d_rel in res:
         assert l2 == pytest.approx(loss.item(), rel=1e-5)
+        assert np.abs(d_ent - ref_e[lo:hi]).max() <= 1e-4 * np.abs(ref_e).max(), rank
+        assert np.abs(d_rel - ref_r).max() <= 1e-4 * np.abs(ref_r).max(), rank
+
+
+@pytest.mark.parametrize("planes", [True, False], ids=["planes", "fp32_block"])
+def test_train_1vsall_bce_world2_on_the_engine_vs_float64_autograd(L, planes):
+    """train.loss bce (offset -1.5) over TWO ranks on the engine's kernels (both on this GPU,
+    collectives over gloo through host memory): each rank's share of the loss summed by the final
+    all_reduce, its shard of dE and the relation gradient against float64 autograd of
+    BCEWithLogits(sum) / B on the whole table -- with hot columns that belong to the other shard,
+    also right past a shard's end (the K padding of its gradient planes)."""
+    import torch.multiprocessing as mp
+
+    world, offset = 2, -1.5
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_world2_worker, args=(r, world, port, planes, q, ("bce", offset))) for r in range(world)]
+    for pr in procs:
+        pr.start()
+    res = sorted([q.get(timeout=240) for _ in range(world)], key=lambda x: x[0])
+    for pr in procs:
+        pr.join(timeout=60)
+        assert pr.exitcode == 0
+    E, R, d, B, ent, rel, tr = _world2_batch()
+    e64, r64 = ent.double().requires_grad_(), rel.double().requires_grad_()
+    ref = 0.0
+    for direction, q_col, lab_col in ((0, 0, 2), (1, 2, 0)):
+        qq = complex_q(e64[tr[:, q_col]], r64[tr[:, 1]], direction)
+        y = torch.zeros(B, E, dtype=torch.float64)
+        y[torch.arange(B), tr[:, lab_col]] = 1.0
+        ref = ref + torch.nn.functional.binary_cross_entropy_with_logits(qq @ e64.T + offset, y, reduction="sum") / B
+    ref.backward()
+    ref_e, ref_r = e64.grad.numpy(), r64.grad.numpy()
+    for rank, lo, hi, value, d_ent, d_rel in res:
+        assert value == pytest.approx(float(ref.detach()), rel=1e-5)
         assert np.abs(d_ent - ref_e[lo:hi]).max() <= 1e-4 * np.abs(ref_e).max(), rank
         assert np.abs(d_rel - ref_r).max() <= 1e-4 * np.abs(ref_r).max(), rank
 
