@@ -400,6 +400,29 @@ def test_row_sharded_on_is_refused_by_the_training_types_that_do_not_shard(train
         dist.destroy_process_group()
 
 
+@pytest.mark.parametrize("train_loss", ["bce_mean", "soft_margin"])
+def test_row_sharded_1vsall_refuses_losses_it_cannot_split_by_rows(train_loss):
+    """Row-sharded 1vsAll training serves kl and bce; any other train.loss fails loudly when the
+    sharded step is set up instead of training on a wrong objective."""
+    from kge import Dataset
+    from kge.job import TrainingJob
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()))
+    dist.init_process_group("gloo", rank=0, world_size=1)
+    try:
+        c = _config()
+        c.set("train.loss", train_loss)
+        c.set("engine.row_sharded", "on")
+        ds = Dataset(c, None)
+        ds._triples = {k: torch.from_numpy(v.astype(np.int32)) for k, v in _splits().items()}
+        job = TrainingJob.create(c, ds)
+        job.sharded_ops = JobOps()
+        with pytest.raises(NotImplementedError, match="kl and bce"):
+            job._prepare()
+    finally:
+        dist.destroy_process_group()
+
+
 def _worker_shard_only(rank, world, port, out_q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
