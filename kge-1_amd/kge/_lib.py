@@ -810,7 +810,7 @@ def bce_grad_planes(s, c0, labels, offset, scale):
     part = torch.empty(n, chunks, device=s.device, dtype=torch.float32)
     _check(lib().kge_bce_grad_planes(ptr(s), rows(s), n, n_pad, m, int(c0), ptr(labels), float(offset), float(scale),
                                      ptr(buf), ld, ptr(part), stream()), "kge_bce_grad_planes")
-    return part.double().sum(), GradPlanes(buf, n, m)
+    return part.sum(dtype=torch.float64), GradPlanes(buf, n, m)
 
 
 def softmax_kl(s, l_ptr, l_col, smoothing, scale, g=None, loss=None):
